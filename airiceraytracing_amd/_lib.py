@@ -1,0 +1,206 @@
+"""ctypes binding of libairice.so (include/airice.h).
+
+The product path: every compute call goes through the HIP library.  There is no
+CPU fallback -- if ``libairice.so`` is missing or cannot be loaded, import of the
+compute entry points raises :class:`AirIceLibraryError`.
+"""
+from __future__ import annotations
+
+import ctypes
+import gzip
+import os
+import subprocess
+
+import numpy as np
+
+PKG_DIR = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(PKG_DIR, "libairice.so")
+CSRC_DIR = os.path.join(PKG_DIR, "csrc")
+DATA_DIR = os.path.join(PKG_DIR, "data")
+
+AIRICE_OK = 0
+VARIANT_MULTIRAY = 0
+VARIANT_PYWRAPPER = 1
+
+SOLVE_NONFINITE_END = 1
+SOLVE_BAD_BRACKET = 2
+SOLVE_STALE_MID = 4
+SOLVE_PROBED = 8
+SOLVE_MAXITER = 16
+SOLVE_NO_AIR_LAYER = 32
+
+TABLE_COLUMNS = 11
+RAY_FIELDS = 18
+SOLVE_FIELDS = 17
+PYSOLVE_FIELDS = 15
+HDTIP_FIELDS = 9
+
+
+class AirIceLibraryError(RuntimeError):
+    pass
+
+
+class Medium(ctypes.Structure):
+    """airice_medium (include/airice.h)."""
+
+    _fields_ = [
+        ("atmlay_cm", ctypes.c_double * 5),
+        ("abc", (ctypes.c_double * 3) * 5),
+        ("B_air", ctypes.c_double * 5),
+        ("C_air", ctypes.c_double * 5),
+        ("N0", ctypes.c_double),
+        ("max_layers", ctypes.c_int32),
+        ("n_points", ctypes.c_int32),
+        ("A_air", ctypes.c_double),
+        ("A_ice", ctypes.c_double),
+        ("B_ice", ctypes.c_double),
+        ("C_ice", ctypes.c_double),
+        ("pi", ctypes.c_double),
+    ]
+
+
+class Grid(ctypes.Structure):
+    """airice_grid (include/airice.h)."""
+
+    _fields_ = [
+        ("start_height", ctypes.c_double),
+        ("stop_height", ctypes.c_double),
+        ("height_step", ctypes.c_double),
+        ("height_steps", ctypes.c_int32),
+        ("start_angle", ctypes.c_double),
+        ("stop_angle", ctypes.c_double),
+        ("angle_step", ctypes.c_double),
+        ("angle_steps", ctypes.c_int32),
+        ("depth_m", ctypes.c_double),
+        ("ice_m", ctypes.c_double),
+        ("in_ice", ctypes.c_int32),
+    ]
+
+    @property
+    def n_rays(self) -> int:
+        return int(self.height_steps) * int(self.angle_steps)
+
+
+# Every symbol include/airice.h declares (checked by tests/test_capi.py).
+EXPORTED_SYMBOLS = (
+    "airice_last_error", "airice_version", "airice_atmosphere_load", "airice_atmosphere_parse",
+    "airice_nz_air", "airice_nz_ice", "airice_grid_init", "airice_table_launch",
+    "airice_table_host", "airice_rays_launch", "airice_solve_launch", "airice_solve_host",
+    "airice_hdtip_launch", "airice_trace_ice_to_air_launch", "airice_trace_ice_to_air_host",
+    "Py_TraceIceToAir", "airice_device_count", "airice_set_device", "airice_malloc",
+    "airice_free", "airice_memcpy_h2d", "airice_memcpy_d2h", "airice_synchronize",
+)
+
+
+def build(force: bool = False) -> str:
+    """Compile libairice.so for gfx950 with hipcc (csrc/Makefile)."""
+    args = ["make", "-s", "-C", CSRC_DIR]
+    if force:
+        args.append("-B")
+    subprocess.run(args, check=True)
+    return LIB_PATH
+
+
+_lib = None
+
+
+def lib() -> ctypes.CDLL:
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise AirIceLibraryError(
+            f"{LIB_PATH} not found: build it with __graft_entry__.build() or "
+            f"'make -C {CSRC_DIR}' (no CPU fallback exists)")
+    # One HIP runtime per process: torch bundles its own libamdhip64 (SONAME
+    # libamdhip64.so.7).  Loading torch first makes libairice.so's NEEDED entry resolve
+    # to that copy; loading libairice.so first would pull /opt/rocm's copy in beside
+    # torch's and torch.cuda would then see no device.
+    try:
+        import torch  # noqa: F401
+    except ImportError:  # plain ctypes users (the Py_TraceIceToAir drop-in) need no torch
+        pass
+    try:
+        L = ctypes.CDLL(LIB_PATH)
+    except OSError as e:  # pragma: no cover - depends on the box
+        raise AirIceLibraryError(f"cannot load {LIB_PATH}: {e}") from e
+    D, I, P, S = ctypes.c_double, ctypes.c_int, ctypes.c_void_p, ctypes.c_size_t
+    M, G = ctypes.POINTER(Medium), ctypes.POINTER(Grid)
+    sig = {
+        "airice_last_error": ([], ctypes.c_char_p),
+        "airice_version": ([], ctypes.c_char_p),
+        "airice_atmosphere_load": ([ctypes.c_char_p, I, M], I),
+        "airice_atmosphere_parse": ([ctypes.c_char_p, S, I, M], I),
+        "airice_nz_air": ([M, D], D),
+        "airice_nz_ice": ([M, D], D),
+        "airice_grid_init": ([G, D, D, D, D, D, D], I),
+        "airice_table_launch": ([M, G, ctypes.c_int32, ctypes.c_int32, P, P, S, P], I),
+        "airice_table_host": ([M, G, ctypes.c_int32, ctypes.c_int32, P, P, S], I),
+        "airice_rays_launch": ([M, P, P, D, D, ctypes.c_int32, S, P, S, P], I),
+        "airice_solve_launch": ([M, I, D, P, P, P, P, S, P, S, P, P], I),
+        "airice_solve_host": ([M, I, D, P, P, P, P, S, P, S, P], I),
+        "airice_hdtip_launch": ([M, P, P, P, D, S, P, S, P, P], I),
+        "airice_trace_ice_to_air_launch": ([M, P, P, P, P, S, P, P], I),
+        "airice_trace_ice_to_air_host": ([M, P, P, P, P, S, P], I),
+        "Py_TraceIceToAir": ([D, D, D, D, ctypes.POINTER(D)], None),
+        "airice_device_count": ([ctypes.POINTER(I)], I),
+        "airice_set_device": ([I], I),
+        "airice_malloc": ([ctypes.POINTER(P), S], I),
+        "airice_free": ([P], I),
+        "airice_memcpy_h2d": ([P, P, S], I),
+        "airice_memcpy_d2h": ([P, P, S], I),
+        "airice_synchronize": ([], I),
+    }
+    for name, (args, res) in sig.items():
+        fn = getattr(L, name)
+        fn.argtypes = args
+        fn.restype = res
+    _lib = L
+    return L
+
+
+def check(rc: int, what: str) -> None:
+    if rc != AIRICE_OK:
+        msg = lib().airice_last_error().decode(errors="replace")
+        raise AirIceLibraryError(f"{what} failed (rc={rc}): {msg}")
+
+
+def ptr(a) -> ctypes.c_void_p | None:
+    """Host numpy array or device tensor -> void*."""
+    if a is None:
+        return None
+    if isinstance(a, np.ndarray):
+        return a.ctypes.data_as(ctypes.c_void_p)
+    if hasattr(a, "data_ptr"):
+        return ctypes.c_void_p(a.data_ptr())
+    if isinstance(a, int):
+        return ctypes.c_void_p(a)
+    raise TypeError(f"cannot take a pointer of {type(a)!r}")
+
+
+def default_atmosphere_path() -> str:
+    """Atmosphere.dat lookup: $AIRICE_ATMOSPHERE, ./Atmosphere.dat (the reference reads the
+    working directory, MultiRayAirIceRefraction.cc:27), then the bundled GDAS file."""
+    env = os.environ.get("AIRICE_ATMOSPHERE")
+    if env and os.path.exists(env):
+        return env
+    if os.path.exists("Atmosphere.dat"):
+        return os.path.abspath("Atmosphere.dat")
+    return os.path.join(DATA_DIR, "Atmosphere.dat.gz")
+
+
+def read_atmosphere_text(path: str | None = None) -> bytes:
+    path = path or default_atmosphere_path()
+    with open(path, "rb") as f:
+        data = f.read()
+    if path.endswith(".gz"):
+        data = gzip.decompress(data)
+    return data
+
+
+def load_medium(path: str | None = None, variant: int = VARIANT_MULTIRAY) -> Medium:
+    text = read_atmosphere_text(path)
+    m = Medium()
+    check(lib().airice_atmosphere_parse(text, len(text), variant, ctypes.byref(m)),
+          "airice_atmosphere_parse")
+    return m

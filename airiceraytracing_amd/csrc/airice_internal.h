@@ -1,0 +1,34 @@
+// airice_internal.h -- host-side internals shared by the runtime and the launchers.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include "airice.h"
+#include "airice_device.hpp"
+
+namespace airice {
+
+// Kernel-argument medium for one variant (pi) built from the parsed medium; the
+// layer-boundary endpoints are evaluated here, on the host, once.
+int build_dev_medium(const airice_medium* m, int variant, DevMedium* out);
+// Batch-uniform ice endpoints: ice height ice_h (m) and antenna depth rx_depth (m, >= 0).
+void build_ice_consts(const DevMedium& M, double ice_h, double rx_depth, IceConsts* out);
+
+Endpoint host_air_endpoint(const DevMedium& M, double x);
+Endpoint host_ice_endpoint(const DevMedium& M, double x);
+
+int launch_table(const DevMedium& M, const IceConsts& I, const airice_grid* g, int row_begin,
+                 int row_count, float* d_table, double* d_full, size_t ld, hipStream_t st);
+int launch_rays(const DevMedium& M, const IceConsts& I, const double* launch, const double* txh,
+                int in_ice, size_t n, double* out, size_t ld, hipStream_t st);
+int launch_solve(const DevMedium& M, const IceConsts& I, int variant, const double* txh,
+                 const double* dist, const double* depth, const double* thr, size_t n,
+                 double* out, size_t ld, uint8_t* status, hipStream_t st);
+int launch_hdtip(const DevMedium& M, const IceConsts& I, const double* src, const double* dist,
+                 const double* depth, double ice_cm, size_t n, double* out, size_t ld,
+                 uint8_t* ok, hipStream_t st);
+int launch_trace(const DevMedium& M, const IceConsts& I, const double* depth, const double* ice,
+                 const double* txh, const double* dist, size_t n, double* out10, hipStream_t st);
+
+void set_error(const char* fmt, ...);
+
+}  // namespace airice

@@ -1,0 +1,552 @@
+// airice_runtime.cpp -- host runtime of libairice.so: GDAS atmosphere ingestion,
+// medium/grid set-up, device bookkeeping and the C-ABI entry points (include/airice.h).
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <fstream>
+#include <mutex>
+#include <sstream>
+#include <string>
+#include <vector>
+
+#include "airice.h"
+#include "airice_internal.h"
+
+namespace airice {
+
+static thread_local char g_err[512] = "";
+
+void set_error(const char* fmt, ...) {
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(g_err, sizeof(g_err), fmt, ap);
+  va_end(ap);
+}
+
+static double variant_pi(int variant) {
+  // MultiRayAirIceRefraction.h:29 / RayTracingFunctions.h:26 vs pythonwrapper AirIceRayTracing.h:25
+  return variant == AIRICE_VARIANT_PYWRAPPER ? 4.0 * std::atan(1.0) : 3.1415927;
+}
+
+// Natural cubic spline through (xs, ys) evaluated at x: second-derivative system
+// solved by symmetric-tridiagonal LDL^T, then the cubic on the bracketing interval
+// (the algorithm of gsl_interp_cspline, which the reference uses for n(h=0) only).
+static double natural_spline_at(const std::vector<double>& xs, const std::vector<double>& ys,
+                                 double x) {
+  const size_t n = xs.size();
+  const size_t m = n - 2;  // interior unknowns
+  std::vector<double> c(n, 0.0), rhs(m), dg(m), od(m);
+  for (size_t i = 0; i < m; ++i) {
+    const double h0 = xs[i + 1] - xs[i], h1 = xs[i + 2] - xs[i + 1];
+    const double g0 = (h0 != 0.0) ? 1.0 / h0 : 0.0;
+    const double g1 = (h1 != 0.0) ? 1.0 / h1 : 0.0;
+    od[i] = h1;
+    dg[i] = 2.0 * (h1 + h0);
+    rhs[i] = 3.0 * ((ys[i + 2] - ys[i + 1]) * g1 - (ys[i + 1] - ys[i]) * g0);
+  }
+  if (m == 1) {
+    c[1] = rhs[0] / dg[0];
+  } else {
+    std::vector<double> piv(m), lo(m), z(m);
+    piv[0] = dg[0];
+    lo[0] = od[0] / piv[0];
+    for (size_t i = 1; i + 1 < m; ++i) {
+      piv[i] = dg[i] - od[i - 1] * lo[i - 1];
+      lo[i] = od[i] / piv[i];
+    }
+    piv[m - 1] = dg[m - 1] - od[m - 2] * lo[m - 2];
+    z[0] = rhs[0];
+    for (size_t i = 1; i < m; ++i) z[i] = rhs[i] - lo[i - 1] * z[i - 1];
+    for (size_t i = 0; i < m; ++i) z[i] = z[i] / piv[i];
+    c[m] = z[m - 1];
+    for (size_t k = m - 1; k-- > 0;) c[k + 1] = z[k] - lo[k] * c[k + 2];
+  }
+  size_t a = 0, b = n - 1;
+  while (b > a + 1) {
+    const size_t mid = (a + b) / 2;
+    if (xs[mid] > x) b = mid; else a = mid;
+  }
+  const double dx = xs[a + 1] - xs[a];
+  if (!(dx > 0.0)) return NAN;
+  const double dy = ys[a + 1] - ys[a];
+  const double t = x - xs[a];
+  const double bi = (dy / dx) - dx * (c[a + 1] + 2.0 * c[a]) / 3.0;
+  const double di = (c[a + 1] - c[a]) / (3.0 * dx);
+  return ys[a] + t * (bi + t * (c[a] + t * di));
+}
+
+// GDAS Atmosphere.dat ingestion with the reference's stream semantics
+// (readATMpar .cc:24-71, readnhFromFile .cc:73-147, FillInAirRefractiveIndex .cc:193-213).
+static int parse_gdas(const std::string& text, airice_medium* m) {
+  std::memset(m, 0, sizeof(*m));
+  m->A_air = 1.00;
+  m->A_ice = 1.78;
+  m->B_ice = -0.43;
+  m->C_ice = 0.0132;
+  {
+    std::istringstream in(text);
+    std::string line;
+    int row = 0;
+    double v[5] = {0, 0, 0, 0, 0};
+    while (std::getline(in, line)) {
+      if (row < 4) in >> v[0] >> v[1] >> v[2] >> v[3] >> v[4];
+      if (row == 0) for (int i = 0; i < 5; ++i) m->atmlay_cm[i] = v[i];
+      if (row >= 1 && row <= 3) for (int i = 0; i < 5; ++i) m->abc[i][row - 1] = v[i];
+      ++row;
+    }
+    for (int k = 0; k < 3; ++k) m->abc[4][k] = m->abc[3][k];
+    m->atmlay_cm[4] = 150000 * 100;
+  }
+  std::vector<double> hs, ns;
+  int groups = 0;
+  {
+    std::istringstream in(text);
+    for (int i = 0; i < 5; ++i) in.ignore(256, '\n');
+    std::string line;
+    int layer = 0;
+    double h = 0, nv = 0;
+    while (std::getline(in, line)) {
+      in >> h >> nv;  // at EOF the last pair is seen twice (removed below, .cc:137-140)
+      if (h > -1) {
+        hs.push_back(h);
+        ns.push_back(nv);
+        if (h * 100 >= m->atmlay_cm[layer < 4 ? layer : 4]) {
+          if (layer > 0) ++groups;
+          ++layer;
+        }
+      }
+    }
+    if (layer > 0) ++groups;
+  }
+  if (groups < 1 || hs.size() < 4) {
+    set_error("atmosphere: no refractive-index profile found");
+    return AIRICE_EIO;
+  }
+  hs.pop_back();
+  ns.pop_back();
+  m->max_layers = groups + 1;
+  m->n_points = (int32_t)hs.size();
+  if (m->max_layers > kMaxLayers) {
+    set_error("atmosphere: %d layers exceed the 5 ATMLAY bounds", m->max_layers);
+    return AIRICE_EINVAL;
+  }
+  m->N0 = natural_spline_at(hs, ns, 0.0);
+  double N0 = 0;
+  for (int il = 0; il < 5; ++il) {
+    const double hlow = m->atmlay_cm[il] / 100;
+    m->C_air[il] = 1.0 / (m->abc[il][2] / 100);
+    if (il > 0) N0 = m->A_air + m->B_air[il - 1] * std::exp(-hlow * m->C_air[il - 1]);
+    if (il == 0) N0 = m->N0;
+    m->B_air[il] = ((N0 - 1) / std::exp(-hlow * m->C_air[il]));
+  }
+  return AIRICE_OK;
+}
+
+static int host_air_layer(const DevMedium& M, double zabs) {
+  int which = 0;
+  for (int l = 0; l < M.ml - 1; ++l) {
+    if (zabs < M.atm[l + 1] && zabs >= M.atm[l]) {
+      which = l;
+      break;
+    }
+  }
+  if (zabs >= M.atm[M.ml - 1]) which = M.ml - 1;
+  return which;
+}
+
+Endpoint host_air_endpoint(const DevMedium& M, double x) {
+  Endpoint p;
+  const double zabs = std::fabs(x);
+  const int l = host_air_layer(M, zabs);
+  p.x = x;
+  p.B = M.B[l];
+  p.C = M.negC[l];
+  const double eabs = std::exp(p.C * zabs);
+  p.n = M.A_air + p.B * eabs;
+  p.e = x >= 0.0 ? eabs : std::exp(p.C * x);
+  p.y = x >= 0.0 ? p.n : M.A_air + p.B * p.e;
+  p.e2 = std::exp(2 * p.C * x);
+  return p;
+}
+
+Endpoint host_ice_endpoint(const DevMedium& M, double x) {
+  Endpoint p;
+  const double zabs = std::fabs(x);
+  p.x = x;
+  p.B = M.B_ice;
+  p.C = M.negC_ice;
+  const double eabs = std::exp(p.C * zabs);
+  p.n = M.A_ice + p.B * eabs;
+  p.e = x >= 0.0 ? eabs : std::exp(p.C * x);
+  p.y = x >= 0.0 ? p.n : M.A_ice + p.B * p.e;
+  p.e2 = std::exp(2 * p.C * x);
+  return p;
+}
+
+int build_dev_medium(const airice_medium* m, int variant, DevMedium* out) {
+  if (m == nullptr || out == nullptr) {
+    set_error("null medium");
+    return AIRICE_EINVAL;
+  }
+  if (m->max_layers < 1 || m->max_layers > kMaxLayers) {
+    set_error("medium not initialised (max_layers=%d)", m->max_layers);
+    return AIRICE_EINVAL;
+  }
+  DevMedium& M = *out;
+  std::memset(&M, 0, sizeof(M));
+  const double pi = variant_pi(variant);
+  for (int i = 0; i < 5; ++i) {
+    M.atm[i] = m->atmlay_cm[i] / 100;
+    M.B[i] = m->B_air[i];
+    M.negC[i] = -m->C_air[i];
+  }
+  M.A_air = m->A_air;
+  M.A_ice = m->A_ice;
+  M.B_ice = m->B_ice;
+  M.negC_ice = -m->C_ice;
+  M.d2r = pi / 180.0;
+  M.r2d = 180 / pi;
+  M.ml = m->max_layers;
+  for (int l = 0; l < kMaxLayers; ++l) {
+    M.start[l] = host_air_endpoint(M, M.atm[l + 1] - 0.00001);
+    M.stop[l] = host_air_endpoint(M, M.atm[l]);
+  }
+  return AIRICE_OK;
+}
+
+void build_ice_consts(const DevMedium& M, double ice_h, double rx_depth, IceConsts* out) {
+  out->ice_h = ice_h;
+  out->ice_air = host_air_endpoint(M, ice_h);
+  out->ice0 = host_ice_endpoint(M, 0.0);
+  out->ice_rx = host_ice_endpoint(M, rx_depth);
+  out->n1_over_n2 = out->ice_air.n / out->ice0.n;
+}
+
+}  // namespace airice
+
+using namespace airice;
+
+#define HIP_TRY(expr)                                                          \
+  do {                                                                         \
+    hipError_t e_ = (expr);                                                    \
+    if (e_ != hipSuccess) {                                                    \
+      set_error("%s failed: %s", #expr, hipGetErrorString(e_));                \
+      return AIRICE_EHIP;                                                      \
+    }                                                                          \
+  } while (0)
+
+extern "C" {
+
+const char* airice_last_error(void) { return g_err; }
+const char* airice_version(void) { return "airice-mi355x 0.1.0 (gfx950, fp64)"; }
+
+int airice_atmosphere_parse(const char* text, size_t len, int variant, airice_medium* out) {
+  if (text == nullptr || out == nullptr) {
+    set_error("null argument");
+    return AIRICE_EINVAL;
+  }
+  int rc = parse_gdas(std::string(text, len), out);
+  if (rc == AIRICE_OK) out->pi = variant_pi(variant);
+  return rc;
+}
+
+int airice_atmosphere_load(const char* path, int variant, airice_medium* out) {
+  if (path == nullptr || out == nullptr) {
+    set_error("null argument");
+    return AIRICE_EINVAL;
+  }
+  std::ifstream f(path, std::ios::binary);
+  if (!f.is_open()) {
+    set_error("cannot open atmosphere file '%s'", path);
+    return AIRICE_EIO;
+  }
+  std::stringstream ss;
+  ss << f.rdbuf();
+  const std::string s = ss.str();
+  return airice_atmosphere_parse(s.data(), s.size(), variant, out);
+}
+
+double airice_nz_air(const airice_medium* m, double z) {
+  DevMedium M;
+  if (build_dev_medium(m, AIRICE_VARIANT_MULTIRAY, &M) != AIRICE_OK) return NAN;
+  return host_air_endpoint(M, std::fabs(z)).n;
+}
+
+double airice_nz_ice(const airice_medium* m, double z) {
+  DevMedium M;
+  if (build_dev_medium(m, AIRICE_VARIANT_MULTIRAY, &M) != AIRICE_OK) return NAN;
+  return host_ice_endpoint(M, std::fabs(z)).n;
+}
+
+int airice_grid_init(airice_grid* g, double depth_cm, double ice_cm, double height_step,
+                     double start_angle, double stop_angle, double angle_step) {
+  if (g == nullptr || !(height_step > 0) || !(angle_step > 0) || !(stop_angle >= start_angle)) {
+    set_error("invalid grid arguments");
+    return AIRICE_EINVAL;
+  }
+  // MakeRayTracingTable (.cc:2021-2061)
+  g->in_ice = depth_cm < 0 ? 1 : 0;
+  g->depth_m = depth_cm / 100;
+  g->ice_m = ice_cm / 100;
+  g->start_height = 100000;
+  g->stop_height = g->in_ice ? g->ice_m : g->ice_m + g->depth_m;
+  g->height_step = height_step;
+  g->height_steps = (int32_t)std::floor((g->start_height - g->stop_height) / height_step) + 1;
+  g->start_angle = start_angle;
+  g->stop_angle = stop_angle;
+  g->angle_step = angle_step;
+  g->angle_steps = (int32_t)std::floor((stop_angle - start_angle) / angle_step) + 1;
+  if (g->height_steps < 1 || g->angle_steps < 1) {
+    set_error("empty grid");
+    return AIRICE_EINVAL;
+  }
+  // The reference skips rows with AirTxHeight <= 0 (.cc:2082); such grids are rejected.
+  if (!(g->start_height - g->height_step * (g->height_steps - 1) > 0)) {
+    set_error("grid reaches non-positive Tx heights");
+    return AIRICE_EINVAL;
+  }
+  return AIRICE_OK;
+}
+
+static int table_prepare(const airice_medium* m, const airice_grid* g, int32_t row_begin,
+                         int32_t row_count, size_t ld, DevMedium* M, IceConsts* I) {
+  if (g == nullptr || row_begin < 0 || row_count < 0 ||
+      (int64_t)row_begin + row_count > g->height_steps) {
+    set_error("row range [%d,+%d) outside grid of %d rows", row_begin, row_count,
+              g ? g->height_steps : -1);
+    return AIRICE_EINVAL;
+  }
+  if (ld < (size_t)row_count * (size_t)g->angle_steps) {
+    set_error("ld smaller than the number of rays");
+    return AIRICE_EINVAL;
+  }
+  int rc = build_dev_medium(m, AIRICE_VARIANT_MULTIRAY, M);
+  if (rc) return rc;
+  build_ice_consts(*M, g->stop_height, -g->depth_m, I);
+  return AIRICE_OK;
+}
+
+int airice_table_launch(const airice_medium* m, const airice_grid* g, int32_t row_begin,
+                        int32_t row_count, float* d_table, double* d_full, size_t ld,
+                        void* stream) {
+  DevMedium M;
+  IceConsts I;
+  int rc = table_prepare(m, g, row_begin, row_count, ld, &M, &I);
+  if (rc) return rc;
+  if (d_table == nullptr) {
+    set_error("null table");
+    return AIRICE_EINVAL;
+  }
+  rc = launch_table(M, I, g, row_begin, row_count, d_table, d_full, ld, (hipStream_t)stream);
+  if (rc) set_error("table launch failed: %s", hipGetErrorString(hipGetLastError()));
+  return rc;
+}
+
+int airice_table_host(const airice_medium* m, const airice_grid* g, int32_t row_begin,
+                      int32_t row_count, float* h_table, double* h_full, size_t ld) {
+  DevMedium M;
+  IceConsts I;
+  int rc = table_prepare(m, g, row_begin, row_count, ld, &M, &I);
+  if (rc) return rc;
+  float* dt = nullptr;
+  double* df = nullptr;
+  HIP_TRY(hipMalloc(&dt, sizeof(float) * 11 * ld));
+  if (h_full) HIP_TRY(hipMalloc(&df, sizeof(double) * 18 * ld));
+  rc = launch_table(M, I, g, row_begin, row_count, dt, df, ld, nullptr);
+  if (rc == AIRICE_OK) {
+    HIP_TRY(hipMemcpy(h_table, dt, sizeof(float) * 11 * ld, hipMemcpyDeviceToHost));
+    if (h_full) HIP_TRY(hipMemcpy(h_full, df, sizeof(double) * 18 * ld, hipMemcpyDeviceToHost));
+  }
+  (void)hipFree(dt);
+  if (df) (void)hipFree(df);
+  return rc;
+}
+
+int airice_rays_launch(const airice_medium* m, const double* d_launch, const double* d_txh,
+                       double ice_h_m, double depth_m, int32_t in_ice, size_t n, double* d_out,
+                       size_t ld, void* stream) {
+  DevMedium M;
+  int rc = build_dev_medium(m, AIRICE_VARIANT_MULTIRAY, &M);
+  if (rc) return rc;
+  if (ld < n) {
+    set_error("ld < n");
+    return AIRICE_EINVAL;
+  }
+  IceConsts I;
+  build_ice_consts(M, ice_h_m, -depth_m, &I);
+  return launch_rays(M, I, d_launch, d_txh, in_ice, n, d_out, ld, (hipStream_t)stream);
+}
+
+int airice_solve_launch(const airice_medium* m, int variant, double ice_h_m, const double* d_txh,
+                        const double* d_dist, const double* d_depth,
+                        const double* d_straight_angle, size_t n, double* d_out, size_t ld,
+                        uint8_t* d_status, void* stream) {
+  if (variant != AIRICE_VARIANT_MULTIRAY && variant != AIRICE_VARIANT_PYWRAPPER) {
+    set_error("unknown variant %d", variant);
+    return AIRICE_EINVAL;
+  }
+  if (ld < n) {
+    set_error("ld < n");
+    return AIRICE_EINVAL;
+  }
+  DevMedium M;
+  int rc = build_dev_medium(m, variant, &M);
+  if (rc) return rc;
+  IceConsts I;
+  build_ice_consts(M, ice_h_m, 0.0, &I);
+  return launch_solve(M, I, variant, d_txh, d_dist, d_depth, d_straight_angle, n, d_out, ld,
+                      d_status, (hipStream_t)stream);
+}
+
+int airice_solve_host(const airice_medium* m, int variant, double ice_h_m, const double* txh,
+                      const double* dist, const double* depth, const double* straight_angle,
+                      size_t n, double* out, size_t ld, uint8_t* status) {
+  if (n == 0) return AIRICE_OK;
+  if (ld < n) {
+    set_error("ld < n");
+    return AIRICE_EINVAL;
+  }
+  const int fields = variant == AIRICE_VARIANT_PYWRAPPER ? AIRICE_PYSOLVE_FIELDS : AIRICE_SOLVE_FIELDS;
+  double *dt = nullptr, *dd = nullptr, *dp = nullptr, *dthr = nullptr, *dout = nullptr;
+  uint8_t* dst = nullptr;
+  HIP_TRY(hipMalloc(&dt, sizeof(double) * n));
+  HIP_TRY(hipMalloc(&dd, sizeof(double) * n));
+  HIP_TRY(hipMalloc(&dp, sizeof(double) * n));
+  HIP_TRY(hipMalloc(&dout, sizeof(double) * fields * ld));
+  HIP_TRY(hipMalloc(&dst, n));
+  HIP_TRY(hipMemcpy(dt, txh, sizeof(double) * n, hipMemcpyHostToDevice));
+  HIP_TRY(hipMemcpy(dd, dist, sizeof(double) * n, hipMemcpyHostToDevice));
+  HIP_TRY(hipMemcpy(dp, depth, sizeof(double) * n, hipMemcpyHostToDevice));
+  if (straight_angle != nullptr) {
+    HIP_TRY(hipMalloc(&dthr, sizeof(double) * n));
+    HIP_TRY(hipMemcpy(dthr, straight_angle, sizeof(double) * n, hipMemcpyHostToDevice));
+  }
+  int rc = airice_solve_launch(m, variant, ice_h_m, dt, dd, dp, dthr, n, dout, ld, dst, nullptr);
+  if (rc == AIRICE_OK) {
+    HIP_TRY(hipMemcpy(out, dout, sizeof(double) * fields * ld, hipMemcpyDeviceToHost));
+    if (status) HIP_TRY(hipMemcpy(status, dst, n, hipMemcpyDeviceToHost));
+  }
+  (void)hipFree(dt);
+  (void)hipFree(dd);
+  (void)hipFree(dp);
+  (void)hipFree(dout);
+  (void)hipFree(dst);
+  if (dthr) (void)hipFree(dthr);
+  return rc;
+}
+
+int airice_hdtip_launch(const airice_medium* m, const double* d_src_cm, const double* d_dist_cm,
+                        const double* d_depth_cm, double ice_cm, size_t n, double* d_out,
+                        size_t ld, uint8_t* d_ok, void* stream) {
+  if (ld < n) {
+    set_error("ld < n");
+    return AIRICE_EINVAL;
+  }
+  DevMedium M;
+  int rc = build_dev_medium(m, AIRICE_VARIANT_MULTIRAY, &M);
+  if (rc) return rc;
+  IceConsts I;
+  build_ice_consts(M, ice_cm / 100, 0.0, &I);
+  return launch_hdtip(M, I, d_src_cm, d_dist_cm, d_depth_cm, ice_cm, n, d_out, ld, d_ok,
+                      (hipStream_t)stream);
+}
+
+int airice_trace_ice_to_air_launch(const airice_medium* m, const double* d_depth,
+                                   const double* d_ice, const double* d_txh, const double* d_dist,
+                                   size_t n, double* d_out10, void* stream) {
+  DevMedium M;
+  int rc = build_dev_medium(m, AIRICE_VARIANT_PYWRAPPER, &M);
+  if (rc) return rc;
+  IceConsts I;
+  build_ice_consts(M, 0.0, 0.0, &I);
+  return launch_trace(M, I, d_depth, d_ice, d_txh, d_dist, n, d_out10, (hipStream_t)stream);
+}
+
+int airice_trace_ice_to_air_host(const airice_medium* m, const double* depth, const double* ice,
+                                 const double* txh, const double* dist, size_t n, double* out10) {
+  if (n == 0) return AIRICE_OK;
+  double* buf = nullptr;
+  HIP_TRY(hipMalloc(&buf, sizeof(double) * 14 * n));
+  double *dd = buf, *di = buf + n, *dt = buf + 2 * n, *ds = buf + 3 * n, *dout = buf + 4 * n;
+  HIP_TRY(hipMemcpy(dd, depth, sizeof(double) * n, hipMemcpyHostToDevice));
+  HIP_TRY(hipMemcpy(di, ice, sizeof(double) * n, hipMemcpyHostToDevice));
+  HIP_TRY(hipMemcpy(dt, txh, sizeof(double) * n, hipMemcpyHostToDevice));
+  HIP_TRY(hipMemcpy(ds, dist, sizeof(double) * n, hipMemcpyHostToDevice));
+  int rc = airice_trace_ice_to_air_launch(m, dd, di, dt, ds, n, dout, nullptr);
+  if (rc == AIRICE_OK) HIP_TRY(hipMemcpy(out10, dout, sizeof(double) * 10 * n, hipMemcpyDeviceToHost));
+  (void)hipFree(buf);
+  return rc;
+}
+
+// Py_TraceIceToAir drop-in (TraceIceToAir.C:75-79).  The reference re-parses
+// "Atmosphere.dat" from the working directory on every call (TraceIceToAir.C:25);
+// here it is parsed once per process and kept with a small device scratch buffer.
+static std::mutex g_py_mu;
+static bool g_py_ready = false;
+static airice_medium g_py_medium;
+static double* g_py_dev = nullptr;
+
+void Py_TraceIceToAir(double AntennaDepth, double IceLayerHeight, double AirTxHeight,
+                      double HorizontalDistance, double ArrayParameters[10]) {
+  std::lock_guard<std::mutex> lock(g_py_mu);
+  for (int i = 0; i < 10; ++i) ArrayParameters[i] = -1000;
+  if (!g_py_ready) {
+    int rc = airice_atmosphere_load("Atmosphere.dat", AIRICE_VARIANT_PYWRAPPER, &g_py_medium);
+    if (rc != AIRICE_OK) {
+      const char* env = std::getenv("AIRICE_ATMOSPHERE");
+      if (env == nullptr ||
+          airice_atmosphere_load(env, AIRICE_VARIANT_PYWRAPPER, &g_py_medium) != AIRICE_OK) {
+        std::fprintf(stderr, "Py_TraceIceToAir: %s\n", airice_last_error());
+        return;
+      }
+    }
+    if (hipMalloc(&g_py_dev, sizeof(double) * 14) != hipSuccess) {
+      std::fprintf(stderr, "Py_TraceIceToAir: hipMalloc failed\n");
+      return;
+    }
+    g_py_ready = true;
+  }
+  double in[4] = {AntennaDepth, IceLayerHeight, AirTxHeight, HorizontalDistance};
+  if (hipMemcpy(g_py_dev, in, sizeof(in), hipMemcpyHostToDevice) != hipSuccess) return;
+  if (airice_trace_ice_to_air_launch(&g_py_medium, g_py_dev, g_py_dev + 1, g_py_dev + 2,
+                                     g_py_dev + 3, 1, g_py_dev + 4, nullptr) != AIRICE_OK) {
+    std::fprintf(stderr, "Py_TraceIceToAir: %s\n", airice_last_error());
+    return;
+  }
+  (void)hipMemcpy(ArrayParameters, g_py_dev + 4, sizeof(double) * 10, hipMemcpyDeviceToHost);
+}
+
+int airice_device_count(int* count) {
+  HIP_TRY(hipGetDeviceCount(count));
+  return AIRICE_OK;
+}
+int airice_set_device(int device) {
+  HIP_TRY(hipSetDevice(device));
+  return AIRICE_OK;
+}
+int airice_malloc(void** ptr, size_t bytes) {
+  HIP_TRY(hipMalloc(ptr, bytes));
+  return AIRICE_OK;
+}
+int airice_free(void* ptr) {
+  HIP_TRY(hipFree(ptr));
+  return AIRICE_OK;
+}
+int airice_memcpy_h2d(void* dst, const void* src, size_t bytes) {
+  HIP_TRY(hipMemcpy(dst, src, bytes, hipMemcpyHostToDevice));
+  return AIRICE_OK;
+}
+int airice_memcpy_d2h(void* dst, const void* src, size_t bytes) {
+  HIP_TRY(hipMemcpy(dst, src, bytes, hipMemcpyDeviceToHost));
+  return AIRICE_OK;
+}
+int airice_synchronize(void) {
+  HIP_TRY(hipDeviceSynchronize());
+  return AIRICE_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,131 @@
+"""Batched host API over libairice.so.
+
+Two flavours of every entry point:
+  * ``*_device``: inputs/outputs already resident in HBM (torch CUDA tensors or raw
+    device pointers), stream-ordered, asynchronous -- the path ``bench.py`` times;
+  * ``*_host``: numpy in, numpy out (the library copies, launches, synchronises).
+
+Layouts follow the reference: the table is 11 float columns
+(``AllTableAllAntData[ant][col][row]``, MultiRayAirIceRefraction.cc:2101-2111), ray and
+solve outputs are the reference ``dummy[]`` slots as double columns.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+
+from . import _lib
+from ._lib import (Grid, Medium, VARIANT_MULTIRAY, VARIANT_PYWRAPPER, check, lib, ptr)
+
+
+def make_grid(antenna_depth_cm: float, ice_height_cm: float, height_step: float = 10.0,
+              start_angle: float = 90.1, stop_angle: float = 180.0,
+              angle_step: float = 0.1) -> Grid:
+    """MakeRayTracingTable grid (MultiRayAirIceRefraction.cc:12-21, 2019-2061).  Defaults are
+    the reference's globals (10 m x 0.1 deg, 90.1..180 deg, 100 km down to the ice)."""
+    g = Grid()
+    check(lib().airice_grid_init(ctypes.byref(g), antenna_depth_cm, ice_height_cm, height_step,
+                                 start_angle, stop_angle, angle_step), "airice_grid_init")
+    return g
+
+
+def _stream_handle(stream):
+    if stream is None:
+        return None
+    if isinstance(stream, int):
+        return ctypes.c_void_p(stream)
+    return ctypes.c_void_p(stream.cuda_stream)  # torch.cuda.Stream
+
+
+class AirIceSolver:
+    """One medium (parsed GDAS atmosphere + ice model) and the batched GPU entry points."""
+
+    def __init__(self, atmosphere: str | None = None, variant: int = VARIANT_MULTIRAY):
+        self.variant = variant
+        self.medium: Medium = _lib.load_medium(atmosphere, variant)
+
+    # ------------------------------------------------------------------ table
+    def table_device(self, grid: Grid, table, full=None, row_begin: int = 0,
+                     row_count: int | None = None, ld: int | None = None, stream=None) -> None:
+        if row_count is None:
+            row_count = grid.height_steps - row_begin
+        n = row_count * grid.angle_steps
+        ld = n if ld is None else ld
+        check(lib().airice_table_launch(ctypes.byref(self.medium), ctypes.byref(grid), row_begin,
+                                        row_count, ptr(table), ptr(full), ld,
+                                        _stream_handle(stream)), "airice_table_launch")
+
+    def table_host(self, grid: Grid, row_begin: int = 0, row_count: int | None = None,
+                   full: bool = False):
+        if row_count is None:
+            row_count = grid.height_steps - row_begin
+        n = row_count * grid.angle_steps
+        table = np.empty((_lib.TABLE_COLUMNS, n), dtype=np.float32)
+        fullarr = np.empty((_lib.RAY_FIELDS, n), dtype=np.float64) if full else None
+        check(lib().airice_table_host(ctypes.byref(self.medium), ctypes.byref(grid), row_begin,
+                                      row_count, ptr(table), ptr(fullarr), n),
+              "airice_table_host")
+        return (table, fullarr) if full else table
+
+    # ------------------------------------------------------------------ rays
+    def rays_device(self, launch_deg, txh, ice_h: float, depth: float, in_ice: bool, out,
+                    ld: int | None = None, stream=None) -> None:
+        n = int(launch_deg.numel())
+        check(lib().airice_rays_launch(ctypes.byref(self.medium), ptr(launch_deg), ptr(txh),
+                                       ice_h, depth, int(in_ice), n, ptr(out),
+                                       n if ld is None else ld, _stream_handle(stream)),
+              "airice_rays_launch")
+
+    # ------------------------------------------------------------------ minimizer
+    def solve_device(self, txh, dist, depth, ice_h: float, out, status=None,
+                     straight_angle=None, ld: int | None = None, stream=None,
+                     variant: int | None = None) -> None:
+        n = int(txh.numel())
+        v = self.variant if variant is None else variant
+        check(lib().airice_solve_launch(ctypes.byref(self.medium), v, ice_h, ptr(txh), ptr(dist),
+                                        ptr(depth), ptr(straight_angle), n, ptr(out),
+                                        n if ld is None else ld, ptr(status),
+                                        _stream_handle(stream)), "airice_solve_launch")
+
+    def solve_host(self, txh, dist, depth, ice_h: float, straight_angle=None,
+                   variant: int | None = None):
+        v = self.variant if variant is None else variant
+        txh = np.ascontiguousarray(txh, dtype=np.float64)
+        dist = np.ascontiguousarray(dist, dtype=np.float64)
+        depth = np.ascontiguousarray(depth, dtype=np.float64)
+        thr = None if straight_angle is None else np.ascontiguousarray(straight_angle, np.float64)
+        n = txh.size
+        fields = _lib.PYSOLVE_FIELDS if v == VARIANT_PYWRAPPER else _lib.SOLVE_FIELDS
+        out = np.empty((fields, n), dtype=np.float64)
+        st = np.empty(n, dtype=np.uint8)
+        check(lib().airice_solve_host(ctypes.byref(self.medium), v, ice_h, ptr(txh), ptr(dist),
+                                      ptr(depth), ptr(thr), n, ptr(out), n, ptr(st)),
+              "airice_solve_host")
+        return out, st
+
+    # ------------------------------------------------------------------ CoREAS entry
+    def hdtip_device(self, src_cm, dist_cm, depth_cm, ice_cm: float, out, ok,
+                     ld: int | None = None, stream=None) -> None:
+        n = int(src_cm.numel())
+        check(lib().airice_hdtip_launch(ctypes.byref(self.medium), ptr(src_cm), ptr(dist_cm),
+                                        ptr(depth_cm), ice_cm, n, ptr(out),
+                                        n if ld is None else ld, ptr(ok),
+                                        _stream_handle(stream)), "airice_hdtip_launch")
+
+    # ------------------------------------------------------------------ pythonwrapper
+    def trace_ice_to_air_device(self, depth, ice, txh, dist, out10, stream=None) -> None:
+        n = int(depth.numel())
+        check(lib().airice_trace_ice_to_air_launch(ctypes.byref(self.medium), ptr(depth), ptr(ice),
+                                                   ptr(txh), ptr(dist), n, ptr(out10),
+                                                   _stream_handle(stream)),
+              "airice_trace_ice_to_air_launch")
+
+    def trace_ice_to_air_host(self, depth, ice, txh, dist):
+        arrs = [np.ascontiguousarray(np.broadcast_to(a, np.shape(depth)), dtype=np.float64).ravel()
+                for a in (depth, ice, txh, dist)]
+        n = arrs[0].size
+        out = np.empty((n, 10), dtype=np.float64)
+        check(lib().airice_trace_ice_to_air_host(ctypes.byref(self.medium), *[ptr(a) for a in arrs],
+                                                 n, ptr(out)), "airice_trace_ice_to_air_host")
+        return out

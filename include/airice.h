@@ -1,0 +1,172 @@
+/*
+ * airice.h -- C-ABI of libairice.so, the MI355X (gfx950) implementation of the
+ * uzairlatif90/AirIceRayTracing hot path:
+ *   - MultiRayAirIceRefraction table generation  (MakeRayTracingTable,
+ *     MultiRayAirIceRefraction.cc:2019-2158, one ray = GetRayTracingSolutions .cc:1796-2017)
+ *   - per-(Tx,Rx) launch-angle root finding      (Air2IceRayTracing .cc:1464-1616 and the
+ *     CoREAS entry GetHorizontalDistanceToIntersectionPoint .cc:945-989)
+ *   - the pythonwrapper ctypes surface           (Py_TraceIceToAir, pythonwrapper/TraceIceToAir.C:75-79)
+ *
+ * Plain C types only (no HIP / torch types).  Device pointers are hipMalloc'd (or
+ * torch CUDA tensors' data_ptr) and `stream` is a hipStream_t passed as void*
+ * (NULL = default stream).  All *_launch entry points are stream-ordered and
+ * asynchronous; *_host entry points copy, launch and synchronise.
+ *
+ * Errors: every int-returning function returns AIRICE_OK (0) or a negative
+ * AIRICE_E* code; airice_last_error() gives a message.  Numerical failure modes
+ * follow the reference (NaN propagation, -1000 / zeroed outputs), see DESIGN.md.
+ *
+ * Thread safety: the reference library is not reentrant (namespace statics,
+ * MultiRayAirIceRefraction.h:33-81).  Here the medium is an explicit value
+ * (airice_medium) and every batch entry point is reentrant.
+ */
+#ifndef AIRICE_H
+#define AIRICE_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define AIRICE_OK 0
+#define AIRICE_EINVAL (-1)
+#define AIRICE_EIO (-2)
+#define AIRICE_EHIP (-3)
+#define AIRICE_ENOMEM (-4)
+
+/* Variant of the reference namespace whose numerics are reproduced. */
+#define AIRICE_VARIANT_MULTIRAY 0  /* MultiRayAirIceRefraction:: (pi = 3.1415927, .h:29) */
+#define AIRICE_VARIANT_PYWRAPPER 1 /* AirIceRayTracing::        (pi = 4*atan(1), pythonwrapper .h:25) */
+
+/* Per-query solve status bits (GSL 2.x bisection semantics). */
+#define AIRICE_SOLVE_NONFINITE_END 1 /* f(lo) or f(hi) non-finite: reference reads uninitialised GSL state */
+#define AIRICE_SOLVE_BAD_BRACKET 2   /* lo > hi: gsl_root_fsolver_set fails */
+#define AIRICE_SOLVE_STALE_MID 4     /* a bisection midpoint gave non-finite f: root frozen */
+#define AIRICE_SOLVE_PROBED 8        /* bracket-probe loop ran (.cc:1490-1511) */
+#define AIRICE_SOLVE_MAXITER 16      /* 40 iterations, interval test never passed */
+#define AIRICE_SOLVE_NO_AIR_LAYER 32 /* no air layer between Tx and the ice */
+
+/* Medium: the GDAS layered atmosphere reduced to its run-time parameters plus the
+ * ice model.  Filled by airice_atmosphere_* (readATMpar .cc:24-71, readnhFromFile
+ * .cc:73-147, MakeAtmosphere .cc:920-942, FillInAirRefractiveIndex .cc:193-213). */
+typedef struct airice_medium {
+  double atmlay_cm[5];   /* ATMLAY (cm); [4] forced to 1.5e7 (.cc:66) */
+  double abc[5][3];      /* mass-overburden a,b,c rows; abc[4]=abc[3] (.cc:62-64) */
+  double B_air[5];       /* n(h) = A_air + B_air[l]*exp(-C_air[l]*h) */
+  double C_air[5];
+  double N0;             /* natural cubic spline of n(h) at h=0 (.cc:203) */
+  int32_t max_layers;    /* MaxLayers (.cc:142) */
+  int32_t n_points;      /* knots in the flattened profile */
+  double A_air;          /* 1.0 (.h:99) */
+  double A_ice, B_ice, C_ice; /* 1.78, -0.43, 0.0132 (.h:64-66) */
+  double pi;             /* variant constant */
+} airice_medium;
+
+/* MakeRayTracingTable grid (.cc:12-21 globals, .cc:2019-2061 set-up). */
+typedef struct airice_grid {
+  double start_height;   /* LoopStartHeight, m (100000, .cc:2044) */
+  double stop_height;    /* LoopStopHeight, m: ice, or ice+depth when Rx is in air */
+  double height_step;    /* HeightStepSize, m (10) */
+  int32_t height_steps;  /* TotalHeightSteps */
+  double start_angle;    /* LoopStartAngle, deg (90.1) */
+  double stop_angle;     /* LoopStopAngle, deg (180) */
+  double angle_step;     /* AngleStepSize, deg (0.1) */
+  int32_t angle_steps;   /* TotalAngleSteps */
+  double depth_m;        /* AntennaDepth, m (negative = in ice) */
+  double ice_m;          /* IceLayerHeight, m */
+  int32_t in_ice;        /* AntennaDepth < 0 */
+} airice_grid;
+
+#define AIRICE_TABLE_COLUMNS 11 /* float columns of AllTableAllAntData (.cc:2101-2111) */
+#define AIRICE_RAY_FIELDS 18    /* GetRayTracingSolutions dummy[0..17] (.cc:1999-2016) */
+#define AIRICE_SOLVE_FIELDS 17  /* Air2IceRayTracing dummy[0..16] (.cc:1597-1614) */
+#define AIRICE_PYSOLVE_FIELDS 15 /* AirIceRayTracing::Air2IceRayTracing dummy[0..14] (pythonwrapper .cc:1070-1084) */
+#define AIRICE_HDTIP_FIELDS 9   /* GetHorizontalDistanceToIntersectionPoint outputs (.cc:963-972) */
+
+const char *airice_last_error(void);
+const char *airice_version(void);
+
+/* --- medium (host) ------------------------------------------------------ */
+/* Parse a GDAS Atmosphere.dat from a file (replaces MakeAtmosphere(), .cc:920). */
+int airice_atmosphere_load(const char *path, int variant, airice_medium *out);
+/* Parse from an in-memory text image of the same file. */
+int airice_atmosphere_parse(const char *text, size_t len, int variant, airice_medium *out);
+/* n(z) of the medium (Getnz_air .cc:259, Getnz_ice .cc:188), host side. */
+double airice_nz_air(const airice_medium *m, double z);
+double airice_nz_ice(const airice_medium *m, double z);
+
+/* --- table (MakeRayTracingTable) ---------------------------------------- */
+/* Grid set-up exactly as .cc:2019-2061 (depth/ice in cm as the reference takes them). */
+int airice_grid_init(airice_grid *g, double antenna_depth_cm, double ice_height_cm,
+                     double height_step_m, double start_angle_deg, double stop_angle_deg,
+                     double angle_step_deg);
+/* Trace rows [row_begin, row_begin+row_count) x all angles of the grid.
+ * d_table: 11 float columns, column c of ray r at d_table[c*ld + r - row_begin*angle_steps]
+ * (the AllTableAllAntData[ant][c][r] layout).  d_full (nullable): 18 double columns,
+ * same indexing (GetRayTracingSolutions dummy[] for parity checks). */
+int airice_table_launch(const airice_medium *m, const airice_grid *g, int32_t row_begin,
+                        int32_t row_count, float *d_table, double *d_full, size_t ld,
+                        void *stream);
+int airice_table_host(const airice_medium *m, const airice_grid *g, int32_t row_begin,
+                      int32_t row_count, float *h_table, double *h_full, size_t ld);
+
+/* --- single forward ray (GetRayTracingSolutions) on the device ---------- */
+/* n rays with per-ray (launch_deg, txh_m); ice/depth/in_ice uniform; out: 18 double columns. */
+int airice_rays_launch(const airice_medium *m, const double *d_launch_deg, const double *d_txh,
+                       double ice_h_m, double depth_m, int32_t in_ice, size_t n, double *d_out,
+                       size_t ld, void *stream);
+
+/* --- minimizer (Air2IceRayTracing) --------------------------------------- */
+/* Batched launch-angle solve.  Inputs in metres: Tx height, horizontal distance, Rx
+ * depth (negative = below the ice surface); ice height uniform.  d_straight_angle is
+ * Air2IceRayTracing's StraightAngle argument (.cc:1464) in degrees; when NULL it is
+ * formed per query as GetHorizontalDistanceToIntersectionPoint does (.cc:952-958).
+ * d_out: AIRICE_SOLVE_FIELDS (MultiRay) or AIRICE_PYSOLVE_FIELDS (pythonwrapper)
+ * double columns, stride ld.  d_status (nullable): AIRICE_SOLVE_* bits. */
+int airice_solve_launch(const airice_medium *m, int variant, double ice_h_m,
+                        const double *d_txh, const double *d_dist, const double *d_depth,
+                        const double *d_straight_angle, size_t n, double *d_out, size_t ld,
+                        uint8_t *d_status, void *stream);
+int airice_solve_host(const airice_medium *m, int variant, double ice_h_m, const double *txh,
+                      const double *dist, const double *depth, const double *straight_angle,
+                      size_t n, double *out, size_t ld, uint8_t *status);
+
+/* CoREAS entry, batched: GetHorizontalDistanceToIntersectionPoint (.cc:945-989) with cm
+ * inputs; d_out: 9 double columns (opticalPathLengthInIce, opticalPathLengthInAir,
+ * geometricalPathLengthInIce, geometricalPathLengthInAir, launchAngle [rad],
+ * horizontalDistanceToIntersectionPoint, transmissionCoefficientS,
+ * transmissionCoefficientP, RecievedAngleInIce [rad]); d_ok: the returned bool. */
+int airice_hdtip_launch(const airice_medium *m, const double *d_src_cm, const double *d_dist_cm,
+                        const double *d_depth_cm, double ice_cm, size_t n, double *d_out,
+                        size_t ld, uint8_t *d_ok, void *stream);
+
+/* pythonwrapper TraceIceToAir, batched: per-query (depth, ice, txh, dist) metres ->
+ * ArrayParameters[10] rows (TraceIceToAir.C:46-68), row-major n x 10. */
+int airice_trace_ice_to_air_launch(const airice_medium *m, const double *d_depth,
+                                   const double *d_ice, const double *d_txh,
+                                   const double *d_dist, size_t n, double *d_out10,
+                                   void *stream);
+int airice_trace_ice_to_air_host(const airice_medium *m, const double *depth, const double *ice,
+                                 const double *txh, const double *dist, size_t n, double *out10);
+
+/* Drop-in for the reference ctypes symbol (TraceIceToAir.C:75-79).  Reads
+ * "Atmosphere.dat" from the working directory like the reference (once, cached;
+ * falls back to $AIRICE_ATMOSPHERE), then solves on the GPU. */
+void Py_TraceIceToAir(double AntennaDepth, double IceLayerHeight, double AirTxHeight,
+                      double HorizontalDistance, double ArrayParameters[10]);
+
+/* Device bookkeeping (thin wrappers so ctypes callers need no HIP runtime binding). */
+int airice_device_count(int *count);
+int airice_set_device(int device);
+int airice_malloc(void **ptr, size_t bytes);
+int airice_free(void *ptr);
+int airice_memcpy_h2d(void *dst, const void *src, size_t bytes);
+int airice_memcpy_d2h(void *dst, const void *src, size_t bytes);
+int airice_synchronize(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* AIRICE_H */

@@ -1,0 +1,214 @@
+"""TEST INFRASTRUCTURE ONLY: ctypes binding of the CPU oracle (oracle/airice_oracle.c).
+
+Only ``tests/``, ``__graft_entry__.smoke()`` and ``bench.py``'s ``cpu_baseline`` leg may
+import this module, and only as the checker / CPU baseline.  The product path
+(``airiceraytracing_amd``) never imports it.
+
+The oracle restates the reference hot path (MultiRayAirIceRefraction.cc and
+pythonwrapper/AirIceRayTracing.cc); see airice_oracle.h for the per-function
+citations and the parity-pinning status.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB_PATH = os.path.join(_HERE, "liboracle_airice.so")
+
+PI_MULTIRAY = 3.1415927             # MultiRayAirIceRefraction.h:29, RayTracingFunctions.h:26
+PI_EXACT = 4.0 * np.arctan(1.0)     # pythonwrapper/AirIceRayTracing.h:25
+
+TABLE_COLUMNS = (1, 2, 7, 6, 11, 3, 14, 15, 16, 17, 13)  # .cc:2101-2111 -> dummy index
+
+SOLVE_NONFINITE_END = 1
+SOLVE_BAD_BRACKET = 2
+SOLVE_STALE_MID = 4
+SOLVE_PROBED = 8
+SOLVE_MAXITER = 16
+SOLVE_NO_AIR_LAYER = 32
+SOLVE_UNPINNED = SOLVE_NONFINITE_END | SOLVE_BAD_BRACKET | SOLVE_NO_AIR_LAYER
+
+
+class Medium(ctypes.Structure):
+    _fields_ = [
+        ("atmlay", ctypes.c_double * 5),
+        ("abc", (ctypes.c_double * 3) * 5),
+        ("C_air", ctypes.c_double * 5),
+        ("B_air", ctypes.c_double * 5),
+        ("N0", ctypes.c_double),
+        ("max_layers", ctypes.c_int),
+        ("n_points", ctypes.c_int),
+        ("layer_sizes", ctypes.c_int * 8),
+        ("A_air", ctypes.c_double),
+        ("A_ice", ctypes.c_double),
+        ("B_ice", ctypes.c_double),
+        ("C_ice", ctypes.c_double),
+        ("pi", ctypes.c_double),
+    ]
+
+
+class Grid(ctypes.Structure):
+    _fields_ = [
+        ("start_height", ctypes.c_double),
+        ("stop_height", ctypes.c_double),
+        ("height_step", ctypes.c_double),
+        ("height_steps", ctypes.c_int),
+        ("start_angle", ctypes.c_double),
+        ("stop_angle", ctypes.c_double),
+        ("angle_step", ctypes.c_double),
+        ("angle_steps", ctypes.c_int),
+        ("depth_m", ctypes.c_double),
+        ("ice_m", ctypes.c_double),
+        ("in_ice", ctypes.c_int),
+    ]
+
+
+def build() -> str:
+    """Compile the oracle with its Makefile (gcc is in the image and on the GPU box)."""
+    subprocess.run(["make", "-s", "-C", _HERE], check=True)
+    return _LIB_PATH
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(_LIB_PATH):
+            build()
+        L = ctypes.CDLL(_LIB_PATH)
+        D, I, P = ctypes.c_double, ctypes.c_int, ctypes.c_void_p
+        M = ctypes.POINTER(Medium)
+        L.or_parse_atmosphere.argtypes = [ctypes.c_char_p, ctypes.c_size_t, D, M]
+        L.or_load_atmosphere.argtypes = [ctypes.c_char_p, D, M]
+        L.or_spline_eval_at.argtypes = [P, P, I, D]
+        L.or_spline_eval_at.restype = D
+        L.or_getnz_air.argtypes = [M, D]
+        L.or_getnz_air.restype = D
+        L.or_getnz_ice.argtypes = [M, D]
+        L.or_getnz_ice.restype = D
+        L.or_layer_hit_point_par.argtypes = [M, D, D, D, D, I, P]
+        L.or_ray_solution.argtypes = [M, D, D, D, D, I, P]
+        L.or_grid_init.argtypes = [ctypes.POINTER(Grid), D, D, D, D, D, D]
+        L.or_table_rows.argtypes = [M, ctypes.POINTER(Grid), I, I, P, P, ctypes.c_size_t, I]
+        L.or_air2ice.argtypes = [M, D, D, D, D, D, P]
+        L.or_air2ice.restype = I
+        L.or_straight_angle.argtypes = [M, D, D, D, D]
+        L.or_straight_angle.restype = D
+        L.or_solve_batch.argtypes = [M, P, P, P, D, ctypes.c_size_t, P, ctypes.c_size_t, P, I]
+        L.or_hdtip.argtypes = [M, D, D, D, D, P]
+        L.or_hdtip.restype = I
+        L.or_py_air2ice.argtypes = [M, D, D, D, D, D, P]
+        L.or_py_air2ice.restype = I
+        L.or_py_trace_ice_to_air.argtypes = [M, D, D, D, D, P]
+        L.or_py_trace_ice_to_air.restype = I
+        L.or_py_trace_batch.argtypes = [M, P, P, P, P, ctypes.c_size_t, P, I]
+        _lib = L
+    return _lib
+
+
+def _ptr(a):
+    return None if a is None else a.ctypes.data_as(ctypes.c_void_p)
+
+
+def parse_atmosphere(text: bytes, pi: float = PI_MULTIRAY) -> Medium:
+    m = Medium()
+    rc = lib().or_parse_atmosphere(text, len(text), pi, ctypes.byref(m))
+    if rc != 0:
+        raise ValueError("oracle: could not parse atmosphere text")
+    return m
+
+
+def load_atmosphere(path: str, pi: float = PI_MULTIRAY) -> Medium:
+    with open(path, "rb") as f:
+        data = f.read()
+    if path.endswith(".gz"):
+        import gzip
+        data = gzip.decompress(data)
+    return parse_atmosphere(data, pi)
+
+
+def getnz_air(m: Medium, z: float) -> float:
+    return lib().or_getnz_air(ctypes.byref(m), z)
+
+
+def getnz_ice(m: Medium, z: float) -> float:
+    return lib().or_getnz_ice(ctypes.byref(m), z)
+
+
+def ray_solution(m: Medium, launch_deg, txh, ice_h, depth, in_ice=True) -> np.ndarray:
+    out = np.zeros(18)
+    lib().or_ray_solution(ctypes.byref(m), launch_deg, txh, ice_h, depth, int(in_ice), _ptr(out))
+    return out
+
+
+def grid_init(depth_cm, ice_cm, height_step=10.0, start_angle=90.1, stop_angle=180.0,
+              angle_step=0.1) -> Grid:
+    g = Grid()
+    lib().or_grid_init(ctypes.byref(g), depth_cm, ice_cm, height_step, start_angle, stop_angle,
+                       angle_step)
+    return g
+
+
+def table_rows(m: Medium, g: Grid, row0: int, row1: int, full: bool = False, nthreads: int = 0):
+    n = (row1 - row0) * g.angle_steps
+    table = np.zeros((11, n), dtype=np.float32)
+    fullarr = np.zeros((18, n), dtype=np.float64) if full else None
+    lib().or_table_rows(ctypes.byref(m), ctypes.byref(g), row0, row1, _ptr(table), _ptr(fullarr),
+                        n, nthreads)
+    return (table, fullarr) if full else table
+
+
+def air2ice(m: Medium, txh, dist, ice_h, depth, straight_angle=None):
+    if straight_angle is None:
+        straight_angle = straight_angle_of(m, txh, dist, ice_h, depth)
+    out = np.zeros(17)
+    st = lib().or_air2ice(ctypes.byref(m), txh, dist, ice_h, depth, straight_angle, _ptr(out))
+    return out, st
+
+
+def straight_angle_of(m: Medium, txh, dist, ice_h, depth) -> float:
+    return lib().or_straight_angle(ctypes.byref(m), txh, dist, ice_h, depth)
+
+
+def solve_batch(m: Medium, txh, dist, depth, ice_h, nthreads: int = 0):
+    txh = np.ascontiguousarray(txh, dtype=np.float64)
+    dist = np.ascontiguousarray(dist, dtype=np.float64)
+    depth = np.ascontiguousarray(depth, dtype=np.float64)
+    n = txh.size
+    out = np.zeros((17, n))
+    st = np.zeros(n, dtype=np.uint8)
+    lib().or_solve_batch(ctypes.byref(m), _ptr(txh), _ptr(dist), _ptr(depth), ice_h, n,
+                         _ptr(out), n, _ptr(st), nthreads)
+    return out, st
+
+
+def hdtip(m: Medium, src_cm, dist_cm, depth_cm, ice_cm):
+    out = np.zeros(9)
+    ok = lib().or_hdtip(ctypes.byref(m), src_cm, dist_cm, depth_cm, ice_cm, _ptr(out))
+    return bool(ok), out
+
+
+def py_air2ice(m: Medium, txh, dist, ice_h, depth, straight_angle):
+    out = np.zeros(15)
+    st = lib().or_py_air2ice(ctypes.byref(m), txh, dist, ice_h, depth, straight_angle, _ptr(out))
+    return out, st
+
+
+def py_trace_ice_to_air(m: Medium, depth, ice_h, txh, dist):
+    out = np.zeros(10)
+    ok = lib().or_py_trace_ice_to_air(ctypes.byref(m), depth, ice_h, txh, dist, _ptr(out))
+    return bool(ok), out
+
+
+def py_trace_batch(m: Medium, depth, ice, txh, dist, nthreads: int = 0):
+    arrs = [np.ascontiguousarray(a, dtype=np.float64) for a in (depth, ice, txh, dist)]
+    n = arrs[0].size
+    out = np.zeros((n, 10))
+    lib().or_py_trace_batch(ctypes.byref(m), *[_ptr(a) for a in arrs], n, _ptr(out), nthreads)
+    return out

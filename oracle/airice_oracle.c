@@ -1,0 +1,813 @@
+/*
+ * airice_oracle.c -- TEST INFRASTRUCTURE ONLY (see airice_oracle.h).
+ *
+ * Plain-C restatement of the reference hot path, written from the reference's
+ * behaviour (file:line cited per function).  Faithful mode: each reference
+ * function is a function here, with the same per-call layer scans, the same
+ * libm calls and the same expression order (pow(x,2) is written x*x, which is
+ * what g++ -O2 folds it to).  Build: oracle/Makefile (gcc -O2 -ffp-contract=off).
+ *
+ * Third-party algorithms restated (GNU GSL, absent from this image; the
+ * reference pins "2.4 is verified", README.md:37, and links libgsl.so.23/.27):
+ *   - gsl_interp_cspline natural cubic spline (interpolation/cspline.c) with
+ *     gsl_linalg_solve_symm_tridiag (linalg/tridiag.c), evaluated once for N0;
+ *   - gsl_root_fsolver_bisection + gsl_root_test_interval
+ *     (roots/bisection.c, roots/convergence.c, roots/fsolver.c).
+ */
+#include "airice_oracle.h"
+
+#include <math.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#ifdef _OPENMP
+#include <omp.h>
+#endif
+
+static const double SPEEDC = 299792458.0; /* MultiRayAirIceRefraction.h:30 */
+
+/* ------------------------------------------------------------------------- */
+/* iostream emulation for the GDAS parser (std::getline / operator>> / ignore) */
+/* ------------------------------------------------------------------------- */
+typedef struct {
+  const char *p, *end;
+  int fail;
+} or_stream;
+
+static int st_getline(or_stream *s) {
+  if (s->fail) return 0;
+  if (s->p >= s->end) { s->fail = 1; return 0; }
+  while (s->p < s->end && *s->p != '\n') s->p++;
+  if (s->p < s->end) s->p++; /* consume delimiter */
+  return 1;
+}
+
+static void st_ignore(or_stream *s, int n, char delim) {
+  if (s->fail) return;
+  for (int i = 0; i < n && s->p < s->end; i++) {
+    char c = *s->p++;
+    if (c == delim) break;
+  }
+}
+
+/* operator>>(double&): skip ws; at EOF -> fail, value unchanged (sentry fails). */
+static void st_read_double(or_stream *s, double *v) {
+  if (s->fail) return;
+  while (s->p < s->end && (*s->p == ' ' || *s->p == '\t' || *s->p == '\n' || *s->p == '\r'
+                           || *s->p == '\v' || *s->p == '\f'))
+    s->p++;
+  if (s->p >= s->end) { s->fail = 1; return; }
+  char buf[64];
+  size_t k = 0;
+  const char *q = s->p;
+  while (q < s->end && k < sizeof(buf) - 1 && !(*q == ' ' || *q == '\t' || *q == '\n' || *q == '\r'))
+    buf[k++] = *q++;
+  buf[k] = 0;
+  char *ep = NULL;
+  double x = strtod(buf, &ep);
+  if (ep == buf) { *v = 0.0; s->fail = 1; return; }
+  s->p += (ep - buf);
+  *v = x;
+}
+
+/* ------------------------------------------------------------------------- */
+/* GSL natural cubic spline (cspline_init natural BC + solve_symm_tridiag +    */
+/* cspline_eval), restated.                                                    */
+/* ------------------------------------------------------------------------- */
+double or_spline_eval_at(const double *xa, const double *ya, int size, double x) {
+  const int max_index = size - 1;
+  const int sys_size = max_index - 1;
+  double *c = (double *)calloc((size_t)size, sizeof(double));
+  double *g = (double *)malloc(sizeof(double) * (size_t)sys_size);
+  double *diag = (double *)malloc(sizeof(double) * (size_t)sys_size);
+  double *offdiag = (double *)malloc(sizeof(double) * (size_t)sys_size);
+  for (int i = 0; i < sys_size; i++) {
+    const double h_i = xa[i + 1] - xa[i];
+    const double h_ip1 = xa[i + 2] - xa[i + 1];
+    const double ydiff_i = ya[i + 1] - ya[i];
+    const double ydiff_ip1 = ya[i + 2] - ya[i + 1];
+    const double g_i = (h_i != 0.0) ? 1.0 / h_i : 0.0;
+    const double g_ip1 = (h_ip1 != 0.0) ? 1.0 / h_ip1 : 0.0;
+    offdiag[i] = h_ip1;
+    diag[i] = 2.0 * (h_ip1 + h_i);
+    g[i] = 3.0 * (ydiff_ip1 * g_ip1 - ydiff_i * g_i);
+  }
+  if (sys_size == 1) {
+    c[1] = g[0] / diag[0];
+  } else {
+    /* LDL^T of the symmetric tridiagonal system (linalg/tridiag.c). */
+    const int N = sys_size;
+    double *gamma = (double *)malloc(sizeof(double) * (size_t)N);
+    double *alpha = (double *)malloc(sizeof(double) * (size_t)N);
+    double *cc = (double *)malloc(sizeof(double) * (size_t)N);
+    double *z = (double *)malloc(sizeof(double) * (size_t)N);
+    alpha[0] = diag[0];
+    gamma[0] = offdiag[0] / alpha[0];
+    for (int i = 1; i < N - 1; i++) {
+      alpha[i] = diag[i] - offdiag[i - 1] * gamma[i - 1];
+      gamma[i] = offdiag[i] / alpha[i];
+    }
+    if (N > 1) alpha[N - 1] = diag[N - 1] - offdiag[N - 2] * gamma[N - 2];
+    z[0] = g[0];
+    for (int i = 1; i < N; i++) z[i] = g[i] - gamma[i - 1] * z[i - 1];
+    for (int i = 0; i < N; i++) cc[i] = z[i] / alpha[i];
+    double *xs = c + 1;
+    xs[N - 1] = cc[N - 1];
+    if (N >= 2) {
+      for (int i = N - 2, j = 0; j <= N - 2; j++, i--) xs[i] = cc[i] - gamma[i] * xs[i + 1];
+    }
+    free(gamma); free(alpha); free(cc); free(z);
+  }
+  /* gsl_interp_bsearch over [0, size-1] */
+  int ilo = 0, ihi = size - 1;
+  while (ihi > ilo + 1) {
+    int i = (ihi + ilo) / 2;
+    if (xa[i] > x) ihi = i; else ilo = i;
+  }
+  double y;
+  const double x_hi = xa[ilo + 1], x_lo = xa[ilo];
+  const double dx = x_hi - x_lo;
+  if (dx > 0.0) {
+    const double y_lo = ya[ilo], y_hi = ya[ilo + 1];
+    const double dy = y_hi - y_lo;
+    const double delx = x - x_lo;
+    const double c_i = c[ilo], c_ip1 = c[ilo + 1];
+    const double b_i = (dy / dx) - dx * (c_ip1 + 2.0 * c_i) / 3.0;
+    const double d_i = (c_ip1 - c_i) / (3.0 * dx);
+    y = y_lo + delx * (b_i + delx * (c_i + delx * d_i));
+  } else {
+    y = NAN;
+  }
+  free(c); free(g); free(diag); free(offdiag);
+  return y;
+}
+
+/* ------------------------------------------------------------------------- */
+/* Atmosphere: readATMpar (.cc:24-71), readnhFromFile (.cc:73-147),          */
+/* MakeAtmosphere (.cc:920-942), FillInAirRefractiveIndex (.cc:193-213).      */
+/* ------------------------------------------------------------------------- */
+int or_parse_atmosphere(const char *text, size_t len, double pi, or_medium *m) {
+  memset(m, 0, sizeof(*m));
+  m->pi = pi;
+  m->A_air = 1.00;
+  m->A_ice = 1.78; m->B_ice = -0.43; m->C_ice = 0.0132;
+
+  /* readATMpar */
+  {
+    or_stream s = {text, text + len, 0};
+    int n1 = 0;
+    double d[5] = {0, 0, 0, 0, 0};
+    while (st_getline(&s)) {
+      if (n1 < 4)
+        for (int i = 0; i < 5; i++) st_read_double(&s, &d[i]);
+      if (n1 == 0) for (int i = 0; i < 5; i++) m->atmlay[i] = d[i];
+      if (n1 == 1) for (int i = 0; i < 5; i++) m->abc[i][0] = d[i];
+      if (n1 == 2) for (int i = 0; i < 5; i++) m->abc[i][1] = d[i];
+      if (n1 == 3) for (int i = 0; i < 5; i++) m->abc[i][2] = d[i];
+      n1++;
+    }
+    for (int k = 0; k < 3; k++) m->abc[4][k] = m->abc[3][k];
+    m->atmlay[4] = 150000 * 100;
+  }
+
+  /* readnhFromFile: collect groups exactly as the push/clear logic does. */
+  size_t cap = len / 8 + 16;
+  double *h = (double *)malloc(sizeof(double) * cap);
+  double *nv = (double *)malloc(sizeof(double) * cap);
+  int ngroups = 0;
+  int group_end[16];
+  size_t npts = 0;
+  {
+    or_stream s = {text, text + len, 0};
+    for (int i = 0; i < 5; i++) st_ignore(&s, 256, '\n');
+    int layer = 0;
+    double d1 = 0, d2 = 0;
+    while (st_getline(&s)) {
+      st_read_double(&s, &d1);
+      st_read_double(&s, &d2);
+      if (d1 > -1) {
+        if (npts >= cap) { cap *= 2; h = realloc(h, sizeof(double) * cap); nv = realloc(nv, sizeof(double) * cap); }
+        h[npts] = d1; nv[npts] = d2; npts++;
+        if (d1 * 100 >= m->atmlay[layer]) {
+          if (layer > 0) { if (ngroups < 16) group_end[ngroups] = (int)npts; ngroups++; }
+          layer++;
+          if (layer > 4) layer = 4; /* ATMLAY has 5 entries; 1.5e7 cm is never reached */
+        }
+      }
+    }
+    if (layer > 0) { if (ngroups < 16) group_end[ngroups] = (int)npts; ngroups++; }
+  }
+  if (ngroups < 1 || npts < 3) { free(h); free(nv); return -1; }
+  /* drop the duplicated last data point from the last group (.cc:138-140) */
+  npts -= 1;
+  group_end[ngroups - 1] -= 1;
+  m->max_layers = ngroups + 1;
+  m->n_points = (int)npts;
+  for (int i = 0; i < ngroups && i < 8; i++)
+    m->layer_sizes[i] = group_end[i] - (i ? group_end[i - 1] : 0);
+
+  /* spline over the flattened profile; only n(0) is ever used (.cc:203) */
+  const double N0s = or_spline_eval_at(h, nv, (int)npts, 0.0);
+  free(h); free(nv);
+
+  double N0 = 0;
+  for (int il = 0; il < 5; il++) {
+    double hlow = m->atmlay[il] / 100;
+    m->C_air[il] = 1.0 / (m->abc[il][2] / 100);
+    if (il > 0) N0 = m->A_air + m->B_air[il - 1] * exp(-hlow * m->C_air[il - 1]);
+    if (il == 0) { N0 = N0s; m->N0 = N0s; }
+    m->B_air[il] = ((N0 - 1) / exp(-hlow * m->C_air[il]));
+  }
+  return 0;
+}
+
+int or_load_atmosphere(const char *path, double pi, or_medium *m) {
+  FILE *f = fopen(path, "rb");
+  if (!f) return -1;
+  fseek(f, 0, SEEK_END);
+  long n = ftell(f);
+  fseek(f, 0, SEEK_SET);
+  char *buf = (char *)malloc((size_t)n + 1);
+  size_t got = fread(buf, 1, (size_t)n, f);
+  fclose(f);
+  buf[got] = 0;
+  int rc = or_parse_atmosphere(buf, got, pi, m);
+  free(buf);
+  return rc;
+}
+
+/* ------------------------------------------------------------------------- */
+/* Medium model (.cc:150-191, 216-263)                                        */
+/* ------------------------------------------------------------------------- */
+static double GetB_ice(const or_medium *m, double z) { (void)z; return m->B_ice; }
+static double GetC_ice(const or_medium *m, double z) { (void)z; return m->C_ice; }
+double or_getnz_ice(const or_medium *m, double z) {
+  z = fabs(z);
+  return m->A_ice + GetB_ice(m, z) * exp(-GetC_ice(m, z) * z);
+}
+
+static int air_layer(const or_medium *m, double z) {
+  double zabs = fabs(z);
+  int which = 0;
+  for (int il = 0; il < m->max_layers - 1; il++) {
+    if (zabs < m->atmlay[il + 1] / 100 && zabs >= m->atmlay[il] / 100) { which = il; il = 100; }
+  }
+  if (zabs >= m->atmlay[m->max_layers - 1] / 100) which = m->max_layers - 1;
+  return which;
+}
+static double GetB_air(const or_medium *m, double z) { return m->B_air[air_layer(m, z)]; }
+static double GetC_air(const or_medium *m, double z) { return m->C_air[air_layer(m, z)]; }
+double or_getnz_air(const or_medium *m, double z) {
+  double zabs = fabs(z);
+  return m->A_air + GetB_air(m, zabs) * exp(-GetC_air(m, zabs) * zabs);
+}
+
+/* Fresnel amplitude transmission (.cc:285-337) */
+static double Trans_S(const or_medium *m, double thetai, double ice_h) {
+  double n1 = or_getnz_air(m, ice_h), n2 = or_getnz_ice(m, 0);
+  double a = (n1 / n2) * (sin(thetai));
+  double sqterm = sqrt(1 - a * a);
+  double num = n1 * cos(thetai) - n2 * sqterm;
+  double den = n1 * cos(thetai) + n2 * sqterm;
+  double tS = 1 + (num / den);
+  if (isnan(tS)) tS = 0;
+  return tS;
+}
+static double Trans_P(const or_medium *m, double thetai, double ice_h) {
+  double n1 = or_getnz_air(m, ice_h), n2 = or_getnz_ice(m, 0);
+  double a = (n1 / n2) * (sin(thetai));
+  double sqterm = sqrt(1 - a * a);
+  double num = n1 * sqterm - n2 * cos(thetai);
+  double den = n1 * sqterm + n2 * cos(thetai);
+  double tP = (1 - (num / den)) * (n1 / n2);
+  if (isnan(tP)) tP = 0;
+  return tP;
+}
+
+/* ------------------------------------------------------------------------- */
+/* Analytic antiderivatives (.cc:377-447)                                     */
+/* ------------------------------------------------------------------------- */
+static double fDnfR(double x, double A, double B, double C, double L) {
+  double y = A + B * exp(C * x);
+  return (L / C) * (1.0 / sqrt(A * A - L * L)) *
+         (C * x - log(A * (A + B * exp(C * x)) - L * L + sqrt(A * A - L * L) * sqrt(y * y - L * L)));
+}
+
+static double ftimeD(const or_medium *m, double x, double A, double C, double Speedc, double L,
+                     int air_or_ice) {
+  double n = air_or_ice ? or_getnz_air(m, x) : or_getnz_ice(m, x);
+  double n2 = n * n; /* pow(Getnz(x),2) */
+  return (1.0 / (Speedc * C * sqrt(n2 - L * L))) *
+         (n2 - L * L +
+          (C * x - log(A * n - L * L + sqrt(A * A - L * L) * sqrt(n2 - L * L))) *
+              (A * A * sqrt(n2 - L * L)) / sqrt(A * A - L * L) +
+          A * sqrt(n2 - L * L) * log(n + sqrt(n2 - L * L)));
+}
+
+static double fpathD(double x, double A, double B, double C, double L) {
+  double e = exp(C * x);
+  double e2 = exp(2 * C * x);
+  double y = A + B * e;
+  double Q = (A * A + 2 * A * B * e + B * B * e2 - L * L) / (y * y);
+  double sA = sqrt(A * A - L * L);
+  return (log(y * (sqrt(Q) + 1)) -
+          (A * log(A * sA * sqrt(Q) + B * sA * e * sqrt(Q) + A * A + A * B * e - L * L)) / sA +
+          (A * C * x) / sA) / C;
+}
+
+/* GetRayHorizontalPath / PropagationTime / GeometricPath (.cc:449-513) */
+static double GetRayHorizontalPath(const or_medium *m, double A, double Rx, double Tx, double L, int air) {
+  double Ba, Ca, Bb, Cb;
+  if (air) { Ba = GetB_air(m, Rx); Ca = -GetC_air(m, Rx); Bb = GetB_air(m, Tx); Cb = -GetC_air(m, Tx); }
+  else     { Ba = GetB_ice(m, Rx); Ca = -GetC_ice(m, Rx); Bb = GetB_ice(m, Tx); Cb = -GetC_ice(m, Tx); }
+  double x1 = +fDnfR(Rx, A, Ba, Ca, L) - fDnfR(Tx, A, Bb, Cb, L);
+  if (air) x1 *= -1;
+  return x1;
+}
+static double GetRayPropagationTime(const or_medium *m, double A, double Rx, double Tx, double L, int air) {
+  double Ca, Cb;
+  if (air) { Ca = -GetC_air(m, Rx); Cb = -GetC_air(m, Tx); }
+  else     { Ca = -GetC_ice(m, Rx); Cb = -GetC_ice(m, Tx); }
+  double t = +ftimeD(m, Rx, A, Ca, SPEEDC, L, air) - ftimeD(m, Tx, A, Cb, SPEEDC, L, air);
+  if (air) t *= -1;
+  return t;
+}
+static double GetRayGeometricPath(const or_medium *m, double A, double Rx, double Tx, double L, int air) {
+  double Ba, Ca, Bb, Cb;
+  if (air) { Ba = GetB_air(m, Rx); Ca = -GetC_air(m, Rx); Bb = GetB_air(m, Tx); Cb = -GetC_air(m, Tx); }
+  else     { Ba = GetB_ice(m, Rx); Ca = -GetC_ice(m, Rx); Bb = GetB_ice(m, Tx); Cb = -GetC_ice(m, Tx); }
+  double g = fpathD(Rx, A, Ba, Ca, L) - fpathD(Tx, A, Bb, Cb, L);
+  if (air) g *= -1;
+  return g;
+}
+
+/* GetLayerHitPointPar (.cc:521-646): {THD, Recv deg, L, t, geo} */
+void or_layer_hit_point_par(const or_medium *m, double n_layer1, double Rx, double Tx,
+                            double IncidentAng, int air, double out[5]) {
+  const double pi = m->pi;
+  double SurfaceRayIncidentAngle = IncidentAng * (pi / 180.0);
+  double A, nzRx, nzTx;
+  if (air) { A = m->A_air; nzRx = or_getnz_air(m, Rx); nzTx = or_getnz_air(m, Tx); }
+  else     { A = m->A_ice; nzRx = or_getnz_ice(m, Rx); nzTx = or_getnz_ice(m, Tx); }
+  double RayAngleInside2ndLayer = asin((n_layer1 / nzTx) * sin(SurfaceRayIncidentAngle));
+  double Lang = RayAngleInside2ndLayer;
+  double ReceiveAngle;
+  if (air) ReceiveAngle = asin((or_getnz_air(m, Tx) * sin(Lang)) / or_getnz_air(m, Rx));
+  else     ReceiveAngle = asin((or_getnz_ice(m, Tx) * sin(Lang)) / or_getnz_ice(m, Rx));
+  double Lvalue = nzRx * sin(ReceiveAngle);
+  out[0] = GetRayHorizontalPath(m, A, Rx, Tx, Lvalue, air);
+  out[1] = ReceiveAngle * (180 / pi);
+  out[2] = Lvalue;
+  out[3] = GetRayPropagationTime(m, A, Rx, Tx, Lvalue, air);
+  out[4] = GetRayGeometricPath(m, A, Rx, Tx, Lvalue, air);
+}
+
+/* Layer skip scans (.cc:1798-1825 == .cc:666-690). */
+static int skip_above(const or_medium *m, double txh) {
+  int skip = 0;
+  for (int il = m->max_layers; il > -1; il--) {
+    /* ATMLAY[il-1] is read only when the first test holds (txh < ATMLAY[0]/100 = 0 at il=0) */
+    if (txh < m->atmlay[il] / 100 && (il - 1 >= 0 ? txh >= m->atmlay[il - 1] / 100 : 0)) il = -100;
+    if (il > -1) skip++;
+  }
+  return skip;
+}
+static int skip_below(const or_medium *m, double ice_h) {
+  int skip = 0;
+  for (int il = 0; il < m->max_layers; il++) {
+    if (ice_h >= m->atmlay[il] / 100 && ice_h < m->atmlay[il + 1] / 100) il = 100;
+    if (il < m->max_layers) skip++;
+  }
+  return skip;
+}
+
+/* GetRayTracingSolutions (.cc:1796-2017) */
+void or_ray_solution(const or_medium *m, double RayLaunchAngleInAir, double AirTxHeight,
+                     double IceLayerHeight, double AntennaDepth, int InIce, double dummy[18]) {
+  const double pi = m->pi;
+  int SkipLayersAbove = skip_above(m, AirTxHeight);
+  int SkipLayersBelow = skip_below(m, IceLayerHeight);
+  double Start_nh = 0, StartHeight = 0, StopHeight = 0, StartAngle = 0;
+  double THDair = 0, GeoAir = 0, TimeAir = 0;
+  const int top = m->max_layers - SkipLayersAbove - 1;
+  for (int il = top; il > SkipLayersBelow - 1; il--) {
+    if (il == top) StartHeight = AirTxHeight;
+    else StartHeight = m->atmlay[il + 1] / 100 - 0.00001;
+    Start_nh = or_getnz_air(m, StartHeight);
+    if (il == (SkipLayersBelow - 1) + 1) StopHeight = IceLayerHeight;
+    else StopHeight = m->atmlay[il] / 100;
+    if (il == top) StartAngle = 180 - RayLaunchAngleInAir;
+    double hp[5];
+    or_layer_hit_point_par(m, Start_nh, StopHeight, StartHeight, StartAngle, 1, hp);
+    THDair += hp[0];
+    StartAngle = hp[1];
+    TimeAir += hp[3];
+    GeoAir += hp[4];
+  }
+  double IncidentAngleonIce = StartAngle;
+  double THDice = 0, GeoIce = 0, TimeIce = 0, RecvIce = 0;
+  if (InIce) {
+    /* TransitionBoundary==0 branch (.cc:1897-1922) */
+    double StartDepth = 0.0;
+    Start_nh = or_getnz_air(m, IceLayerHeight);
+    double StopDepth = -AntennaDepth;
+    StartAngle = IncidentAngleonIce;
+    double hp[5];
+    or_layer_hit_point_par(m, Start_nh, StopDepth, StartDepth, StartAngle, 0, hp);
+    THDice += hp[0];
+    StartAngle = hp[1];
+    TimeIce += hp[3];
+    GeoIce += hp[4];
+    RecvIce = hp[1];
+  }
+  for (int i = 0; i < 18; i++) dummy[i] = 0;
+  dummy[0] = 0;
+  dummy[1] = AirTxHeight;
+  dummy[2] = THDair + THDice;
+  dummy[3] = THDair;
+  dummy[4] = THDice;
+  dummy[5] = (TimeIce + TimeAir) * SPEEDC;
+  dummy[6] = TimeAir * SPEEDC;
+  dummy[7] = TimeIce * SPEEDC;
+  dummy[8] = (TimeIce + TimeAir) * 1e9;
+  dummy[9] = TimeAir * 1e9;
+  dummy[10] = TimeIce * 1e9;
+  dummy[11] = RayLaunchAngleInAir;
+  dummy[12] = IncidentAngleonIce;
+  dummy[13] = RecvIce;
+  dummy[14] = Trans_S(m, IncidentAngleonIce * (pi / 180.0), IceLayerHeight);
+  dummy[15] = Trans_P(m, IncidentAngleonIce * (pi / 180.0), IceLayerHeight);
+  dummy[16] = GeoAir;
+  dummy[17] = GeoIce;
+}
+
+/* MakeRayTracingTable grid arithmetic (.cc:12-21, 2019-2061). */
+void or_grid_init(or_grid *g, double depth_cm, double ice_cm, double height_step,
+                  double start_angle, double stop_angle, double angle_step) {
+  g->in_ice = depth_cm < 0;
+  g->depth_m = depth_cm / 100;
+  g->ice_m = ice_cm / 100;
+  g->start_height = 100000;
+  g->stop_height = g->in_ice ? g->ice_m : g->ice_m + g->depth_m;
+  g->height_step = height_step;
+  g->height_steps = (int)floor((g->start_height - g->stop_height) / height_step) + 1;
+  g->start_angle = start_angle;
+  g->stop_angle = stop_angle;
+  g->angle_step = angle_step;
+  g->angle_steps = (int)floor((stop_angle - start_angle) / angle_step) + 1;
+}
+
+/* Table columns (.cc:2101-2111): dummy indices */
+static const int TABLE_COL[11] = {1, 2, 7, 6, 11, 3, 14, 15, 16, 17, 13};
+
+void or_table_rows(const or_medium *m, const or_grid *g, int row0, int row1, float *table,
+                   double *full, size_t ld, int nthreads) {
+  const int na = g->angle_steps;
+  const long total = (long)(row1 - row0) * na;
+#ifdef _OPENMP
+  if (nthreads > 0) omp_set_num_threads(nthreads);
+#pragma omp parallel for schedule(dynamic, 64) if (nthreads > 0)
+#endif
+  for (long k = 0; k < total; k++) {
+    int ihei = row0 + (int)(k / na);
+    int iang = (int)(k % na);
+    double H = g->start_height - g->height_step * ihei;
+    if (!(H > 0)) continue; /* .cc:2082 */
+    double th = g->start_angle + g->angle_step * iang;
+    if (H != g->stop_height && ihei == g->height_steps - 1) H = g->stop_height;
+    if (iang == na - 1) th = g->stop_angle;
+    double d[18];
+    or_ray_solution(m, th, H, g->stop_height, g->depth_m, g->in_ice, d);
+    size_t r = (size_t)(ihei - row0) * na + iang;
+    if (table) for (int c = 0; c < 11; c++) table[c * ld + r] = (float)d[TABLE_COL[c]];
+    if (full) for (int c = 0; c < 18; c++) full[c * ld + r] = d[c];
+  }
+}
+
+/* ------------------------------------------------------------------------- */
+/* Minimizer path                                                             */
+/* ------------------------------------------------------------------------- */
+/* GetAirPropagationPar (.cc:661-804): out[5*ML+2]; returns filled layers. */
+static int air_propagation(const or_medium *m, double LaunchAngleAir, double AirTxHeight,
+                           double IceLayerHeight, double *out) {
+  const double pi = m->pi;
+  int SkipLayersAbove = skip_above(m, AirTxHeight);
+  int SkipLayersBelow = skip_below(m, IceLayerHeight);
+  double StartAngle = 0, StartHeight = 0, Start_nh = 0, StopHeight = 0;
+  double L0 = 0;
+  int nf = 0;
+  const int top = m->max_layers - SkipLayersAbove - 1;
+  for (int il = top; il > SkipLayersBelow - 1; il--) {
+    if (il == top) StartHeight = AirTxHeight;
+    else StartHeight = m->atmlay[il + 1] / 100 - 0.00001;
+    Start_nh = or_getnz_air(m, StartHeight);
+    if (il == (SkipLayersBelow - 1) + 1) StopHeight = IceLayerHeight;
+    else StopHeight = m->atmlay[il] / 100;
+    if (il == top) StartAngle = 180 - LaunchAngleAir;
+    if (il == top) {
+      double hp[5];
+      or_layer_hit_point_par(m, Start_nh, StopHeight, StartHeight, StartAngle, 1, hp);
+      for (int j = 0; j < 5; j++) out[nf * 5 + j] = hp[j];
+      L0 = hp[2];
+      StartAngle = hp[1];
+      nf++;
+    }
+    if (il < top) {
+      double nzStop = or_getnz_air(m, StopHeight);
+      double RecAng = asin(L0 / nzStop);
+      RecAng = RecAng * (180 / pi);
+      out[nf * 5 + 0] = GetRayHorizontalPath(m, m->A_air, StopHeight, StartHeight, L0, 1);
+      out[nf * 5 + 1] = RecAng;
+      out[nf * 5 + 2] = L0;
+      out[nf * 5 + 3] = GetRayPropagationTime(m, m->A_air, StopHeight, StartHeight, L0, 1);
+      out[nf * 5 + 4] = GetRayGeometricPath(m, m->A_air, StopHeight, StartHeight, L0, 1);
+      StartAngle = RecAng;
+      nf++;
+    }
+  }
+  out[5 * m->max_layers + 1] = nf;
+  return nf;
+}
+
+/* GetIcePropagationPar (.cc:807-869), TransitionBoundary==0 branch. */
+static void ice_propagation(const or_medium *m, double IceLayerHeight, double AntennaDepth,
+                            double Lvalue, double out[5]) {
+  (void)IceLayerHeight;
+  const double pi = m->pi;
+  double StartDepth = 0.0, StopDepth = AntennaDepth;
+  double nzStopDepth = or_getnz_ice(m, StopDepth);
+  out[0] = GetRayHorizontalPath(m, m->A_ice, StopDepth, StartDepth, Lvalue, 0);
+  out[1] = asin(Lvalue / nzStopDepth) * (180 / pi);
+  out[2] = Lvalue;
+  out[3] = GetRayPropagationTime(m, m->A_ice, StopDepth, StartDepth, Lvalue, 0);
+  out[4] = GetRayGeometricPath(m, m->A_ice, StopDepth, StartDepth, Lvalue, 0);
+}
+
+typedef struct { double airtxheight, icelayerheight, antennadepth, horizontaldistance; } minp;
+
+/* MinimizeforLaunchAngle (.cc:873-917) */
+static double MinimizeforLaunchAngle(const or_medium *m, double x, const minp *p) {
+  double out[5 * 8 + 2];
+  int nf = air_propagation(m, x, p->airtxheight, p->icelayerheight, out);
+  double thd_air = 0;
+  for (int i = 0; i < nf; i++) thd_air += out[i * 5];
+  /* nf==0 (Tx above 150 km or below the ice): the reference reads out[-4] and an
+   * unset out[2] (UB); modelled as NaN. */
+  double L = nf > 0 ? out[2] : NAN;
+  double thd_ice = 0;
+  if (p->antennadepth != 0) {
+    double ic[5];
+    ice_propagation(m, p->icelayerheight, p->antennadepth, L, ic);
+    thd_ice += ic[0];
+  }
+  return (p->horizontaldistance - (thd_ice + thd_air));
+}
+
+/* FindFunctionRoot (.cc:340-374) with GSL bisection semantics.
+ * Uninitialised-state cases are modelled as a zero-filled state. */
+static double bisection_root(const or_medium *m, const minp *p, double x_lo, double x_hi,
+                             double tol, int max_iter, int *status) {
+  double root, lo, hi, f_lower = 0.0, f_upper = 0.0;
+  if (x_lo > x_hi) { *status |= OR_SOLVE_BAD_BRACKET; return 0.0; }
+  root = 0.5 * (x_lo + x_hi);
+  lo = x_lo; hi = x_hi;
+  {
+    double fl = MinimizeforLaunchAngle(m, lo, p);
+    if (!isfinite(fl)) { *status |= OR_SOLVE_NONFINITE_END; goto loop; }
+    double fu = MinimizeforLaunchAngle(m, hi, p);
+    if (!isfinite(fu)) { *status |= OR_SOLVE_NONFINITE_END; goto loop; }
+    f_lower = fl; f_upper = fu;
+  }
+loop:;
+  int iter = 0;
+  int cont;
+  double r = 0;
+  do {
+    iter++;
+    /* bisection_iterate */
+    if (f_lower == 0.0) { root = lo; hi = lo; }
+    else if (f_upper == 0.0) { root = hi; lo = hi; }
+    else {
+      double xb = (lo + hi) / 2.0;
+      double fb = MinimizeforLaunchAngle(m, xb, p);
+      if (!isfinite(fb)) {
+        *status |= OR_SOLVE_STALE_MID; /* EBADFUNC: no state change */
+      } else if (fb == 0.0) {
+        root = xb; lo = xb; hi = xb;
+      } else if ((f_lower > 0.0 && fb < 0.0) || (f_lower < 0.0 && fb > 0.0)) {
+        root = 0.5 * (lo + xb); hi = xb; f_upper = fb;
+      } else {
+        root = 0.5 * (xb + hi); lo = xb; f_lower = fb;
+      }
+    }
+    r = root;
+    /* gsl_root_test_interval(lo, hi, 0, tol) */
+    if (lo > hi) { cont = 0; }
+    else {
+      double min_abs = ((lo > 0.0 && hi > 0.0) || (lo < 0.0 && hi < 0.0))
+                           ? (fabs(lo) < fabs(hi) ? fabs(lo) : fabs(hi)) : 0;
+      double tolerance = 0 + tol * min_abs;
+      cont = !(fabs(hi - lo) < tolerance);
+    }
+  } while (cont && iter < max_iter);
+  if (cont) *status |= OR_SOLVE_MAXITER;
+  return r;
+}
+
+double or_straight_angle(const or_medium *m, double H, double D, double ice, double depth) {
+  double thR = 0;
+  if (depth < 0) thR = 180 - (atan(D / (H - ice - depth)) * (180.0 / m->pi));
+  if (depth >= 0) thR = 180 - (atan(D / (H - (ice + depth))) * (180.0 / m->pi));
+  return thR;
+}
+
+/* Bracket set-up shared by both variants (.cc:1472-1516, AirIceRayTracing.cc:937-987). */
+static double bracket_and_solve(const or_medium *m, double AirTxHeight, double HorizontalDistance,
+                                double *IceLayerHeight, double *AntennaDepth, double StraightAngle,
+                                minp *p, int *status) {
+  if (*AntennaDepth >= 0) {
+    *IceLayerHeight = *AntennaDepth + *IceLayerHeight;
+    *AntennaDepth = 0;
+    p->airtxheight = AirTxHeight; p->icelayerheight = *IceLayerHeight;
+    p->antennadepth = *AntennaDepth; p->horizontaldistance = HorizontalDistance;
+  }
+  if (*AntennaDepth < 0) {
+    p->airtxheight = AirTxHeight; p->icelayerheight = *IceLayerHeight;
+    p->antennadepth = -*AntennaDepth; p->horizontaldistance = HorizontalDistance;
+  }
+  double lo = StraightAngle - 16;
+  double hi = StraightAngle;
+  if (lo < 90.001) {
+    lo = 90.001;
+    int checknan = 0;
+    double out[5 * 8 + 2];
+    while (checknan == 0 && lo > 89.9) {
+      int nf = air_propagation(m, lo, AirTxHeight, *IceLayerHeight, out);
+      double s = 0;
+      for (int i = 0; i < nf; i++) s += out[i * 5];
+      if ((isnan(s) == 0 && s > 0) || lo > hi - 0.1) checknan = 1;
+      else { lo = lo + 0.05; *status |= OR_SOLVE_PROBED; }
+    }
+  }
+  if (hi < 90.001 && hi > 90.00) hi = 90.05;
+  return bisection_root(m, p, lo, hi, 0.000000001, 40, status);
+}
+
+/* Air2IceRayTracing (.cc:1464-1616) */
+int or_air2ice(const or_medium *m, double AirTxHeight, double HorizontalDistance,
+               double IceLayerHeight, double AntennaDepth, double StraightAngle, double dummy[17]) {
+  const double pi = m->pi;
+  int status = 0;
+  minp p;
+  double LaunchAngleAir = bracket_and_solve(m, AirTxHeight, HorizontalDistance, &IceLayerHeight,
+                                            &AntennaDepth, StraightAngle, &p, &status);
+  double out[5 * 8 + 2];
+  int nf = air_propagation(m, LaunchAngleAir, AirTxHeight, IceLayerHeight, out);
+  double thd_air = 0, t_air = 0, geo_air = 0;
+  for (int i = 0; i < nf; i++) { thd_air += out[i * 5]; t_air += out[3 + i * 5]; geo_air += out[4 + i * 5]; }
+  double L = nf > 0 ? out[2] : NAN;
+  double inc = nf > 0 ? out[1 + (nf - 1) * 5] : NAN;
+  if (nf == 0) status |= OR_SOLVE_NO_AIR_LAYER;
+  double thd_ice = 0, ant = 0, t_ice = 0, geo_ice = 0;
+  if (AntennaDepth < 0) {
+    double ic[5];
+    ice_propagation(m, IceLayerHeight, -AntennaDepth, L, ic);
+    thd_ice = ic[0]; ant = ic[1]; t_ice = ic[3]; geo_ice = ic[4];
+  }
+  double thd = thd_ice + thd_air;
+  double tt = t_ice + t_air;
+  dummy[0] = AirTxHeight;
+  dummy[1] = thd;
+  dummy[2] = thd_air;
+  dummy[3] = thd_ice;
+  dummy[4] = tt * SPEEDC;
+  dummy[5] = t_ice * SPEEDC;
+  dummy[6] = t_air * SPEEDC;
+  dummy[7] = tt;
+  dummy[8] = t_ice;
+  dummy[9] = t_air;
+  dummy[10] = LaunchAngleAir;
+  dummy[11] = ant;
+  dummy[12] = Trans_S(m, inc * (pi / 180.0), IceLayerHeight);
+  dummy[13] = Trans_P(m, inc * (pi / 180.0), IceLayerHeight);
+  dummy[14] = geo_air;
+  dummy[15] = geo_ice;
+  dummy[16] = inc;
+  return status;
+}
+
+void or_solve_batch(const or_medium *m, const double *txh, const double *dist, const double *depth,
+                    double ice_h, size_t n, double *out, size_t ld, uint8_t *status, int nthreads) {
+#ifdef _OPENMP
+  if (nthreads > 0) omp_set_num_threads(nthreads);
+#pragma omp parallel for schedule(dynamic, 16) if (nthreads > 0)
+#endif
+  for (long i = 0; i < (long)n; i++) {
+    double thR = or_straight_angle(m, txh[i], dist[i], ice_h, depth[i]);
+    double d[17];
+    int st = or_air2ice(m, txh[i], dist[i], ice_h, depth[i], thR, d);
+    for (int c = 0; c < 17; c++) out[c * ld + i] = d[c];
+    if (status) status[i] = (uint8_t)st;
+  }
+}
+
+/* GetHorizontalDistanceToIntersectionPoint (.cc:945-989) */
+int or_hdtip(const or_medium *m, double Src, double Dist, double Depth, double Ice, double o[9]) {
+  const double pi = m->pi;
+  double H = Src / 100, D = Dist / 100, I = Ice / 100, d = Depth / 100;
+  double thR = or_straight_angle(m, H, D, I, d);
+  double dm[17];
+  or_air2ice(m, H, D, I, d, thR, dm);
+  o[0] = dm[5] * 100;   /* opticalPathLengthInIce */
+  o[1] = dm[6] * 100;   /* opticalPathLengthInAir */
+  o[2] = dm[15] * 100;  /* geometricalPathLengthInIce */
+  o[3] = dm[14] * 100;  /* geometricalPathLengthInAir */
+  o[4] = dm[10] * (pi / 180);
+  o[5] = dm[2] * 100;
+  o[6] = dm[12];
+  o[7] = dm[13];
+  o[8] = dm[11] * (pi / 180);
+  int ok = 0;
+  if ((fabs(dm[1] - D) / D < 0.01 && D <= 100) || (fabs(dm[1] - D) < 1 && D > 100)) ok = 1;
+  if (dm[1] < 0) ok = 0;
+  return ok;
+}
+
+/* ------------------------------------------------------------------------- */
+/* pythonwrapper variant (pythonwrapper/AirIceRayTracing.cc, TraceIceToAir.C) */
+/* ------------------------------------------------------------------------- */
+int or_py_air2ice(const or_medium *m, double AirTxHeight, double HorizontalDistance,
+                  double IceLayerHeight, double AntennaDepth, double StraightAngle, double dummy[15]) {
+  const double pi = m->pi;
+  int status = 0;
+  minp p;
+  double LaunchAngleAir = bracket_and_solve(m, AirTxHeight, HorizontalDistance, &IceLayerHeight,
+                                            &AntennaDepth, StraightAngle, &p, &status);
+  double out[5 * 8 + 2];
+  int nf = air_propagation(m, LaunchAngleAir, AirTxHeight, IceLayerHeight, out);
+  double thd_air = 0, t_air = 0, geo_air = 0;
+  for (int i = 0; i < nf; i++) { thd_air += out[i * 5]; t_air += out[3 + i * 5]; geo_air += out[4 + i * 5]; }
+  double L = nf > 0 ? out[2] : NAN;
+  double inc = nf > 0 ? out[1 + (nf - 1) * 5] : NAN;
+  if (nf == 0) status |= OR_SOLVE_NO_AIR_LAYER;
+  double thd_ice = 0, ant = 0, t_ice = 0, geo_ice = 0;
+  if (AntennaDepth < 0) {
+    double ic[5];
+    ice_propagation(m, IceLayerHeight, -AntennaDepth, L, ic);
+    thd_ice = ic[0]; ant = ic[1]; t_ice = ic[3]; geo_ice = ic[4];
+  }
+  double thd = thd_ice + thd_air;
+  double tt = t_ice + t_air;
+  dummy[0] = AirTxHeight;
+  dummy[1] = thd;
+  dummy[2] = thd_air;
+  dummy[3] = thd_ice;
+  dummy[4] = tt * SPEEDC;
+  dummy[5] = t_ice * SPEEDC;
+  dummy[6] = t_air * SPEEDC;
+  dummy[7] = tt;
+  dummy[8] = t_ice;
+  dummy[9] = t_air;
+  dummy[10] = LaunchAngleAir;
+  dummy[11] = asin((or_getnz_air(m, IceLayerHeight) / or_getnz_ice(m, 0)) * sin(inc * (pi / 180))) * (180. / pi);
+  dummy[12] = ant;
+  dummy[13] = geo_air;
+  dummy[14] = geo_ice;
+  return status;
+}
+
+int or_py_trace_ice_to_air(const or_medium *m, double AntennaDepth, double IceLayerHeight,
+                           double AirTxHeight, double HorizontalDistance, double a[10]) {
+  /* GetRayTracingSolution (AirIceRayTracing.cc:884-927), metres */
+  double thR = or_straight_angle(m, AirTxHeight, HorizontalDistance, IceLayerHeight, AntennaDepth);
+  double dm[15];
+  int st = or_py_air2ice(m, AirTxHeight, HorizontalDistance, IceLayerHeight, AntennaDepth, thR, dm);
+  double geo_ice = dm[14], geo_air = dm[13];
+  double launch = dm[10], hd = dm[2], aoi = dm[11], recv = dm[12];
+  int ok = 0;
+  if ((fabs(dm[1] - HorizontalDistance) / HorizontalDistance < 0.01 && HorizontalDistance <= 100) ||
+      (fabs(dm[1] - HorizontalDistance) < 1 && HorizontalDistance > 100))
+    ok = 1;
+  if (dm[1] < 0) ok = 0;
+  /* TraceIceToAir.C:33-34: swap(launch, recv); recv = 180 - recv */
+  double t = launch; launch = recv; recv = t;
+  recv = 180 - recv;
+  if (ok) {
+    a[0] = AirTxHeight; a[1] = HorizontalDistance; a[2] = geo_ice; a[3] = geo_air;
+    a[4] = launch; a[5] = recv; a[6] = hd; a[7] = aoi; a[8] = 0; a[9] = 0;
+  } else {
+    for (int i = 0; i < 10; i++) a[i] = -1000;
+  }
+  (void)st;
+  return ok;
+}
+
+void or_py_trace_batch(const or_medium *m, const double *depth, const double *ice,
+                       const double *txh, const double *dist, size_t n, double *out10, int nthreads) {
+#ifdef _OPENMP
+  if (nthreads > 0) omp_set_num_threads(nthreads);
+#pragma omp parallel for schedule(dynamic, 16) if (nthreads > 0)
+#endif
+  for (long i = 0; i < (long)n; i++)
+    or_py_trace_ice_to_air(m, depth[i], ice[i], txh[i], dist[i], out10 + 10 * i);
+}

@@ -1,0 +1,118 @@
+/*
+ * airice_oracle.h -- TEST INFRASTRUCTURE ONLY.
+ *
+ * CPU restatement ("oracle") of the uzairlatif90/AirIceRayTracing hot path:
+ * MultiRayAirIceRefraction table rays + Air2Ice launch-angle bisection, and the
+ * pythonwrapper (AirIceRayTracing::) variant.  Only tests/, __graft_entry__.smoke()
+ * and bench.py's cpu_baseline leg may load this library, and only as the checker /
+ * CPU baseline.  The product path (airiceraytracing_amd/, libairice.so) never
+ * links or calls it.
+ *
+ * Parity status: the reference needs GNU GSL (absent from this image), so it is
+ * unbuildable here; the oracle is a restatement pinned by (a) scipy's natural
+ * cubic spline for the atmosphere N0, and (b) the known-answer values recorded in
+ * SURVEY.md §4 (see tests/golden/README.md for their provenance).
+ *
+ * Every function cites the reference file:line it restates.  Faithful mode: the
+ * call structure mirrors the reference (per-call layer scans, repeated libm calls),
+ * so its timing stands in for the reference CPU path.
+ */
+#ifndef AIRICE_ORACLE_H
+#define AIRICE_ORACLE_H
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Atmosphere + ice medium (MultiRayAirIceRefraction.h:57-81, .cc:24-213). */
+typedef struct or_medium {
+  double atmlay[5];    /* ATMLAY, cm (ATMLAY[4] forced to 1.5e7, .cc:66) */
+  double abc[5][3];    /* mass-overburden a,b,c (abc[4]=abc[3], .cc:62-64) */
+  double C_air[5];     /* .cc:198 */
+  double B_air[5];     /* .cc:200-205 */
+  double N0;           /* natural cubic spline n(h=0), .cc:203 */
+  int    max_layers;   /* |h_data|+1, .cc:142 */
+  int    n_points;     /* flattened spline knots */
+  int    layer_sizes[8];
+  double A_air;        /* .h:99 */
+  double A_ice, B_ice, C_ice;  /* .h:64-66 */
+  double pi;           /* 3.1415927 (MultiRay/RTF) or 4*atan(1) (pythonwrapper) */
+} or_medium;
+
+/* Status codes of one bisection solve (GSL 2.x bisection semantics). */
+enum {
+  OR_SOLVE_OK = 0,            /* bracket finite; loop ended on test_interval or max_iter */
+  OR_SOLVE_NONFINITE_END = 1, /* f(lo) or f(hi) non-finite: reference reads uninitialised
+                                 GSL state (UB) -> row unpinned; we model zeroed state */
+  OR_SOLVE_BAD_BRACKET = 2,   /* lo > hi: gsl_root_fsolver_set fails (UB downstream) */
+  OR_SOLVE_STALE_MID = 4,     /* a midpoint f was non-finite; root frozen (GSL EBADFUNC) */
+  OR_SOLVE_PROBED = 8,        /* the 0.05-degree bracket-probe loop ran (.cc:1490-1511) */
+  OR_SOLVE_MAXITER = 16,      /* 40 iterations without test_interval success */
+  OR_SOLVE_NO_AIR_LAYER = 32  /* no air layer between Tx and ice (reference reads out[-4]) */
+};
+
+/* Parse a GDAS Atmosphere.dat text image (readATMpar .cc:24-71, readnhFromFile
+ * .cc:73-147, flatten .cc:649, spline .cc:931-933, FillInAirRefractiveIndex .cc:193).
+ * pi selects the variant constant.  Returns 0 on success. */
+int or_parse_atmosphere(const char *text, size_t len, double pi, or_medium *m);
+int or_load_atmosphere(const char *path, double pi, or_medium *m);
+
+/* Natural cubic spline of the flattened profile evaluated at x (GSL cspline). */
+double or_spline_eval_at(const double *xa, const double *ya, int n, double x);
+
+/* Scalar pieces (exposed for unit tests). */
+double or_getnz_air(const or_medium *m, double z);
+double or_getnz_ice(const or_medium *m, double z);
+void   or_layer_hit_point_par(const or_medium *m, double n_layer1, double rx, double tx,
+                              double inc_deg, int air_or_ice, double out[5]);
+
+/* GetRayTracingSolutions (.cc:1796-2017): dummy[18]. */
+void or_ray_solution(const or_medium *m, double launch_deg, double txh, double ice_h,
+                     double depth, int in_ice, double dummy[18]);
+
+/* MakeRayTracingTable grid (.cc:12-21, 2019-2061). */
+typedef struct or_grid {
+  double start_height, stop_height, height_step;
+  int    height_steps;
+  double start_angle, stop_angle, angle_step;
+  int    angle_steps;
+  double depth_m, ice_m;
+  int    in_ice;
+} or_grid;
+void or_grid_init(or_grid *g, double depth_cm, double ice_cm, double height_step,
+                  double start_angle, double stop_angle, double angle_step);
+/* Rays [row0,row1) x all angles; table: 11 float columns (col stride = ld);
+ * full (nullable): 18 double columns (col stride = ld). nthreads<=0 -> serial. */
+void or_table_rows(const or_medium *m, const or_grid *g, int row0, int row1,
+                   float *table, double *full, size_t ld, int nthreads);
+
+/* Air2IceRayTracing (.cc:1464-1616): dummy[17], returns status bits. */
+int or_air2ice(const or_medium *m, double txh, double dist, double ice_h, double depth,
+               double straight_angle, double dummy[17]);
+/* thR of GetHorizontalDistanceToIntersectionPoint (.cc:952-958), metres. */
+double or_straight_angle(const or_medium *m, double txh, double dist, double ice_h, double depth);
+/* Batched minimizer over (txh, dist, depth) metres; out: 17 double columns (stride ld). */
+void or_solve_batch(const or_medium *m, const double *txh, const double *dist,
+                    const double *depth, double ice_h, size_t n, double *out, size_t ld,
+                    uint8_t *status, int nthreads);
+
+/* GetHorizontalDistanceToIntersectionPoint (.cc:945-989), cm in, outs[9], returns bool. */
+int or_hdtip(const or_medium *m, double src_cm, double dist_cm, double depth_cm,
+             double ice_cm, double outs[9]);
+
+/* pythonwrapper variant: AirIceRayTracing::Air2IceRayTracing (AirIceRayTracing.cc:929-1086),
+ * dummy[15]; TraceIceToAir (TraceIceToAir.C:5-73) -> ArrayParameters[10]. */
+int or_py_air2ice(const or_medium *m, double txh, double dist, double ice_h, double depth,
+                  double straight_angle, double dummy[15]);
+int or_py_trace_ice_to_air(const or_medium *m, double depth, double ice_h, double txh,
+                           double dist, double out10[10]);
+void or_py_trace_batch(const or_medium *m, const double *depth, const double *ice,
+                       const double *txh, const double *dist, size_t n, double *out10,
+                       int nthreads);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,94 @@
+"""Parity rule shared by the GPU tests and bench.py.
+
+|g - r| <= RTOL * max(|r|, floor_col), NaN positions identical, float table entries
+within 1 float32 ulp of the oracle's float(r).
+"""
+from __future__ import annotations
+
+import numpy as np
+
+RTOL = 1e-9  # north_star: outputs within 1e-9 relative of the CPU/GSL path
+
+# floors per dummy[] slot of GetRayTracingSolutions (.cc:1999-2016)
+RAY_FLOORS = np.array([1e-6, 1e-6, 1e-6, 1e-6, 1e-6, 1e-6, 1e-6, 1e-6,   # 0..7: m
+                       1e-6, 1e-6, 1e-6,                                 # 8..10: ns
+                       1e-9, 1e-9, 1e-9,                                 # 11..13: deg
+                       1e-9, 1e-9,                                       # 14..15: T_S, T_P
+                       1e-6, 1e-6])                                      # 16..17: m
+# floors per dummy[] slot of Air2IceRayTracing (.cc:1597-1614)
+SOLVE_FLOORS = np.array([1e-6, 1e-6, 1e-6, 1e-6, 1e-6, 1e-6, 1e-6,      # 0..6: m
+                         1e-15, 1e-15, 1e-15,                            # 7..9: s
+                         1e-9, 1e-9, 1e-9, 1e-9,                         # 10..13
+                         1e-6, 1e-6, 1e-9])                              # 14..16
+# pythonwrapper Air2IceRayTracing dummy[0..14] (AirIceRayTracing.cc:1070-1084)
+PYSOLVE_FLOORS = np.array([1e-6] * 7 + [1e-15] * 3 + [1e-9, 1e-9, 1e-9, 1e-6, 1e-6])
+TRACE_FLOORS = np.array([1e-6, 1e-6, 1e-6, 1e-6, 1e-9, 1e-9, 1e-6, 1e-9, 1e-9, 1e-9])
+HDTIP_FLOORS = np.array([1e-4, 1e-4, 1e-4, 1e-4, 1e-9, 1e-4, 1e-9, 1e-9, 1e-9])
+
+
+def compare_columns(gpu: np.ndarray, ref: np.ndarray, floors: np.ndarray, mask=None,
+                    rtol: float = RTOL):
+    """gpu/ref: (fields, n).  Returns a report dict; 'ok' is the verdict."""
+    gpu = np.asarray(gpu, dtype=np.float64)
+    ref = np.asarray(ref, dtype=np.float64)
+    if mask is not None:
+        gpu = gpu[:, mask]
+        ref = ref[:, mask]
+    nan_g, nan_r = np.isnan(gpu), np.isnan(ref)
+    nan_mismatch = int(np.count_nonzero(nan_g != nan_r))
+    inf_mismatch = int(np.count_nonzero(np.isinf(gpu) != np.isinf(ref)))
+    both = ~(nan_g | nan_r | np.isinf(gpu) | np.isinf(ref))
+    scale = np.maximum(np.abs(ref), floors[:, None])
+    err = np.where(both, np.abs(gpu - ref) / scale, 0.0)
+    absd = np.where(both, np.abs(gpu - ref), 0.0)
+    worst = float(err.max()) if err.size else 0.0
+    bad = err > rtol
+    rep = {
+        "n": int(ref.shape[1]),
+        "nan_mismatch": nan_mismatch,
+        "inf_mismatch": inf_mismatch,
+        "max_rel": worst,
+        "max_abs": float(absd.max()) if absd.size else 0.0,
+        "n_bad": int(np.count_nonzero(bad.any(axis=0))),
+        "bad_cols": sorted(set(np.nonzero(bad)[0].tolist())),
+        "max_rel_per_col": [float(x) for x in err.max(axis=1)] if err.size else [],
+    }
+    rep["ok"] = nan_mismatch == 0 and inf_mismatch == 0 and rep["n_bad"] == 0
+    return rep
+
+
+def float_ulp_diff(gpu: np.ndarray, ref: np.ndarray) -> int:
+    """Max distance in float32 ulps between two float32 arrays (NaN==NaN, NaN vs number = huge)."""
+    g = np.ascontiguousarray(gpu, dtype=np.float32)
+    r = np.ascontiguousarray(ref, dtype=np.float32)
+    ng, nr = np.isnan(g), np.isnan(r)
+    if np.any(ng != nr):
+        return 1 << 30
+    gi = g.view(np.int32).astype(np.int64)
+    ri = r.view(np.int32).astype(np.int64)
+    # map sign-magnitude to a monotone integer line
+    gi = np.where(gi < 0, -(gi & 0x7FFFFFFF), gi)
+    ri = np.where(ri < 0, -(ri & 0x7FFFFFFF), ri)
+    d = np.abs(gi - ri)
+    d[ng] = 0
+    return int(d.max()) if d.size else 0
+
+
+def cfg3_queries(n: int, seed: int = 12345):
+    """BASELINE cfg3: TxH~U(3001,1e5) m, D~U(0,5e4) m, depth~-U(0,300) m, ice 3000 m
+    (SURVEY.md §8(d)); mt19937_64 stream is replaced by numpy's PCG64 with the stated seed."""
+    rng = np.random.default_rng(seed)
+    txh = rng.uniform(3001.0, 100000.0, n)
+    dist = rng.uniform(0.0, 50000.0, n)
+    depth = -rng.uniform(0.0, 300.0, n)
+    return txh, dist, depth
+
+
+def cfg5_queries(n: int, seed: int = 777):
+    """BASELINE cfg5 (Py_TraceIceToAir): depth~-U(1,300), TxH~U(3001,20000), D~U(0,30000)."""
+    rng = np.random.default_rng(seed)
+    depth = -rng.uniform(1.0, 300.0, n)
+    txh = rng.uniform(3001.0, 20000.0, n)
+    dist = rng.uniform(0.0, 30000.0, n)
+    ice = np.full(n, 3000.0)
+    return depth, ice, txh, dist
