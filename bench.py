@@ -1,0 +1,234 @@
+#!/usr/bin/env python3
+"""bench.py -- solved air->ice rays/s of the MI355X table path (BASELINE.json metric).
+
+Workload (N=1): BASELINE cfg2 = MakeRayTracingTable on one MI355X, TxH 100000 -> 3000 m
+@ 20 m x launch angle 92 -> 180 deg @ 0.5 deg, antenna 200 m below the 3000 m ice surface:
+4,851 x 177 = 858,627 rays per step.  One step = one table build, i.e.
+one launch of table_kernel writing the 11 float columns of AllTableAllAntData into HBM.
+
+N>1 (torch.distributed.run, one process per GPU): weak scaling -- rank r builds the table
+of its own antenna (depth 200 + 10 r m), as the reference builds one table per antenna
+(RunMultiRayCode.C:29-52); no collective in the data path.  Timing: W untimed warm-up
+steps, then K steps bracketed by barrier + synchronize, max over ranks.
+
+Also reported: the minimizer (cfg3, 1e6 Air2IceRayTracing solves) as a secondary line item,
+the roofline of table_kernel (FP64 VALU bound), the CPU baseline (the oracle, OpenMP, on
+the box's host cores, on the same cfg2 grid) and max |delta| of the GPU table vs the CPU path.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+# FP64 VALU peak of one MI355X: 256 CU x 64 FP64 lane-ops/clk x 2.4 GHz (= 78.6 TFLOP/s with
+# FMA counted twice; MI355X spec FP64 vector rate).  Work is counted in lane-ops.
+PEAK_FP64_VALU_TOPS = 256 * 64 * 2.4e9 / 1e12
+CFG2 = dict(depth_cm=-20000.0, ice_cm=300000.0, height_step=20.0, start_angle=92.0,
+            stop_angle=180.0, angle_step=0.5)
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=50)
+    p.add_argument("--warmup", type=int, default=5)
+    p.add_argument("--solve-n", type=int, default=1_000_000)
+    p.add_argument("--solve-steps", type=int, default=5)
+    p.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
+    p.add_argument("--no-solve", action="store_true", help="skip the minimizer line item")
+    p.add_argument("--cpu-threads", type=int, default=16)
+    return p.parse_args()
+
+
+def load_opweights():
+    with open(os.path.join(ROOT, "tools", "opweights.json")) as f:
+        return json.load(f)
+
+
+def table_work_per_ray(grid, weights) -> tuple[float, dict]:
+    """Algorithmic FP64 VALU lane-ops per table ray: per-segment counts of
+    the CSE'd kernel x the number of segments of each ray of the grid, + per-ray terms."""
+    from tools.workmodel import segments_per_ray, ray_ops
+    segs = segments_per_ray(grid)
+    ops = ray_ops(segs, weights)
+    return ops["W"], {"mean_air_segments": segs["mean_air"], **ops}
+
+
+def pmc_traffic(kernel: str):
+    path = os.path.join(ROOT, "profiles", "pmc_summary.json")
+    try:
+        with open(path) as f:
+            d = json.load(f)
+        return d.get(kernel, {}).get("hbm_bytes_per_launch")
+    except (OSError, ValueError):
+        return None
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        dist.init_process_group(backend="nccl", device_id=torch.device(f"cuda:{local}"))
+    torch.cuda.set_device(local)
+    dev = torch.device(f"cuda:{local}")
+
+    from airiceraytracing_amd import AirIceSolver, make_grid
+    solver = AirIceSolver()
+    depth_cm = CFG2["depth_cm"] - 1000.0 * rank  # rank r: antenna at 200 + 10 r m
+    grid = make_grid(depth_cm, CFG2["ice_cm"], CFG2["height_step"], CFG2["start_angle"],
+                     CFG2["stop_angle"], CFG2["angle_step"])
+    n = grid.n_rays
+    table = torch.empty((11, n), dtype=torch.float32, device=dev)
+    stream = torch.cuda.current_stream()
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+
+    def step():
+        solver.table_device(grid, table, None, stream=stream)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    barrier()
+    torch.cuda.synchronize()
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+          for _ in range(args.steps)]
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        ev[i][0].record(stream)
+        step()
+        ev[i][1].record(stream)
+    torch.cuda.synchronize()
+    barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+    el = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(el, op=dist.ReduceOp.MAX)
+    elapsed = float(el.item())
+    total_rays = world * n * args.steps
+    value = total_rays / elapsed
+
+    # minimizer line item (cfg3: 1e6 random queries, ice 3000 m)
+    solve = None
+    if not args.no_solve:
+        from tests.parity import cfg3_queries
+        txh, dst, dep = cfg3_queries(args.solve_n, seed=12345 + rank)
+        tq = [torch.from_numpy(a).to(dev) for a in (txh, dst, dep)]
+        out = torch.empty((17, args.solve_n), dtype=torch.float64, device=dev)
+        stt = torch.empty(args.solve_n, dtype=torch.uint8, device=dev)
+        solver.solve_device(tq[0], tq[1], tq[2], 3000.0, out, stt, stream=stream)
+        torch.cuda.synchronize()
+        barrier()
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        t1 = time.perf_counter()
+        e0.record(stream)
+        for _ in range(args.solve_steps):
+            solver.solve_device(tq[0], tq[1], tq[2], 3000.0, out, stt, stream=stream)
+        e1.record(stream)
+        torch.cuda.synchronize()
+        barrier()
+        torch.cuda.synchronize()
+        se = torch.tensor([time.perf_counter() - t1], dtype=torch.float64, device=dev)
+        if world > 1:
+            dist.all_reduce(se, op=dist.ReduceOp.MAX)
+        solve = {
+            "metric": "Air2IceRayTracing solves/s (cfg3, 1e6 random queries per GPU)",
+            "value": world * args.solve_n * args.solve_steps / float(se.item()),
+            "unit": "solves/s",
+            "kernel_ms": e0.elapsed_time(e1) / args.solve_steps,
+            "solved_fraction": float((stt.cpu().numpy() & 3 == 0).mean()),
+        }
+
+    # parity of this step's table vs the CPU path + CPU baseline (rank 0, N=1 only)
+    cpu = None
+    parity_rep = None
+    if rank == 0 and world == 1 and not args.no_cpu:
+        import oracle
+        from tests import parity
+        om = oracle.load_atmosphere(os.path.join(ROOT, "airiceraytracing_amd", "data",
+                                                 "Atmosphere.dat.gz"))
+        og = oracle.grid_init(depth_cm, CFG2["ice_cm"], CFG2["height_step"], CFG2["start_angle"],
+                              CFG2["stop_angle"], CFG2["angle_step"])
+        nthr = max(1, min(args.cpu_threads, os.cpu_count() or 1))
+        c0 = time.perf_counter()
+        ot = oracle.table_rows(om, og, 0, og.height_steps, nthreads=nthr)
+        cdt = time.perf_counter() - c0
+        # 1-thread rate on a strided sample of rows
+        rows1 = list(range(0, og.height_steps, 97))
+        c1 = time.perf_counter()
+        for r in rows1:
+            oracle.table_rows(om, og, r, r + 1)
+        c1dt = time.perf_counter() - c1
+        cpu = {"value": og.height_steps * og.angle_steps / cdt, "unit": "rays/s", "cores": nthr,
+               "kind": "port",
+               "sample": f"full cfg2 grid ({og.height_steps * og.angle_steps} rays), oracle C "
+                         f"restatement, OpenMP {nthr} threads, gcc -O2; 1-thread "
+                         f"{len(rows1) * og.angle_steps / c1dt:.3e} rays/s on {len(rows1)} rows",
+               "seconds": cdt}
+        gt = table.cpu().numpy()
+        ulps = parity.float_ulp_diff(gt, ot)
+        finite = np.isfinite(ot) & np.isfinite(gt)
+        rel = np.abs(gt.astype(np.float64) - ot) / np.maximum(np.abs(ot.astype(np.float64)), 1e-30)
+        parity_rep = {"table_max_float_ulps": ulps,
+                      "table_max_abs": float(np.max(np.abs(gt - ot)[finite])),
+                      "table_max_rel": float(np.max(rel[finite])),
+                      "nan_pattern_equal": bool(np.array_equal(np.isnan(gt), np.isnan(ot)))}
+
+    weights = load_opweights()
+    W, work = table_work_per_ray(grid, weights)
+    achieved = n * W / (kern_ms * 1e-3) / 1e12
+    roof = {"bound": "valu", "kernel": "table_kernel", "achieved": achieved,
+            "peak": PEAK_FP64_VALU_TOPS, "unit": "TFLOP/s (FP64 VALU lane-ops/s x 1e-12)",
+            "frac": achieved / PEAK_FP64_VALU_TOPS, "traffic": pmc_traffic("table_kernel"),
+            "algorithmic_ops_per_ray": W, "rays_per_launch": n, "kernel_ms": kern_ms,
+            "hbm_bytes_per_launch_algorithmic": 44 * n}
+
+    if rank == 0:
+        line = {
+            "metric": "solved air->ice rays/sec (MakeRayTracingTable rays)",
+            "value": value,
+            "unit": "rays/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": elapsed / args.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic (BASELINE cfg2 grid) over the reference GDAS Atmosphere.dat",
+            "config": {"workload": "MakeRayTracingTable cfg2: TxH 100000->3000 m @20 m x "
+                                   "92->180 deg @0.5 deg, antenna 200 m below 3000 m ice",
+                       "rays_per_gpu_step": n, "table_columns": 11, "store": "f32",
+                       "parallelism": f"replicas{world} (one antenna table per GPU)"},
+            "roofline": roof,
+            "cpu_baseline": cpu,
+            "parity_vs_cpu": parity_rep,
+            "minimizer": solve,
+            "work_model": work,
+        }
+        print(json.dumps(line))
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()
