@@ -1,0 +1,23 @@
+#!/bin/bash
+# PMC passes (separate runs, --pmc only with --kernel-trace/--stats-free collection) for the
+# bench kernels and the ocml op-weight micro-kernels.  Writes gpurun_out/pmc/*.
+set -o pipefail
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+OUT=$R/gpurun_out/pmc
+mkdir -p $OUT
+export TMPDIR=/tmp
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -ffp-contract=off -o /tmp/opweights_bench $R/tools/opweights_bench.hip || exit 1
+cd /tmp
+P1="SQ_INSTS_VALU SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_TRANS_F64 SQ_WAVES"
+P2="SQ_ACTIVE_INST_VALU SQ_BUSY_CYCLES SQ_WAVE_CYCLES GRBM_GUI_ACTIVE SQ_WAVES"
+run() { # name, counters, cmd...
+  local name=$1; shift; local ctr=$1; shift
+  timeout -k 10 300 rocprofv3 --pmc $ctr -d $OUT/$name -o $name --output-format csv -- "$@" > $OUT/$name.log 2>&1 || { echo "pass $name failed rc=$?"; tail -5 $OUT/$name.log; return 1; }
+}
+run ow_a "$P1" /tmp/opweights_bench && \
+run bench_a "$P1" python $R/bench.py --no-cpu --steps 3 --warmup 1 --solve-steps 1 && \
+run bench_b "$P2" python $R/bench.py --no-cpu --steps 3 --warmup 1 --solve-steps 1 && \
+run bench_w "WRITE_SIZE" python $R/bench.py --no-cpu --steps 3 --warmup 1 --solve-steps 1 && \
+run bench_f "FETCH_SIZE" python $R/bench.py --no-cpu --steps 3 --warmup 1 --solve-steps 1 && \
+python $R/tools/pmc_summarize.py $OUT/opweights_pmc.json $OUT/ow_a && \
+python $R/tools/pmc_summarize.py $OUT/bench_pmc.json $OUT/bench_a $OUT/bench_b $OUT/bench_w $OUT/bench_f

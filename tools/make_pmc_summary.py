@@ -1,0 +1,49 @@
+"""Derive per-kernel metrics from the PMC passes (tools/gpu_pmc.sh) -> profiles/pmc_summary.json.
+
+HBM bytes follow MI355X_MICROARCH.md §HBM: WRITE_SIZE/FETCH_SIZE are KiB (x1024); FETCH_SIZE
+under-reports wide coalesced streaming reads by 2x on gfx950 -- the kernels here read only
+kernel arguments and <=24 B per query, so FETCH is reported both raw and doubled (upper bound).
+VALU busy uses the gfx9 formula 100*SQ_ACTIVE_INST_VALU*4/SIMDs/(GRBM_GUI_ACTIVE/XCDs).
+"""
+import json
+import sys
+
+SIMDS = 256 * 4
+XCDS = 8
+
+units = {"table_kernel": 858627, "solve_kernel<0>": 1000000}
+
+
+def derive(name, c, n_units, kernel_ns=None):
+    waves = c.get("SQ_WAVES", 0.0)
+    f64 = sum(c.get(k, 0.0) for k in ("SQ_INSTS_VALU_ADD_F64", "SQ_INSTS_VALU_MUL_F64",
+                                       "SQ_INSTS_VALU_FMA_F64", "SQ_INSTS_VALU_TRANS_F64"))
+    grbm = c.get("GRBM_GUI_ACTIVE", 0.0)
+    d = {
+        "units_per_launch": n_units,
+        "valu_insts_per_unit": c.get("SQ_INSTS_VALU", 0.0) * 64 / n_units,
+        "fp64_valu_insts_per_unit": f64 * 64 / n_units,
+        "fp64_fma_share": c.get("SQ_INSTS_VALU_FMA_F64", 0.0) / f64 if f64 else None,
+        "valu_busy_pct": 100 * c.get("SQ_ACTIVE_INST_VALU", 0.0) * 4 / SIMDS / (grbm / XCDS)
+        if grbm else None,
+        "waves": waves,
+        "write_bytes_per_launch": c.get("WRITE_SIZE", 0.0) * 1024,
+        "fetch_bytes_per_launch_raw": c.get("FETCH_SIZE", 0.0) * 1024,
+    }
+    d["hbm_bytes_per_launch"] = d["write_bytes_per_launch"] + 2 * d["fetch_bytes_per_launch_raw"]
+    return d
+
+
+if __name__ == "__main__":
+    src, dst = sys.argv[1], sys.argv[2]
+    with open(src) as f:
+        raw = json.load(f)
+    out = {"_source": "rocprofv3 --pmc passes of `python bench.py --no-cpu --steps 3` "
+                      "(tools/gpu_pmc.sh), mean per dispatch"}
+    for k, c in raw.items():
+        if k in units:
+            out[k.replace("<0>", "")] = {**derive(k, c, units[k]),
+                                         "raw": {a: b for a, b in c.items() if not a.startswith("_")}}
+    with open(dst, "w") as f:
+        json.dump(out, f, indent=1)
+    print(json.dumps(out, indent=1)[:3000])
