@@ -74,6 +74,7 @@ def build() -> str:
 
 
 _lib = None
+_FN = ctypes.CFUNCTYPE(ctypes.c_double, ctypes.c_double, ctypes.c_void_p)
 
 
 def lib():
@@ -98,6 +99,8 @@ def lib():
         L.or_table_rows.argtypes = [M, ctypes.POINTER(Grid), I, I, P, P, ctypes.c_size_t, I]
         L.or_air2ice.argtypes = [M, D, D, D, D, D, P]
         L.or_air2ice.restype = I
+        L.or_bisect.argtypes = [_FN, P, D, D, D, I, ctypes.POINTER(I)]
+        L.or_bisect.restype = D
         L.or_straight_angle.argtypes = [M, D, D, D, D]
         L.or_straight_angle.restype = D
         L.or_solve_batch.argtypes = [M, P, P, P, D, ctypes.c_size_t, P, ctypes.c_size_t, P, I]
@@ -170,6 +173,21 @@ def air2ice(m: Medium, txh, dist, ice_h, depth, straight_angle=None):
     out = np.zeros(17)
     st = lib().or_air2ice(ctypes.byref(m), txh, dist, ice_h, depth, straight_angle, _ptr(out))
     return out, st
+
+
+def bisect(fn, lo: float, hi: float, tol: float = 1e-9, max_iter: int = 40):
+    """GSL-bisection emulation (FindFunctionRoot, .cc:340-374) on a Python callable.
+    Returns (root, status bits, number of f evaluations)."""
+    calls = []
+
+    def cb(x, _ctx):
+        calls.append(x)
+        return float(fn(x))
+
+    cfn = _FN(cb)
+    st = ctypes.c_int(0)
+    r = lib().or_bisect(cfn, None, lo, hi, tol, max_iter, ctypes.byref(st))
+    return r, st.value, calls
 
 
 def straight_angle_of(m: Medium, txh, dist, ice_h, depth) -> float:

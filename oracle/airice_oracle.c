@@ -563,18 +563,21 @@ static double MinimizeforLaunchAngle(const or_medium *m, double x, const minp *p
   return (p->horizontaldistance - (thd_ice + thd_air));
 }
 
-/* FindFunctionRoot (.cc:340-374) with GSL bisection semantics.
- * Uninitialised-state cases are modelled as a zero-filled state. */
-static double bisection_root(const or_medium *m, const minp *p, double x_lo, double x_hi,
-                             double tol, int max_iter, int *status) {
+/* FindFunctionRoot (.cc:340-374) with GSL bisection semantics:
+ * gsl_root_fsolver_set (fsolver.c) + bisection_init/bisection_iterate (bisection.c) +
+ * gsl_root_test_interval(lo, hi, 0, tol) (convergence.c), loop while CONTINUE and
+ * iter < max_iter, return the last root.  Uninitialised-state cases (a non-finite
+ * endpoint) are modelled as a zero-filled state. */
+double or_bisect(or_fn f, void *ctx, double x_lo, double x_hi, double tol, int max_iter,
+                 int *status) {
   double root, lo, hi, f_lower = 0.0, f_upper = 0.0;
   if (x_lo > x_hi) { *status |= OR_SOLVE_BAD_BRACKET; return 0.0; }
   root = 0.5 * (x_lo + x_hi);
   lo = x_lo; hi = x_hi;
   {
-    double fl = MinimizeforLaunchAngle(m, lo, p);
+    double fl = f(lo, ctx);
     if (!isfinite(fl)) { *status |= OR_SOLVE_NONFINITE_END; goto loop; }
-    double fu = MinimizeforLaunchAngle(m, hi, p);
+    double fu = f(hi, ctx);
     if (!isfinite(fu)) { *status |= OR_SOLVE_NONFINITE_END; goto loop; }
     f_lower = fl; f_upper = fu;
   }
@@ -589,7 +592,7 @@ loop:;
     else if (f_upper == 0.0) { root = hi; lo = hi; }
     else {
       double xb = (lo + hi) / 2.0;
-      double fb = MinimizeforLaunchAngle(m, xb, p);
+      double fb = f(xb, ctx);
       if (!isfinite(fb)) {
         *status |= OR_SOLVE_STALE_MID; /* EBADFUNC: no state change */
       } else if (fb == 0.0) {
@@ -612,6 +615,17 @@ loop:;
   } while (cont && iter < max_iter);
   if (cont) *status |= OR_SOLVE_MAXITER;
   return r;
+}
+
+typedef struct { const or_medium *m; const minp *p; } minctx;
+static double min_cb(double x, void *c) {
+  const minctx *mc = (const minctx *)c;
+  return MinimizeforLaunchAngle(mc->m, x, mc->p);
+}
+static double bisection_root(const or_medium *m, const minp *p, double x_lo, double x_hi,
+                             double tol, int max_iter, int *status) {
+  minctx c = {m, p};
+  return or_bisect(min_cb, &c, x_lo, x_hi, tol, max_iter, status);
 }
 
 double or_straight_angle(const or_medium *m, double H, double D, double ice, double depth) {

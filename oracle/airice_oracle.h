@@ -91,6 +91,10 @@ void or_table_rows(const or_medium *m, const or_grid *g, int row0, int row1,
 /* Air2IceRayTracing (.cc:1464-1616): dummy[17], returns status bits. */
 int or_air2ice(const or_medium *m, double txh, double dist, double ice_h, double depth,
                double straight_angle, double dummy[17]);
+/* Generic GSL-bisection driver (FindFunctionRoot .cc:340-374), exposed for unit tests. */
+typedef double (*or_fn)(double x, void *ctx);
+double or_bisect(or_fn f, void *ctx, double x_lo, double x_hi, double tol, int max_iter,
+                 int *status);
 /* thR of GetHorizontalDistanceToIntersectionPoint (.cc:952-958), metres. */
 double or_straight_angle(const or_medium *m, double txh, double dist, double ice_h, double depth);
 /* Batched minimizer over (txh, dist, depth) metres; out: 17 double columns (stride ld). */
