@@ -80,10 +80,17 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        dist.init_process_group(backend="nccl", device_id=torch.device(f"cuda:{local}"))
-    torch.cuda.set_device(local)
-    dev = torch.device(f"cuda:{local}")
+    distributed = "RANK" in os.environ  # launched by torch.distributed.run (any world size)
+    backend = os.environ.get("AIRICE_DIST_BACKEND", "nccl")  # gloo: rehearsal ranks sharing a GPU
+    ndev = torch.cuda.device_count()
+    dev = torch.device(f"cuda:{local % max(1, ndev)}")
+    torch.cuda.set_device(dev)
+    if distributed:
+        if backend == "nccl":
+            dist.init_process_group(backend="nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend=backend)
+    coll_dev = dev if backend == "nccl" else torch.device("cpu")
 
     from airiceraytracing_amd import AirIceSolver, make_grid
     solver = AirIceSolver()
@@ -95,7 +102,7 @@ def main():
     stream = torch.cuda.current_stream()
 
     def barrier():
-        if world > 1:
+        if distributed:
             dist.barrier()
 
     def step():
@@ -118,8 +125,8 @@ def main():
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
-    el = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-    if world > 1:
+    el = torch.tensor([elapsed], dtype=torch.float64, device=coll_dev)
+    if distributed:
         dist.all_reduce(el, op=dist.ReduceOp.MAX)
     elapsed = float(el.item())
     total_rays = world * n * args.steps
@@ -146,8 +153,8 @@ def main():
         torch.cuda.synchronize()
         barrier()
         torch.cuda.synchronize()
-        se = torch.tensor([time.perf_counter() - t1], dtype=torch.float64, device=dev)
-        if world > 1:
+        se = torch.tensor([time.perf_counter() - t1], dtype=torch.float64, device=coll_dev)
+        if distributed:
             dist.all_reduce(se, op=dist.ReduceOp.MAX)
         solve = {
             "metric": "Air2IceRayTracing solves/s (cfg3, 1e6 random queries per GPU)",
@@ -226,7 +233,7 @@ def main():
             "work_model": work,
         }
         print(json.dumps(line))
-    if world > 1:
+    if distributed:
         dist.destroy_process_group()
 
 

@@ -1,0 +1,84 @@
+"""Sharding + gather of the table grid / query batches (airiceraytracing_amd/distributed.py)
+over gloo with world_size 2 on CPU; the per-shard compute is the oracle (no GPU here).  The
+assembled result must be bitwise equal to a single-process run."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from airiceraytracing_amd.distributed import shard_rows
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+@pytest.mark.parametrize("total,world", [(4851, 2), (4851, 8), (7, 8), (9701, 3), (1, 2)])
+def test_shard_rows_cover_exactly(total, world):
+    seen = []
+    per0 = None
+    for r in range(world):
+        b, c, per = shard_rows(total, world, r)
+        per0 = per if per0 is None else per0
+        assert per == per0 and 0 <= c <= per
+        seen.extend(range(b, b + c))
+    assert seen == list(range(total))
+
+
+def _worker(rank, world, port, q):
+    import oracle
+    from airiceraytracing_amd.distributed import queries_sharded, table_sharded
+    from tests.conftest import ATMOSPHERE_GZ
+    from tests.parity import cfg3_queries
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    m = oracle.load_atmosphere(ATMOSPHERE_GZ)
+    g = oracle.grid_init(-20000.0, 300000.0, 500.0, 92.0, 180.0, 2.0)
+
+    def tcompute(begin, count, out):
+        t = oracle.table_rows(m, g, begin, begin + count)
+        out[:, :t.shape[1]] = torch.from_numpy(t)
+
+    table = table_sharded(g, tcompute)
+    txh, dst, dep = cfg3_queries(301, seed=99)
+
+    def qcompute(begin, count, out):
+        o, _ = oracle.solve_batch(m, txh[begin:begin + count], dst[begin:begin + count],
+                                  dep[begin:begin + count], 3000.0)
+        out[:, :count] = torch.from_numpy(o)
+
+    sol = queries_sharded(301, qcompute, cols=17)
+    if rank == 0:
+        q.put((table.numpy(), sol.numpy()))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_gloo_world2_sharded_equals_single_process():
+    import oracle
+    from tests.conftest import ATMOSPHERE_GZ
+    from tests.parity import cfg3_queries
+    ctx = mp.get_context("spawn")
+    q = ctx.SimpleQueue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    table, sol = q.get()
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    m = oracle.load_atmosphere(ATMOSPHERE_GZ)
+    g = oracle.grid_init(-20000.0, 300000.0, 500.0, 92.0, 180.0, 2.0)
+    ref = oracle.table_rows(m, g, 0, g.height_steps)
+    assert table.shape == ref.shape
+    np.testing.assert_array_equal(table, ref)
+    txh, dst, dep = cfg3_queries(301, seed=99)
+    refq, _ = oracle.solve_batch(m, txh, dst, dep, 3000.0)
+    np.testing.assert_array_equal(sol, refq)
