@@ -1,18 +1,30 @@
 // airice_device.hpp -- FP64 device math of the air->ice ray solver (gfx950).
 //
-// One ray (table) or one query (minimizer) per lane.  Every expression keeps the
-// reference's evaluation order (MultiRayAirIceRefraction.cc:377-447 antiderivatives,
-// :521-646 segment, :661-869 propagation, :1796-2017 forward ray) and is compiled with
-// -ffp-contract=off, so device results differ from the CPU/GSL path only by the
-// ulp-level differences of ocml vs glibc transcendentals.
+// One ray (table) or one query (minimizer) per lane; FP64 throughout, compiled with
+// -ffp-contract=off.  The closed forms are those of the reference
+// (MultiRayAirIceRefraction.cc: fDnfR :377-386, ftimeD :412-431, fpathD :434-447,
+// GetLayerHitPointPar :521-646), evaluated with fewer operations; every rewrite below is an
+// exact identity whose only effect is ulp-level rounding (parity <= 1e-9 relative is checked
+// on the full BASELINE grids in tests/test_gpu_parity.py):
 //
-// What is NOT a translation: identical pure sub-expressions are computed once
-// (exp(C x) is shared by n(z), fDnfR, ftimeD, fpathD; sqrt(n^2-L^2) and the first
-// log are shared by fDnfR and ftimeD), and every endpoint that does not depend on
-// the ray (layer boundaries, the ice surface, the antenna depth of a table) is
-// evaluated once on the host and passed in the kernel-argument block (SGPRs), so
-// only the Tx endpoint needs device exp() -- the reference re-evaluates n(z) and
-// the layer scan ~hundreds of times per ray.
+//  (1) fpathD.  With y = A + B e^{Cx} and e^{2Cx} = (e^{Cx})^2 its radicand is
+//      Q = (A^2 + 2ABe + B^2e^2 - L^2)/y^2 = (y^2 - L^2)/y^2, so sqrt(Q) = s/y with
+//      s = sqrt(y^2 - L^2), and its two logarithms are log(y + s) (== ftimeD's log(n + s))
+//      and log(A y - L^2 + sqrt(A^2-L^2) s) (== fDnfR's log).  fpathD costs no extra
+//      transcendental; exp(2Cx) disappears.
+//  (2) sin(asin(u)) == u for |u| <= 1 (NaN otherwise).  The reference's per-layer chain
+//      angle -> sin -> asin -> sin -> asin -> sin -> degrees -> next layer collapses to one
+//      running sine v: L = n_Rx * v_Rx, v_next = v_Rx.  asin is evaluated only where an angle
+//      is an output (incidence on the ice, receive angle at the antenna).
+//  (3) Divisions by per-segment / per-layer constants become products with their reciprocal
+//      (1/sqrt(A^2-L^2) is already a factor of fDnfR; 1/C is precomputed per layer).
+//  (5) Both ends of every segment lie in one layer (same C), so F(R) - F(T) of each
+//      antiderivative needs log(a_R / a_T) instead of log(a_R) - log(a_T), and ftimeD's
+//      (n^2 - L^2)/sqrt(n^2 - L^2) term is sqrt(n^2 - L^2): per segment 2 logarithms instead
+//      of the reference's 12 (3 functions x 2 logs x 2 ends).
+//  (4) Endpoint quantities that do not depend on the ray (layer boundaries, the ice surface,
+//      a table's antenna depth) are evaluated once on the host and passed in the kernel-argument
+//      block (SGPRs / scalar cache); only the Tx endpoint costs a device exp().
 #pragma once
 #include <hip/hip_runtime.h>
 
@@ -20,12 +32,30 @@ namespace airice {
 
 constexpr int kMaxLayers = 4;  // ATMLAY has 5 bounds -> at most 4 air layers
 
-// One endpoint of a segment: the analytic antiderivatives need, at height/depth x,
-//   C = the "c" parameter (= -C_layer, .cc:455-461), B, e = exp(C x), e2 = exp(2 C x),
-//   y = A + B e (fDnfR/fpathD form) and n = Getnz(x) (ftimeD form; == y for x >= 0).
+// One end of a segment at height/depth x in a medium n(z) = A + B exp(C |z|) (C < 0 here:
+// C is the "c" parameter the reference passes, -C_layer, .cc:455-461).
+//   y = A + B exp(C x)   (fDnfR / fpathD form),   n = Getnz(x) = A + B exp(C |x|)  (ftimeD form)
 struct Endpoint {
-  double x, C, B, e, e2, y, n;
+  double x, C, invC, y, n;
+  double Ay, y2, n2, An, Cx, ACx;  // A*y, y*y, n*n, A*n, C*x, (A*C)*x
 };
+
+__host__ __device__ inline Endpoint make_endpoint(double A, double B, double C, double x,
+                                                  double e_abs, double e_x) {
+  Endpoint p;
+  p.x = x;
+  p.C = C;
+  p.invC = 1.0 / C;
+  p.n = A + B * e_abs;
+  p.y = (x >= 0.0) ? p.n : A + B * e_x;
+  p.Ay = A * p.y;
+  p.y2 = p.y * p.y;
+  p.n2 = p.n * p.n;
+  p.An = A * p.n;
+  p.Cx = C * x;
+  p.ACx = (A * C) * x;
+  return p;
+}
 
 struct DevMedium {
   double atm[5];    // ATMLAY[i]/100, m
@@ -46,10 +76,9 @@ struct IceConsts {
   Endpoint ice_air;    // air model at the ice height (stop of the lowest air layer)
   Endpoint ice0;       // ice model at depth 0 (.cc:1899)
   Endpoint ice_rx;     // ice model at the antenna depth (table: uniform)
-  double n1_over_n2;   // Getnz_air(ice)/Getnz_ice(0) (Trans_S/P, .cc:287-292)
 };
 
-__device__ __forceinline__ double sel4(const double (&a)[5], int l) {
+__device__ __forceinline__ double sel5(const double (&a)[5], int l) {
   double r = a[0];
   r = (l == 1) ? a[1] : r;
   r = (l == 2) ? a[2] : r;
@@ -69,157 +98,94 @@ __device__ __forceinline__ int air_layer(const DevMedium& M, double zabs) {
       found = true;
     }
   }
-  if (zabs >= sel4(M.atm, M.ml - 1)) which = M.ml - 1;
+  if (zabs >= sel5(M.atm, M.ml - 1)) which = M.ml - 1;
   return which;
 }
 
 __device__ __forceinline__ Endpoint air_endpoint(const DevMedium& M, double x) {
-  Endpoint p;
   const double zabs = fabs(x);
   const int l = air_layer(M, zabs);
-  p.x = x;
-  p.B = sel4(M.B, l);
-  p.C = sel4(M.negC, l);
-  const double eabs = exp(p.C * zabs);
-  p.n = M.A_air + p.B * eabs;
-  if (x >= 0.0) {
-    p.e = eabs;
-    p.y = p.n;
-  } else {
-    p.e = exp(p.C * x);
-    p.y = M.A_air + p.B * p.e;
-  }
-  p.e2 = exp(2 * p.C * x);
-  return p;
+  const double B = sel5(M.B, l), C = sel5(M.negC, l);
+  const double e_abs = exp(C * zabs);
+  const double e_x = (x >= 0.0) ? e_abs : exp(C * x);
+  return make_endpoint(M.A_air, B, C, x, e_abs, e_x);
 }
 
 __device__ __forceinline__ Endpoint ice_endpoint(const DevMedium& M, double x) {
-  Endpoint p;
   const double zabs = fabs(x);
-  p.x = x;
-  p.B = M.B_ice;
-  p.C = M.negC_ice;
-  const double eabs = exp(p.C * zabs);
-  p.n = M.A_ice + p.B * eabs;
-  if (x >= 0.0) {
-    p.e = eabs;
-    p.y = p.n;
-  } else {
-    p.e = exp(p.C * x);
-    p.y = M.A_ice + p.B * p.e;
-  }
-  p.e2 = exp(2 * p.C * x);
-  return p;
+  const double e_abs = exp(M.negC_ice * zabs);
+  const double e_x = (x >= 0.0) ? e_abs : exp(M.negC_ice * x);
+  return make_endpoint(M.A_ice, M.B_ice, M.negC_ice, x, e_abs, e_x);
 }
 
 __device__ __forceinline__ Endpoint pick(bool c, const Endpoint& a, const Endpoint& b) {
   Endpoint r;
   r.x = c ? a.x : b.x;
   r.C = c ? a.C : b.C;
-  r.B = c ? a.B : b.B;
-  r.e = c ? a.e : b.e;
-  r.e2 = c ? a.e2 : b.e2;
+  r.invC = c ? a.invC : b.invC;
   r.y = c ? a.y : b.y;
   r.n = c ? a.n : b.n;
+  r.Ay = c ? a.Ay : b.Ay;
+  r.y2 = c ? a.y2 : b.y2;
+  r.n2 = c ? a.n2 : b.n2;
+  r.An = c ? a.An : b.An;
+  r.Cx = c ? a.Cx : b.Cx;
+  r.ACx = c ? a.ACx : b.ACx;
   return r;
 }
 
-// Antiderivatives at one endpoint for a ray parameter L (sAL = sqrt(A*A-L*L), LL = L*L).
-// fDnfR .cc:385, ftimeD .cc:424/427, fpathD .cc:445 -- operand order kept.
-struct Prims {
-  double D, T, G;
+// sin(asin(u)): u on the domain of asin, NaN outside it (identity (2)).
+__device__ __forceinline__ double sin_asin(double u) { return (fabs(u) <= 1.0) ? u : __builtin_nan(""); }
+
+// Per-segment constants of the ray parameter L.
+struct RayL {
+  double L, LL, sAL, rsAL;  // L, L^2, sqrt(A^2-L^2), 1/sqrt(A^2-L^2)
 };
 
-__device__ __forceinline__ double prim_D(const Endpoint& P, double A, double L, double LL,
-                                         double sAL) {
-  const double s = sqrt(P.y * P.y - LL);
-  const double lg = log(A * P.y - LL + sAL * s);
-  return (L / P.C) * (1.0 / sAL) * (P.C * P.x - lg);
-}
-
-__device__ __forceinline__ Prims prim_all(const Endpoint& P, double A, double L, double LL,
-                                          double sAL, double speedc) {
-  Prims r;
-  // fDnfR
-  const double sy = sqrt(P.y * P.y - LL);
-  const double lgy = log(A * P.y - LL + sAL * sy);
-  const double Cx = P.C * P.x;
-  r.D = (L / P.C) * (1.0 / sAL) * (Cx - lgy);
-  // ftimeD: same sqrt/log when n == y (x >= 0)
-  double sn = sy, lgn = lgy;
-  if (P.n != P.y) {
-    sn = sqrt(P.n * P.n - LL);
-    lgn = log(A * P.n - LL + sAL * sn);
-  }
-  r.T = (1.0 / (speedc * P.C * sn)) *
-        (P.n * P.n - LL + (Cx - lgn) * (A * A * sn) / sAL + A * sn * log(P.n + sn));
-  // fpathD
-  const double Q = (A * A + 2 * A * P.B * P.e + P.B * P.B * P.e2 - LL) / (P.y * P.y);
-  const double sq = sqrt(Q);
-  r.G = (log(P.y * (sq + 1)) -
-         (A * log(A * sAL * sq + P.B * sAL * P.e * sq + A * A + A * P.B * P.e - LL)) / sAL +
-         (A * P.C * P.x) / sAL) /
-        P.C;
+__device__ __forceinline__ RayL ray_L(double A2, double L) {
+  RayL r;
+  r.L = L;
+  r.LL = L * L;
+  r.sAL = sqrt(A2 - r.LL);
+  r.rsAL = 1.0 / r.sAL;
   return r;
 }
 
 struct Segment {
-  double thd, recv_deg, L, t, geo;
+  double thd, t, geo;
 };
 
-// GetLayerHitPointPar (.cc:521-646): Tx endpoint T, Rx endpoint R, incoming index n1,
-// incidence angle in degrees.  air: results negated (.cc:464-466, 486-488, 508-510).
-__device__ __forceinline__ Segment segment_full(const DevMedium& M, double A, const Endpoint& T,
-                                                const Endpoint& R_, double n1, double inc_deg,
-                                                bool air) {
-  const double speedc = 299792458.0;
-  // Same height -> the reference evaluates the same function of the same x at both
-  // ends (zero-length segment, exactly 0 or NaN); endpoints built on host and device
-  // can differ by an ulp, so reuse one.
-  const Endpoint R = pick(R_.x == T.x, T, R_);
-  const double sria = inc_deg * M.d2r;
-  const double lang = asin((n1 / T.n) * sin(sria));
-  const double recv = asin((T.n * sin(lang)) / R.n);
-  const double L = R.n * sin(recv);
-  const double LL = L * L;
-  const double sAL = sqrt(A * A - LL);
-  const Prims pr = prim_all(R, A, L, LL, sAL, speedc);
-  const Prims pt = prim_all(T, A, L, LL, sAL, speedc);
-  Segment s;
-  s.thd = +pr.D - pt.D;
-  s.t = +pr.T - pt.T;
-  s.geo = pr.G - pt.G;
-  if (air) {
-    s.thd *= -1;
-    s.t *= -1;
-    s.geo *= -1;
-  }
-  s.recv_deg = recv * M.r2d;
-  s.L = L;
-  return s;
+// F(R) - F(T) for the three antiderivatives; air results negated (.cc:464-466, 486-488,
+// 508-510).  A segment whose ends are at the same height is exactly 0 (or NaN) in the
+// reference: the same function of the same x at both ends.  Endpoints built on the host
+// and on the device can differ by an ulp, so one endpoint is reused.
+__device__ __forceinline__ double log_ratio(double a, double b) {
+  // log(a) - log(b) as one logarithm when both are in log's domain (identity (5))
+  return (a > 0.0 && b > 0.0) ? log(a / b) : log(a) - log(b);
 }
 
-// Segment with a given L (GetAirPropagationPar lower layers .cc:757-771, GetIcePropagationPar
-// .cc:820-827): receive angle asin(L/n(Rx)).
-__device__ __forceinline__ Segment segment_with_L(const DevMedium& M, double A, const Endpoint& T,
-                                                  const Endpoint& R_, double L, bool air) {
+__device__ __forceinline__ Segment segment(const Endpoint& T, const Endpoint& R_, double A,
+                                           double A2, const RayL& RL, bool air) {
   const double speedc = 299792458.0;
-  const Endpoint R = pick(R_.x == T.x, T, R_);  // zero-length segment, see segment_full
-  const double LL = L * L;
-  const double sAL = sqrt(A * A - LL);
-  const Prims pr = prim_all(R, A, L, LL, sAL, speedc);
-  const Prims pt = prim_all(T, A, L, LL, sAL, speedc);
+  const Endpoint R = pick(R_.x == T.x, T, R_);
+  // Both ends lie in one layer (same C) at x >= 0 -- true of every segment the table and
+  // minimizer paths form (layer bounds come from the same scans; heights and depths are
+  // validated >= 0 at the API).  Identity (5): each antiderivative difference needs
+  // log(a_R/a_T) instead of two logarithms, and
+  // ftimeD = (s + A^2 (Cx - lg1)/sqrt(A^2-L^2) + A lg2) / (c C) since (n^2-L^2)/s = s.
   Segment s;
-  s.thd = +pr.D - pt.D;
-  s.t = +pr.T - pt.T;
-  s.geo = pr.G - pt.G;
+  const double syR = sqrt(R.y2 - RL.LL), syT = sqrt(T.y2 - RL.LL);
+  const double d1 = log_ratio(R.Ay - RL.LL + RL.sAL * syR, T.Ay - RL.LL + RL.sAL * syT);
+  const double d2 = log_ratio(R.n + syR, T.n + syT);
+  const double dCx = R.Cx - T.Cx;
+  s.thd = (RL.L * R.invC) * RL.rsAL * (dCx - d1);
+  s.t = ((syR - syT) + A2 * RL.rsAL * (dCx - d1) + A * d2) * (R.invC * (1.0 / speedc));
+  s.geo = (d2 - (A * d1) * RL.rsAL + (R.ACx - T.ACx) * RL.rsAL) * R.invC;
   if (air) {
     s.thd *= -1;
     s.t *= -1;
     s.geo *= -1;
   }
-  s.recv_deg = asin(L / R.n) * M.r2d;
-  s.L = L;
   return s;
 }
 
@@ -227,7 +193,7 @@ __device__ __forceinline__ Segment segment_with_L(const DevMedium& M, double A, 
 __device__ __forceinline__ int top_layer(const DevMedium& M, double txh) {
   int skip = 0;
   for (int il = M.ml; il > -1; il--) {
-    const bool hit = (txh < sel4(M.atm, il)) && (il >= 1 ? (txh >= sel4(M.atm, il - 1)) : false);
+    const bool hit = (txh < sel5(M.atm, il)) && (il >= 1 ? (txh >= sel5(M.atm, il - 1)) : false);
     if (hit) break;
     skip++;
   }
@@ -237,7 +203,7 @@ __device__ __forceinline__ int top_layer(const DevMedium& M, double txh) {
 __device__ __forceinline__ int bottom_layer(const DevMedium& M, double ice_h) {
   int skip = 0;
   for (int il = 0; il < M.ml; il++) {
-    if (ice_h >= sel4(M.atm, il) && ice_h < sel4(M.atm, il + 1)) break;
+    if (ice_h >= sel5(M.atm, il) && ice_h < sel5(M.atm, il + 1)) break;
     skip++;
   }
   return skip;
@@ -246,9 +212,9 @@ __device__ __forceinline__ int bottom_layer(const DevMedium& M, double ice_h) {
 // Fresnel amplitude transmission (.cc:285-337), thetai in radians.
 __device__ __forceinline__ void fresnel_trans(double n1, double n2, double thetai, double& tS,
                                               double& tP) {
-  const double a = (n1 / n2) * (sin(thetai));
+  const double st = sin(thetai), ct = cos(thetai);
+  const double a = (n1 / n2) * st;
   const double sqterm = sqrt(1 - a * a);
-  const double ct = cos(thetai);
   double num = n1 * ct - n2 * sqterm;
   double den = n1 * ct + n2 * sqterm;
   tS = 1 + (num / den);

@@ -4,10 +4,10 @@
 //                   (MultiRayAirIceRefraction.cc:2079-2122 loop body -> GetRayTracingSolutions
 //                   .cc:1796-2017), writes the 11 float table columns (.cc:2101-2111) and,
 //                   optionally, the 18 doubles of dummy[] for parity checks.
-//  rays_kernel    : same ray for arbitrary (angle, height) lists.
+//  rays_kernel    : the same ray for arbitrary (angle, height) lists.
 //  solve_kernel   : one lane per query of Air2IceRayTracing (.cc:1464-1616): bracket set-up,
 //                   the 0.05-degree probe loop, GSL-bisection emulation (tolerance 1e-9,
-//                   40 iterations) over a THD-only evaluator, and one full evaluation at the root.
+//                   40 iterations) over a THD-only evaluator, one full evaluation at the root.
 //                   VARIANT selects MultiRay (dummy[17]) / pythonwrapper (dummy[15]) outputs.
 //  hdtip_kernel   : GetHorizontalDistanceToIntersectionPoint (.cc:945-989), cm in/out.
 //  trace_kernel   : pythonwrapper TraceIceToAir (TraceIceToAir.C:5-73) rows of 10.
@@ -30,39 +30,46 @@ constexpr int kBlock = 256;
 
 // ---------------------------------------------------------------------------
 // Forward ray: GetRayTracingSolutions (.cc:1796-2017).  d[] = dummy[0..17].
+// The layer loop follows the reference (each layer re-derives L from the incidence angle
+// it receives, .cc:1871) with the running sine of identity (2).
 // ---------------------------------------------------------------------------
-struct RayOut {
-  double d[18];
-};
-
 __device__ __forceinline__ void ray_solution(const DevMedium& M, const IceConsts& I, double theta,
                                              double H, bool in_ice, int bot, double* d) {
   const int top = top_layer(M, H);
   const Endpoint tx = air_endpoint(M, H);
-  double start_angle = 0.0, thd_air = 0.0, t_air = 0.0, geo_air = 0.0;
+  const double A2 = M.A_air * M.A_air;
+  double v = sin((180 - theta) * M.d2r);  // sine of StartAngle (.cc:1863)
+  double thd_air = 0.0, t_air = 0.0, geo_air = 0.0;
 #pragma unroll
   for (int il = kMaxLayers - 1; il >= 0; --il) {
     if (il > top || il < bot) continue;
-    const bool first = (il == top);
-    const Endpoint T = pick(first, tx, M.start[il]);
+    const Endpoint T = pick(il == top, tx, M.start[il]);
     const Endpoint R = pick(il == bot, I.ice_air, M.stop[il]);
-    if (first) start_angle = 180 - theta;
-    // n_layer1 = Getnz_air(StartHeight) = T.n (.cc:1850, 1871)
-    const Segment s = segment_full(M, M.A_air, T, R, T.n, start_angle, true);
+    // n_layer1 == Getnz_air(StartHeight) == nzTx: Snell into the layer is the identity
+    const double v2 = sin_asin((T.n * sin_asin(v)) / R.n);
+    const RayL RL = ray_L(A2, R.n * v2);
+    const Segment s = segment(T, R, M.A_air, A2, RL, true);
     thd_air += s.thd;
-    start_angle = s.recv_deg;
     t_air += s.t;
     geo_air += s.geo;
+    v = v2;
   }
-  const double inc = start_angle;
+  // IncidentAngleonIce = last layer's receive angle; 0 when no air layer (.cc:1832, 1881)
+  const bool any = top >= bot;
+  const double inc = any ? asin(v) * M.r2d : 0.0;
+  const double vinc = any ? v : 0.0;
   double thd_ice = 0.0, t_ice = 0.0, geo_ice = 0.0, recv_ice = 0.0;
   if (in_ice) {
     // .cc:1897-1922: n_layer1 = Getnz_air(IceLayerHeight), Rx = -AntennaDepth, Tx = 0
-    const Segment s = segment_full(M, M.A_ice, I.ice0, I.ice_rx, I.ice_air.n, inc, false);
+    const double A2i = M.A_ice * M.A_ice;
+    const double u = sin_asin((I.ice_air.n / I.ice0.n) * vinc);
+    const double v2 = sin_asin((I.ice0.n * u) / I.ice_rx.n);
+    const RayL RL = ray_L(A2i, I.ice_rx.n * v2);
+    const Segment s = segment(I.ice0, I.ice_rx, M.A_ice, A2i, RL, false);
     thd_ice += s.thd;
     t_ice += s.t;
     geo_ice += s.geo;
-    recv_ice = s.recv_deg;
+    recv_ice = asin(v2) * M.r2d;
   }
   double tS, tP;
   fresnel_trans(I.ice_air.n, I.ice0.n, inc * M.d2r, tS, tP);
@@ -145,7 +152,8 @@ __global__ __launch_bounds__(kBlock) void rays_kernel(DevMedium M, IceConsts I,
 }
 
 // ---------------------------------------------------------------------------
-// Minimizer: per-query air path (GetAirPropagationPar .cc:661-804 semantics).
+// Minimizer: per-query air path (GetAirPropagationPar .cc:661-804 semantics: the first
+// layer derives L, the lower layers reuse it, .cc:757-771).
 // ---------------------------------------------------------------------------
 struct AirPath {
   Endpoint tx;      // Tx height endpoint
@@ -173,213 +181,323 @@ __device__ __forceinline__ AirPath make_air_path(const DevMedium& M, double H, d
   return P;
 }
 
-// L of the first layer (GetLayerHitPointPar .cc:562-589 with n_layer1 == nzTx).
-__device__ __forceinline__ double first_layer_L(const DevMedium& M, const AirPath& P, double theta) {
-  const double sria = (180 - theta) * M.d2r;
-  // (n_layer1/nzTx) is Getnz_air(Start)/Getnz_air(Start) == 1.0 exactly
-  const double lang = asin(sin(sria));
-  const double recv = asin((P.tx.n * sin(lang)) / P.rtop.n);
-  return P.rtop.n * sin(recv);
+// sin of the receive angle of the first layer (GetLayerHitPointPar .cc:562-589).
+__device__ __forceinline__ double first_layer_v2(const DevMedium& M, double n_tx, double n_rtop,
+                                                 double theta) {
+  const double v1 = sin((180 - theta) * M.d2r);
+  return sin_asin((n_tx * sin_asin(v1)) / n_rtop);
 }
 
-// Sum of per-layer horizontal distances in air for launch angle theta (THD only:
-// the time and geometric-path terms of the reference do not enter f).  Returns L0.
-__device__ __forceinline__ double air_thd(const DevMedium& M, const AirPath& P, double theta,
+// The four endpoint quantities fDnfR needs (prim_D): a bisection keeps only these in VGPRs.
+struct Slim {
+  double y2, Ay, Cx, invC;
+};
+
+__device__ __forceinline__ Slim slim(const Endpoint& p) { return Slim{p.y2, p.Ay, p.Cx, p.invC}; }
+
+__device__ __forceinline__ Slim pick(bool c, const Slim& a, const Slim& b) {
+  return Slim{c ? a.y2 : b.y2, c ? a.Ay : b.Ay, c ? a.Cx : b.Cx, c ? a.invC : b.invC};
+}
+
+// Slim air endpoint at x >= 0 (Tx heights and ice heights are non-negative; a negative x
+// would need y(x) != n(|x|), handled by the full Endpoint path).
+__device__ __forceinline__ Slim air_slim(const DevMedium& M, double x, double& n) {
+  const double zabs = fabs(x);
+  const int l = air_layer(M, zabs);
+  const double B = sel5(M.B, l), C = sel5(M.negC, l);
+  const double e_abs = exp(C * zabs);
+  n = M.A_air + B * e_abs;
+  const double y = (x >= 0.0) ? n : M.A_air + B * exp(C * x);
+  return Slim{y * y, M.A_air * y, C * x, 1.0 / C};
+}
+
+__device__ __forceinline__ Slim stop_slim(const DevMedium& M, int l) {
+  Slim r = slim(M.stop[0]);
+  r = pick(l == 1, slim(M.stop[1]), r);
+  r = pick(l == 2, slim(M.stop[2]), r);
+  r = pick(l == 3, slim(M.stop[3]), r);
+  return r;
+}
+
+__device__ __forceinline__ double stop_n(const DevMedium& M, int l) {
+  double r = M.stop[0].n;
+  r = (l == 1) ? M.stop[1].n : r;
+  r = (l == 2) ? M.stop[2].n : r;
+  r = (l == 3) ? M.stop[3].n : r;
+  return r;
+}
+
+
+// fDnfR(R) - fDnfR(T) with one logarithm when both ends share C (identity (5)).
+__device__ __forceinline__ double delta_D(const Slim& T, const Slim& R, const RayL& RL) {
+  const double syR = sqrt(R.y2 - RL.LL), syT = sqrt(T.y2 - RL.LL);
+  const double d1 = log_ratio(R.Ay - RL.LL + RL.sAL * syR, T.Ay - RL.LL + RL.sAL * syT);
+  return (RL.L * R.invC) * RL.rsAL * ((R.Cx - T.Cx) - d1);
+}
+
+// Per-query state of the root finder (MinforLAng_params + the air path's endpoints).
+struct Query {
+  Slim tx, rtop, iceair, rx;
+  double n_tx, n_rtop;
+  int top, bot;
+  double dist;
+  double depth_pos;  // MinforLAng_params.antennadepth (> 0 in ice, 0 in air)
+};
+
+// Sum of per-layer horizontal distances in air for launch angle theta (THD only: the time
+// and geometric-path terms do not enter f).  Returns L0 through the reference.
+__device__ __forceinline__ double air_thd(const DevMedium& M, const Query& q, double theta,
                                           double& L0) {
-  if (P.top < P.bot) {  // no layer: reference reads unset output slots (UB)
+  if (q.top < q.bot) {  // no layer: the reference reads unset output slots (UB)
     L0 = __builtin_nan("");
     return 0.0;
   }
-  const double L = first_layer_L(M, P, theta);
+  const double L = q.n_rtop * first_layer_v2(M, q.n_tx, q.n_rtop, theta);
   L0 = L;
-  const double LL = L * L;
-  const double sAL = sqrt(M.A_air * M.A_air - LL);
+  const RayL RL = ray_L(M.A_air * M.A_air, L);
   double thd = 0.0;
-#pragma unroll
+#pragma unroll 1
   for (int il = kMaxLayers - 1; il >= 0; --il) {
-    if (il > P.top || il < P.bot) continue;
-    const Endpoint T = pick(il == P.top, P.tx, M.start[il]);
-    const Endpoint R = pick(il == P.top, P.rtop, pick(il == P.bot, P.iceair, M.stop[il]));
-    double x1 = +prim_D(R, M.A_air, L, LL, sAL) - prim_D(T, M.A_air, L, LL, sAL);
+    if (il > q.top || il < q.bot) continue;
+    const Slim T = pick(il == q.top, q.tx, slim(M.start[il]));
+    const Slim R = pick(il == q.top, q.rtop, pick(il == q.bot, q.iceair, slim(M.stop[il])));
+    double x1 = delta_D(T, R, RL);
     x1 *= -1;
     thd += x1;
   }
   return thd;
 }
 
-struct Query {
-  AirPath P;
-  Endpoint rx;      // ice endpoint at the antenna depth (if in ice)
-  double dist;
-  double depth_pos; // MinforLAng_params.antennadepth (> 0 in ice, 0 in air)
+// ---------------------------------------------------------------------------
+// Air2IceRayTracing (.cc:1464-1616) in two launches: stage 1 finds the launch angle
+// (bracket, probe, bisection) keeping only the slim per-query state live; stage 2 rebuilds
+// the full endpoints and evaluates every output at the root.  Splitting keeps the
+// register-hungry full evaluation out of the bisection kernel's allocation.  Stage 1 parks
+// the root and status in output slots that stage 2 overwrites.
+// ---------------------------------------------------------------------------
+struct Geometry {
+  double H, D, ice, depth;  // after the Rx-in-air shift (.cc:1472-1479)
+  double depth_pos;         // MinforLAng_params.antennadepth
 };
 
-// MinimizeforLaunchAngle (.cc:873-917)
-__device__ __forceinline__ double fmin_eval(const DevMedium& M, const IceConsts& I, const Query& q,
-                                            double x) {
-  double L;
-  const double thd_air = air_thd(M, q.P, x, L);
-  double thd_ice = 0;
-  if (q.depth_pos != 0) {
-    const double LL = L * L;
-    const double sAL = sqrt(M.A_ice * M.A_ice - LL);
-    thd_ice += +prim_D(q.rx, M.A_ice, L, LL, sAL) - prim_D(I.ice0, M.A_ice, L, LL, sAL);
+__device__ __forceinline__ Geometry shift(double H, double D, double ice, double depth) {
+  Geometry g;
+  g.H = H;
+  g.D = D;
+  if (depth >= 0) {
+    g.ice = depth + ice;
+    g.depth = 0;
+    g.depth_pos = 0;
+  } else {
+    g.ice = ice;
+    g.depth = depth;
+    g.depth_pos = -depth;
   }
-  return (q.dist - (thd_ice + thd_air));
+  return g;
 }
 
+// Root finding of Air2IceRayTracing (.cc:1487-1521): the probe loop, gsl_root_fsolver_set
+// and the FindFunctionRoot driver (.cc:340-374) with gsl_root_fsolver_bisection +
+// gsl_root_test_interval(lo, hi, 0, 1e-9) semantics, as one per-lane state machine with a
+// single evaluation site: lanes that are probing, setting up the bracket or bisecting share
+// each evaluation instead of waiting for each other (the probe runs in ~7% of queries).
+// An uninitialised solver state (non-finite bracket end) is modelled as zeros.
 struct SolveResult {
   double root;
   int status;
 };
 
-// FindFunctionRoot (.cc:340-374) with gsl_root_fsolver_bisection + gsl_root_test_interval
-// semantics; an uninitialised solver state (non-finite endpoint) is modelled as zeros.
-__device__ __forceinline__ SolveResult bisect(const DevMedium& M, const IceConsts& I,
-                                              const Query& q, double x_lo, double x_hi) {
-  SolveResult res{0.0, 0};
-  if (x_lo > x_hi) {
-    res.status |= AIRICE_SOLVE_BAD_BRACKET;
-    return res;
+enum { PH_PROBE = 0, PH_FLO = 1, PH_FHI = 2, PH_BISECT = 3, PH_DONE = 4 };
+
+__device__ __forceinline__ SolveResult solve_root(const DevMedium& M, const IceConsts& I,
+                                                  const Geometry& g, double thR) {
+  int status = 0;
+  Query q;
+  q.depth_pos = g.depth_pos;
+  q.dist = g.D;
+  q.top = top_layer(M, g.H);
+  q.bot = bottom_layer(M, g.ice);
+  q.tx = air_slim(M, g.H, q.n_tx);
+  double n_ice;
+  q.iceair = air_slim(M, g.ice, n_ice);
+  // Rx end of the top layer: the ice, or the layer's lower boundary (stop endpoint)
+  const bool to_ice = q.top == q.bot;
+  q.rtop = pick(to_ice, q.iceair, stop_slim(M, q.top));
+  q.n_rtop = to_ice ? n_ice : stop_n(M, q.top);
+  const double x_rtop = to_ice ? g.ice : sel5(M.atm, q.top);
+  if (x_rtop == g.H) {  // zero-length top segment (see segment())
+    q.rtop = q.tx;
+    q.n_rtop = q.n_tx;
   }
-  double lo = x_lo, hi = x_hi;
-  double root = 0.5 * (x_lo + x_hi);
-  double f_lower = 0.0, f_upper = 0.0;
-  const double fl = fmin_eval(M, I, q, lo);
-  if (!isfinite(fl)) {
-    res.status |= AIRICE_SOLVE_NONFINITE_END;
-  } else {
-    const double fu = fmin_eval(M, I, q, hi);
-    if (!isfinite(fu)) {
-      res.status |= AIRICE_SOLVE_NONFINITE_END;
-    } else {
-      f_lower = fl;
-      f_upper = fu;
-    }
+  {
+    const double e = exp(M.negC_ice * g.depth_pos);
+    const double y = M.A_ice + M.B_ice * e;
+    q.rx = Slim{y * y, M.A_ice * y, M.negC_ice * g.depth_pos, 1.0 / M.negC_ice};
   }
-  const double tol = 0.000000001;
-  bool cont = true;
-  for (int iter = 1; iter <= 40 && cont; ++iter) {
-    if (f_lower == 0.0) {
-      root = lo;
-      hi = lo;
-    } else if (f_upper == 0.0) {
-      root = hi;
-      lo = hi;
-    } else {
-      const double xb = (lo + hi) / 2.0;
-      const double fb = fmin_eval(M, I, q, xb);
-      if (!isfinite(fb)) {
-        // EBADFUNC leaves the state unchanged: every later iterate repeats this one,
-        // so the driver ends at max_iter with the same root.
-        res.status |= AIRICE_SOLVE_STALE_MID | AIRICE_SOLVE_MAXITER;
-        break;
-      } else if (fb == 0.0) {
-        root = xb;
-        lo = xb;
-        hi = xb;
-      } else if ((f_lower > 0.0 && fb < 0.0) || (f_lower < 0.0 && fb > 0.0)) {
-        root = 0.5 * (lo + xb);
-        hi = xb;
-        f_upper = fb;
-      } else {
-        root = 0.5 * (xb + hi);
-        lo = xb;
-        f_lower = fb;
+
+  double lo = thR - 16;
+  double hi = thR;
+  int phase = PH_FLO;
+  if (lo < 90.001) {
+    lo = 90.001;
+    phase = PH_PROBE;
+    // While n(Tx) sin(180-lo) exceeds 1 by a margin (1e-6) the ray parameter L > A_air = 1,
+    // so sqrt(A^2-L^2) and THD are NaN whatever the rounding: those probe steps need no
+    // evaluation (.cc:1496-1509 would reject each of them).
+    if (q.top >= q.bot) {
+      const double thr = 180 - asin((1 + 1e-6) / q.n_tx) * M.r2d;  // NaN if n(Tx) < 1+1e-6
+      while (lo < thr && !(lo > hi - 0.1)) {
+        lo = lo + 0.05;
+        status |= AIRICE_SOLVE_PROBED;
       }
     }
-    if (lo > hi) {
-      cont = false;
-    } else {
-      const double min_abs = ((lo > 0.0 && hi > 0.0) || (lo < 0.0 && hi < 0.0))
-                                 ? (fabs(lo) < fabs(hi) ? fabs(lo) : fabs(hi))
-                                 : 0.0;
-      const double tolerance = 0 + tol * min_abs;
-      cont = !(fabs(hi - lo) < tolerance);
+  } else {
+    if (hi < 90.001 && hi > 90.00) hi = 90.05;
+    if (lo > hi) {  // gsl_root_fsolver_set: EINVAL, nothing initialised
+      status |= AIRICE_SOLVE_BAD_BRACKET;
+      phase = PH_DONE;
     }
-    if (cont && iter == 40) res.status |= AIRICE_SOLVE_MAXITER;
   }
-  res.root = root;
-  return res;
+  double root = 0.5 * (lo + hi);
+  double f_lower = 0.0, f_upper = 0.0, f_lo_set = 0.0;
+  const double tol = 0.000000001;
+  int iter = 0;
+  while (phase != PH_DONE) {
+    const bool shortcut = phase == PH_BISECT && (f_lower == 0.0 || f_upper == 0.0);
+    const double x = (phase == PH_FHI) ? hi : (phase == PH_BISECT) ? (lo + hi) / 2.0 : lo;
+    double thd_air = 0.0, f = 0.0;
+    if (!shortcut) {  // the single evaluation site: MinimizeforLaunchAngle (.cc:873-917)
+      double L;
+      thd_air = air_thd(M, q, x, L);
+      double thd_ice = 0;
+      if (q.depth_pos != 0) {
+        const RayL RL = ray_L(M.A_ice * M.A_ice, L);
+        thd_ice += delta_D(slim(I.ice0), q.rx, RL);
+      }
+      f = (q.dist - (thd_ice + thd_air));
+    }
+    if (phase == PH_PROBE) {
+      if ((!isnan(thd_air) && thd_air > 0) || lo > hi - 0.1) {
+        if (hi < 90.001 && hi > 90.00) hi = 90.05;
+        root = 0.5 * (lo + hi);
+        phase = PH_FLO;
+        if (lo > hi) {
+          status |= AIRICE_SOLVE_BAD_BRACKET;
+          root = 0.0;
+          phase = PH_DONE;
+        }
+      } else {
+        lo = lo + 0.05;
+        status |= AIRICE_SOLVE_PROBED;
+      }
+    } else if (phase == PH_FLO) {
+      if (!isfinite(f)) {
+        status |= AIRICE_SOLVE_NONFINITE_END;
+        phase = PH_BISECT;
+      } else {
+        f_lo_set = f;
+        phase = PH_FHI;
+      }
+    } else if (phase == PH_FHI) {
+      if (!isfinite(f)) {
+        status |= AIRICE_SOLVE_NONFINITE_END;
+      } else {
+        f_lower = f_lo_set;
+        f_upper = f;
+      }
+      phase = PH_BISECT;
+    } else {  // PH_BISECT: one gsl_root_fsolver_iterate + gsl_root_test_interval
+      ++iter;
+      bool frozen = false;
+      if (f_lower == 0.0) {
+        root = lo;
+        hi = lo;
+      } else if (f_upper == 0.0) {
+        root = hi;
+        lo = hi;
+      } else if (!isfinite(f)) {
+        // EBADFUNC leaves the state unchanged: every later iterate repeats this one, so the
+        // driver ends at max_iter with the same root.
+        status |= AIRICE_SOLVE_STALE_MID | AIRICE_SOLVE_MAXITER;
+        frozen = true;
+      } else if (f == 0.0) {
+        root = x;
+        lo = x;
+        hi = x;
+      } else if ((f_lower > 0.0 && f < 0.0) || (f_lower < 0.0 && f > 0.0)) {
+        root = 0.5 * (lo + x);
+        hi = x;
+        f_upper = f;
+      } else {
+        root = 0.5 * (x + hi);
+        lo = x;
+        f_lower = f;
+      }
+      bool cont;
+      if (lo > hi) {
+        cont = false;
+      } else {
+        const double min_abs = ((lo > 0.0 && hi > 0.0) || (lo < 0.0 && hi < 0.0))
+                                   ? (fabs(lo) < fabs(hi) ? fabs(lo) : fabs(hi))
+                                   : 0.0;
+        const double tolerance = 0 + tol * min_abs;
+        cont = !(fabs(hi - lo) < tolerance);
+      }
+      if (cont && iter == 40) status |= AIRICE_SOLVE_MAXITER;
+      if (frozen || !cont || iter == 40) phase = PH_DONE;
+    }
+  }
+  return SolveResult{root, status};
 }
 
 struct Solved {
   double launch, thd_air, t_air, geo_air, inc, thd_ice, t_ice, geo_ice, ant;
-  double ice_h;  // IceLayerHeight after the Rx-in-air shift
+  double ice_n;  // Getnz_air(IceLayerHeight) after the Rx-in-air shift
   int status;
 };
 
-// Air2IceRayTracing (.cc:1464-1616) up to the outputs.
-__device__ __forceinline__ Solved air2ice(const DevMedium& M, const IceConsts& I, double H,
-                                          double D, double ice, double depth, double thR) {
+// Outputs at the root (GetAirPropagationPar + GetIcePropagationPar, .cc:1524-1566).
+__device__ __forceinline__ Solved evaluate_root(const DevMedium& M, const IceConsts& I,
+                                                const Geometry& g, double x, int status) {
   Solved S;
-  S.status = 0;
-  Query q;
-  if (depth >= 0) {
-    ice = depth + ice;
-    depth = 0;
-    q.depth_pos = depth;
-  } else {
-    q.depth_pos = -depth;
-  }
-  q.dist = D;
-  q.P = make_air_path(M, H, ice);
-  q.rx = ice_endpoint(M, q.depth_pos);
-  S.ice_h = ice;
-
-  double lo = thR - 16;
-  double hi = thR;
-  if (lo < 90.001) {
-    lo = 90.001;
-    bool checknan = false;
-    while (!checknan && lo > 89.9) {
-      double Ld;
-      const double s = air_thd(M, q.P, lo, Ld);
-      if ((!isnan(s) && s > 0) || lo > hi - 0.1) {
-        checknan = true;
-      } else {
-        lo = lo + 0.05;
-        S.status |= AIRICE_SOLVE_PROBED;
-      }
-    }
-  }
-  if (hi < 90.001 && hi > 90.00) hi = 90.05;
-  const SolveResult r = bisect(M, I, q, lo, hi);
-  S.status |= r.status;
-  const double x = r.root;
+  S.status = status;
   S.launch = x;
-
-  // Final evaluation (GetAirPropagationPar + GetIcePropagationPar, .cc:1524-1566).
+  const AirPath P = make_air_path(M, g.H, g.ice);
+  S.ice_n = P.iceair.n;
   S.thd_air = 0.0;
   S.t_air = 0.0;
   S.geo_air = 0.0;
   S.inc = __builtin_nan("");
   double L0 = __builtin_nan("");
-  const AirPath& P = q.P;
-  if (P.top < P.bot) S.status |= AIRICE_SOLVE_NO_AIR_LAYER;
-  for (int il = P.top; il > P.bot - 1; --il) {
-    Segment sg;
-    if (il == P.top) {
-      sg = segment_full(M, M.A_air, P.tx, P.rtop, P.tx.n, 180 - x, true);
-      L0 = sg.L;
-    } else {
-      const Endpoint T = M.start[il];
-      const Endpoint R = pick(il == P.bot, P.iceair, stop_of(M, il));
-      sg = segment_with_L(M, M.A_air, T, R, L0, true);
+  if (P.top < P.bot) {
+    S.status |= AIRICE_SOLVE_NO_AIR_LAYER;
+  } else {
+    const double v2 = first_layer_v2(M, P.tx.n, P.rtop.n, x);
+    L0 = P.rtop.n * v2;
+    const double A2 = M.A_air * M.A_air;
+    const RayL RL = ray_L(A2, L0);
+    for (int il = P.top; il > P.bot - 1; --il) {
+      const Endpoint T = (il == P.top) ? P.tx : M.start[il];
+      const Endpoint R = (il == P.top) ? P.rtop : ((il == P.bot) ? P.iceair : M.stop[il]);
+      const Segment sg = segment(T, R, M.A_air, A2, RL, true);
+      S.thd_air += sg.thd;
+      S.t_air += sg.t;
+      S.geo_air += sg.geo;
     }
-    S.thd_air += sg.thd;
-    S.t_air += sg.t;
-    S.geo_air += sg.geo;
-    S.inc = sg.recv_deg;
+    // receive angle of the last layer: asin(v2) for the first layer, asin(L0/n(Stop)) below
+    S.inc = asin(P.top == P.bot ? v2 : L0 / P.iceair.n) * M.r2d;
   }
   S.thd_ice = 0.0;
   S.t_ice = 0.0;
   S.geo_ice = 0.0;
   S.ant = 0.0;
-  if (depth < 0) {
-    const Segment sg = segment_with_L(M, M.A_ice, I.ice0, q.rx, L0, false);
+  if (g.depth < 0) {
+    const Endpoint rx = ice_endpoint(M, g.depth_pos);
+    const double A2i = M.A_ice * M.A_ice;
+    const RayL RL = ray_L(A2i, L0);
+    const Segment sg = segment(I.ice0, rx, M.A_ice, A2i, RL, false);
     S.thd_ice = sg.thd;
-    S.ant = sg.recv_deg;
+    S.ant = asin(L0 / rx.n) * M.r2d;
     S.t_ice = sg.t;
     S.geo_ice = sg.geo;
   }
@@ -394,24 +512,89 @@ __device__ __forceinline__ double straight_angle(const DevMedium& M, double H, d
   return thR;
 }
 
-template <int VARIANT>
-__global__ __launch_bounds__(kBlock) void solve_kernel(DevMedium M, IceConsts I,
-                                                       const double* __restrict__ txh,
-                                                       const double* __restrict__ dist,
-                                                       const double* __restrict__ depth,
-                                                       const double* __restrict__ thr_in,
-                                                       long long n, double* __restrict__ out,
-                                                       size_t ld, uint8_t* __restrict__ status) {
+// Query sources.  IN_M: metres, uniform ice (Air2IceRayTracing batch); IN_CM: centimetres
+// (GetHorizontalDistanceToIntersectionPoint, .cc:947-950); IN_TRACE: per-query ice, metres
+// (TraceIceToAir).
+enum { IN_M = 0, IN_CM = 1, IN_TRACE = 2 };
+
+struct QueryArgs {
+  const double* a;    // IN_M: txh    IN_CM: src_cm   IN_TRACE: depth
+  const double* b;    //       dist          dist_cm            ice
+  const double* c;    //       depth         depth_cm           txh
+  const double* d;    //       thR (opt.)    -                  dist
+  double ice;         // uniform ice height (m) or ice_cm for IN_CM
+  long long n;
+};
+
+template <int IN>
+__device__ __forceinline__ Geometry load_query(const DevMedium& M, const QueryArgs& Q, long long k,
+                                               double& thR) {
+  double H, D, ice, dep;
+  if (IN == IN_M) {
+    H = Q.a[k];
+    D = Q.b[k];
+    dep = Q.c[k];
+    ice = Q.ice;
+    thR = Q.d != nullptr ? Q.d[k] : straight_angle(M, H, D, ice, dep);
+  } else if (IN == IN_CM) {
+    H = Q.a[k] / 100;
+    D = Q.b[k] / 100;
+    ice = Q.ice / 100;
+    dep = Q.c[k] / 100;
+    thR = straight_angle(M, H, D, ice, dep);
+  } else {
+    dep = Q.a[k];
+    ice = Q.b[k];
+    H = Q.c[k];
+    D = Q.d[k];
+    thR = straight_angle(M, H, D, ice, dep);
+  }
+  return shift(H, D, ice, dep);
+}
+
+// Where stage 1 parks (root, status) for stage 2.
+struct Park {
+  double* root;
+  double* status;
+  long long stride;
+};
+
+template <int IN>
+__global__ __launch_bounds__(kBlock, 4) void roots_kernel(DevMedium M, IceConsts I, QueryArgs Q,
+                                                       Park park) {
   const long long k = (long long)blockIdx.x * kBlock + threadIdx.x;
-  if (k >= n) return;
-  const double H = txh[k], D = dist[k], dep = depth[k];
-  // StraightAngle argument of Air2IceRayTracing (.cc:1464); default: the thR that
-  // GetHorizontalDistanceToIntersectionPoint forms (.cc:952-958).
-  const double thR = thr_in != nullptr ? thr_in[k] : straight_angle(M, H, D, I.ice_h, dep);
-  const Solved S = air2ice(M, I, H, D, I.ice_h, dep, thR);
+  if (k >= Q.n) return;
+  double thR;
+  const Geometry g = load_query<IN>(M, Q, k, thR);
+  const SolveResult r = solve_root(M, I, g, thR);
+  park.root[k * park.stride] = r.root;
+  park.status[k * park.stride] = (double)r.status;
+}
+
+__device__ __forceinline__ bool check_solution(double thd, double D) {
+  // CheckSolution (.cc:978-983, AirIceRayTracing.cc:916-921)
+  bool good = false;
+  if ((fabs(thd - D) / D < 0.01 && D <= 100) || (fabs(thd - D) < 1 && D > 100)) good = true;
+  if (thd < 0) good = false;
+  return good;
+}
+
+// Stage 2 of Air2IceRayTracing: dummy[0..16] (MultiRay, .cc:1597-1614) or dummy[0..14]
+// (pythonwrapper, AirIceRayTracing.cc:1070-1084), SoA with stride ld.
+template <int VARIANT>
+__global__ __launch_bounds__(kBlock) void solve_out_kernel(DevMedium M, IceConsts I, QueryArgs Q,
+                                                           double* __restrict__ out, size_t ld,
+                                                           uint8_t* __restrict__ status) {
+  const long long k = (long long)blockIdx.x * kBlock + threadIdx.x;
+  if (k >= Q.n) return;
+  double thR;
+  const Geometry g = load_query<IN_M>(M, Q, k, thR);
+  const double x = out[10 * ld + k];
+  const int st = (int)out[0 * ld + k];
+  const Solved S = evaluate_root(M, I, g, x, st);
   const double thd = S.thd_ice + S.thd_air;
   const double tt = S.t_ice + S.t_air;
-  out[0 * ld + k] = H;
+  out[0 * ld + k] = g.H;
   out[1 * ld + k] = thd;
   out[2 * ld + k] = S.thd_air;
   out[3 * ld + k] = S.thd_ice;
@@ -422,10 +605,9 @@ __global__ __launch_bounds__(kBlock) void solve_kernel(DevMedium M, IceConsts I,
   out[8 * ld + k] = S.t_ice;
   out[9 * ld + k] = S.t_air;
   out[10 * ld + k] = S.launch;
-  const Endpoint iceair = air_endpoint(M, S.ice_h);
   if (VARIANT == AIRICE_VARIANT_MULTIRAY) {
     double tS, tP;
-    fresnel_trans(iceair.n, I.ice0.n, S.inc * M.d2r, tS, tP);
+    fresnel_trans(S.ice_n, I.ice0.n, S.inc * M.d2r, tS, tP);
     out[11 * ld + k] = S.ant;
     out[12 * ld + k] = tS;
     out[13 * ld + k] = tP;
@@ -433,8 +615,7 @@ __global__ __launch_bounds__(kBlock) void solve_kernel(DevMedium M, IceConsts I,
     out[15 * ld + k] = S.geo_ice;
     out[16 * ld + k] = S.inc;
   } else {
-    // pythonwrapper AirIceRayTracing.cc:1081-1084
-    out[11 * ld + k] = asin((iceair.n / I.ice0.n) * sin(S.inc * M.d2r)) * M.r2d;
+    out[11 * ld + k] = asin((S.ice_n / I.ice0.n) * sin(S.inc * M.d2r)) * M.r2d;
     out[12 * ld + k] = S.ant;
     out[13 * ld + k] = S.geo_air;
     out[14 * ld + k] = S.geo_ice;
@@ -442,24 +623,20 @@ __global__ __launch_bounds__(kBlock) void solve_kernel(DevMedium M, IceConsts I,
   if (status != nullptr) status[k] = (uint8_t)S.status;
 }
 
-// GetHorizontalDistanceToIntersectionPoint (.cc:945-989), cm in, 9 outputs + bool.
-__global__ __launch_bounds__(kBlock) void hdtip_kernel(DevMedium M, IceConsts I,
-                                                       const double* __restrict__ src_cm,
-                                                       const double* __restrict__ dist_cm,
-                                                       const double* __restrict__ depth_cm,
-                                                       double ice_cm, long long n,
-                                                       double* __restrict__ out, size_t ld,
-                                                       uint8_t* __restrict__ ok) {
+// Stage 2 of GetHorizontalDistanceToIntersectionPoint (.cc:945-989): 9 outputs (cm, rad) + bool.
+__global__ __launch_bounds__(kBlock) void hdtip_out_kernel(DevMedium M, IceConsts I, QueryArgs Q,
+                                                           double* __restrict__ out, size_t ld,
+                                                           uint8_t* __restrict__ ok) {
   const long long k = (long long)blockIdx.x * kBlock + threadIdx.x;
-  if (k >= n) return;
-  const double H = src_cm[k] / 100, D = dist_cm[k] / 100, ice = ice_cm / 100,
-               dep = depth_cm[k] / 100;
-  const double thR = straight_angle(M, H, D, ice, dep);
-  const Solved S = air2ice(M, I, H, D, ice, dep, thR);
+  if (k >= Q.n) return;
+  double thR;
+  const Geometry g = load_query<IN_CM>(M, Q, k, thR);
+  const double x = out[4 * ld + k];
+  const int st = (int)out[0 * ld + k];
+  const Solved S = evaluate_root(M, I, g, x, st);
   const double thd = S.thd_ice + S.thd_air;
-  const Endpoint iceair = air_endpoint(M, S.ice_h);
   double tS, tP;
-  fresnel_trans(iceair.n, I.ice0.n, S.inc * M.d2r, tS, tP);
+  fresnel_trans(S.ice_n, I.ice0.n, S.inc * M.d2r, tS, tP);
   out[0 * ld + k] = (S.t_ice * kSpeedC) * 100;
   out[1 * ld + k] = (S.t_air * kSpeedC) * 100;
   out[2 * ld + k] = S.geo_ice * 100;
@@ -469,36 +646,26 @@ __global__ __launch_bounds__(kBlock) void hdtip_kernel(DevMedium M, IceConsts I,
   out[6 * ld + k] = tS;
   out[7 * ld + k] = tP;
   out[8 * ld + k] = S.ant * M.d2r;
-  bool good = false;
-  if ((fabs(thd - D) / D < 0.01 && D <= 100) || (fabs(thd - D) < 1 && D > 100)) good = true;
-  if (thd < 0) good = false;
-  ok[k] = good ? 1 : 0;
+  ok[k] = check_solution(thd, g.D) ? 1 : 0;
 }
 
-// pythonwrapper TraceIceToAir (TraceIceToAir.C:5-73) with GetRayTracingSolution
-// (AirIceRayTracing.cc:884-927); per-query ice height.
-__global__ __launch_bounds__(kBlock) void trace_kernel(DevMedium M, IceConsts I,
-                                                       const double* __restrict__ depth,
-                                                       const double* __restrict__ iceh,
-                                                       const double* __restrict__ txh,
-                                                       const double* __restrict__ dist,
-                                                       long long n, double* __restrict__ out10) {
+// Stage 2 of the pythonwrapper TraceIceToAir (TraceIceToAir.C:5-73), rows of 10.
+__global__ __launch_bounds__(kBlock) void trace_out_kernel(DevMedium M, IceConsts I, QueryArgs Q,
+                                                           double* __restrict__ out10) {
   const long long k = (long long)blockIdx.x * kBlock + threadIdx.x;
-  if (k >= n) return;
-  const double H = txh[k], D = dist[k], ice = iceh[k], dep = depth[k];
-  const double thR = straight_angle(M, H, D, ice, dep);
-  const Solved S = air2ice(M, I, H, D, ice, dep, thR);
-  const double thd = S.thd_ice + S.thd_air;
-  const Endpoint iceair = air_endpoint(M, S.ice_h);
-  const double aoi = asin((iceair.n / I.ice0.n) * sin(S.inc * M.d2r)) * M.r2d;
-  bool good = false;
-  if ((fabs(thd - D) / D < 0.01 && D <= 100) || (fabs(thd - D) < 1 && D > 100)) good = true;
-  if (thd < 0) good = false;
+  if (k >= Q.n) return;
+  double thR;
+  const Geometry g = load_query<IN_TRACE>(M, Q, k, thR);
   double* o = out10 + 10 * k;
-  if (good) {
+  const double x = o[5];
+  const int st = (int)o[9];
+  const Solved S = evaluate_root(M, I, g, x, st);
+  const double thd = S.thd_ice + S.thd_air;
+  const double aoi = asin((S.ice_n / I.ice0.n) * sin(S.inc * M.d2r)) * M.r2d;
+  if (check_solution(thd, g.D)) {
     // swap(launch, received); received = 180 - received (TraceIceToAir.C:33-34)
-    o[0] = H;
-    o[1] = D;
+    o[0] = g.H;
+    o[1] = g.D;
     o[2] = S.geo_ice;
     o[3] = S.geo_air;
     o[4] = S.ant;
@@ -518,6 +685,8 @@ __global__ __launch_bounds__(kBlock) void trace_kernel(DevMedium M, IceConsts I,
 // ---------------------------------------------------------------------------
 static inline unsigned grid_for(long long n) { return (unsigned)((n + kBlock - 1) / kBlock); }
 
+static inline int launch_ok() { return hipGetLastError() == hipSuccess ? AIRICE_OK : AIRICE_EHIP; }
+
 int launch_table(const DevMedium& M, const IceConsts& I, const airice_grid* g, int row_begin,
                  int row_count, float* d_table, double* d_full, size_t ld, hipStream_t st) {
   TableArgs A;
@@ -536,7 +705,7 @@ int launch_table(const DevMedium& M, const IceConsts& I, const airice_grid* g, i
   if (A.n == 0) return AIRICE_OK;
   hipLaunchKernelGGL(table_kernel, dim3(grid_for(A.n)), dim3(kBlock), 0, st, M, I, A, d_table,
                      d_full);
-  return hipGetLastError() == hipSuccess ? AIRICE_OK : AIRICE_EHIP;
+  return launch_ok();
 }
 
 int launch_rays(const DevMedium& M, const IceConsts& I, const double* launch, const double* txh,
@@ -544,39 +713,47 @@ int launch_rays(const DevMedium& M, const IceConsts& I, const double* launch, co
   if (n == 0) return AIRICE_OK;
   hipLaunchKernelGGL(rays_kernel, dim3(grid_for((long long)n)), dim3(kBlock), 0, st, M, I, launch,
                      txh, in_ice, (long long)n, out, ld);
-  return hipGetLastError() == hipSuccess ? AIRICE_OK : AIRICE_EHIP;
+  return launch_ok();
 }
 
 int launch_solve(const DevMedium& M, const IceConsts& I, int variant, const double* txh,
                  const double* dist, const double* depth, const double* thr, size_t n,
                  double* out, size_t ld, uint8_t* status, hipStream_t st) {
   if (n == 0) return AIRICE_OK;
+  const QueryArgs Q{txh, dist, depth, thr, I.ice_h, (long long)n};
+  const Park park{out + 10 * ld, out, 1};
+  const dim3 grid(grid_for((long long)n)), block(kBlock);
+  hipLaunchKernelGGL(roots_kernel<IN_M>, grid, block, 0, st, M, I, Q, park);
   if (variant == AIRICE_VARIANT_MULTIRAY)
-    hipLaunchKernelGGL(solve_kernel<AIRICE_VARIANT_MULTIRAY>, dim3(grid_for((long long)n)),
-                       dim3(kBlock), 0, st, M, I, txh, dist, depth, thr, (long long)n, out, ld,
-                       status);
+    hipLaunchKernelGGL(solve_out_kernel<AIRICE_VARIANT_MULTIRAY>, grid, block, 0, st, M, I, Q, out,
+                       ld, status);
   else
-    hipLaunchKernelGGL(solve_kernel<AIRICE_VARIANT_PYWRAPPER>, dim3(grid_for((long long)n)),
-                       dim3(kBlock), 0, st, M, I, txh, dist, depth, thr, (long long)n, out, ld,
-                       status);
-  return hipGetLastError() == hipSuccess ? AIRICE_OK : AIRICE_EHIP;
+    hipLaunchKernelGGL(solve_out_kernel<AIRICE_VARIANT_PYWRAPPER>, grid, block, 0, st, M, I, Q,
+                       out, ld, status);
+  return launch_ok();
 }
 
 int launch_hdtip(const DevMedium& M, const IceConsts& I, const double* src, const double* dist,
                  const double* depth, double ice_cm, size_t n, double* out, size_t ld,
                  uint8_t* ok, hipStream_t st) {
   if (n == 0) return AIRICE_OK;
-  hipLaunchKernelGGL(hdtip_kernel, dim3(grid_for((long long)n)), dim3(kBlock), 0, st, M, I, src,
-                     dist, depth, ice_cm, (long long)n, out, ld, ok);
-  return hipGetLastError() == hipSuccess ? AIRICE_OK : AIRICE_EHIP;
+  const QueryArgs Q{src, dist, depth, nullptr, ice_cm, (long long)n};
+  const Park park{out + 4 * ld, out, 1};
+  const dim3 grid(grid_for((long long)n)), block(kBlock);
+  hipLaunchKernelGGL(roots_kernel<IN_CM>, grid, block, 0, st, M, I, Q, park);
+  hipLaunchKernelGGL(hdtip_out_kernel, grid, block, 0, st, M, I, Q, out, ld, ok);
+  return launch_ok();
 }
 
 int launch_trace(const DevMedium& M, const IceConsts& I, const double* depth, const double* ice,
                  const double* txh, const double* dist, size_t n, double* out10, hipStream_t st) {
   if (n == 0) return AIRICE_OK;
-  hipLaunchKernelGGL(trace_kernel, dim3(grid_for((long long)n)), dim3(kBlock), 0, st, M, I, depth,
-                     ice, txh, dist, (long long)n, out10);
-  return hipGetLastError() == hipSuccess ? AIRICE_OK : AIRICE_EHIP;
+  const QueryArgs Q{depth, ice, txh, dist, 0.0, (long long)n};
+  const Park park{out10 + 5, out10 + 9, 10};
+  const dim3 grid(grid_for((long long)n)), block(kBlock);
+  hipLaunchKernelGGL(roots_kernel<IN_TRACE>, grid, block, 0, st, M, I, Q, park);
+  hipLaunchKernelGGL(trace_out_kernel, grid, block, 0, st, M, I, Q, out10);
+  return launch_ok();
 }
 
 }  // namespace airice

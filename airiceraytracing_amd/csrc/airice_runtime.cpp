@@ -159,32 +159,19 @@ static int host_air_layer(const DevMedium& M, double zabs) {
 }
 
 Endpoint host_air_endpoint(const DevMedium& M, double x) {
-  Endpoint p;
   const double zabs = std::fabs(x);
   const int l = host_air_layer(M, zabs);
-  p.x = x;
-  p.B = M.B[l];
-  p.C = M.negC[l];
-  const double eabs = std::exp(p.C * zabs);
-  p.n = M.A_air + p.B * eabs;
-  p.e = x >= 0.0 ? eabs : std::exp(p.C * x);
-  p.y = x >= 0.0 ? p.n : M.A_air + p.B * p.e;
-  p.e2 = std::exp(2 * p.C * x);
-  return p;
+  const double C = M.negC[l];
+  const double e_abs = std::exp(C * zabs);
+  const double e_x = x >= 0.0 ? e_abs : std::exp(C * x);
+  return make_endpoint(M.A_air, M.B[l], C, x, e_abs, e_x);
 }
 
 Endpoint host_ice_endpoint(const DevMedium& M, double x) {
-  Endpoint p;
   const double zabs = std::fabs(x);
-  p.x = x;
-  p.B = M.B_ice;
-  p.C = M.negC_ice;
-  const double eabs = std::exp(p.C * zabs);
-  p.n = M.A_ice + p.B * eabs;
-  p.e = x >= 0.0 ? eabs : std::exp(p.C * x);
-  p.y = x >= 0.0 ? p.n : M.A_ice + p.B * p.e;
-  p.e2 = std::exp(2 * p.C * x);
-  return p;
+  const double e_abs = std::exp(M.negC_ice * zabs);
+  const double e_x = x >= 0.0 ? e_abs : std::exp(M.negC_ice * x);
+  return make_endpoint(M.A_ice, M.B_ice, M.negC_ice, x, e_abs, e_x);
 }
 
 int build_dev_medium(const airice_medium* m, int variant, DevMedium* out) {
@@ -223,7 +210,6 @@ void build_ice_consts(const DevMedium& M, double ice_h, double rx_depth, IceCons
   out->ice_air = host_air_endpoint(M, ice_h);
   out->ice0 = host_ice_endpoint(M, 0.0);
   out->ice_rx = host_ice_endpoint(M, rx_depth);
-  out->n1_over_n2 = out->ice_air.n / out->ice0.n;
 }
 
 }  // namespace airice

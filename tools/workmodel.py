@@ -9,12 +9,14 @@ from __future__ import annotations
 
 import numpy as np
 
-# per air/ice segment (segment_full): 3 sin, 2 asin, 1+2x2 sqrt, 2x4 log, 2+2x8 div,
-# and ~103 add/mul (two prim_all endpoints at ~43 each + the Snell chain + combination)
-SEGMENT = {"sin": 3, "asin": 2, "sqrt": 5, "log": 8, "div": 18, "arith": 103}
-# per ray: Tx endpoint (2 exp), grid coordinates, Fresnel T_S/T_P, output scaling/accumulation
-PER_RAY = {"exp": 2, "sin": 1, "cos": 1, "sqrt": 1, "div": 4, "arith": 5 + 4 + 14 + 8}
-PER_SEGMENT_ACC = {"arith": 4}
+# per air/ice segment (airice_device.hpp segment(), identities (1)-(5)): Snell step 1 div,
+# ray parameter 1 sqrt + 1 div, two ends x (1 sqrt), two log ratios (2 div + 2 log), and
+# ~40 add/mul forming THD, time and geometric path from them
+SEGMENT = {"sqrt": 3, "log": 2, "div": 4, "arith": 40}
+# per ray: Tx endpoint (1 exp + 1 div + 8 products), launch sine, incidence asin, ice-segment
+# Snell ratio and receive asin, Fresnel T_S/T_P (sin, cos, sqrt, 4 div), output scaling
+PER_RAY = {"exp": 1, "sin": 2, "cos": 1, "asin": 2, "sqrt": 1, "div": 6, "arith": 40}
+PER_SEGMENT_ACC = {"arith": 3}  # THD/time/geo accumulation
 
 
 def _layers_m(medium):
