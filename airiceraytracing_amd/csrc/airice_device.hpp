@@ -70,13 +70,58 @@ struct DevMedium {
   Endpoint stop[kMaxLayers];   // layer l stop:  x = ATMLAY[l]/100          (.cc:1858)
 };
 
-// Per-launch endpoints that are uniform over the batch.
+// A segment whose two ends are known before launch (the lower air layers of a ray, a table's
+// ice segment): everything the closed forms need from the ends, folded on the host so the
+// kernel reads them as scalars (no SGPR-SGPR arithmetic, no selects).
+struct SegConst {
+  double Tn, Ty2, TAy;  // start end: n, y^2, A*y
+  double Rn, Ry2, RAy;  // stop end
+  double ratio;         // Tn / Rn: Snell step sin(recv) = (Tn/Rn) sin(lang)
+  double invC, invCc;   // 1/C, 1/(C c)
+  double dCx, dACx;     // R.Cx - T.Cx, R.ACx - T.ACx
+};
+
+// Stop end of the first (Tx) layer of a ray, indexed by that layer: the layer's lower bound,
+// or the ice when the layer is the lowest one.
+struct TopEnd {
+  double x, n, y2, Ay, invC, invCc, Cx, ACx;
+};
+
+// Per-launch constants that are uniform over the batch.
 struct IceConsts {
   double ice_h;        // IceLayerHeight (m) of the launch
   Endpoint ice_air;    // air model at the ice height (stop of the lowest air layer)
   Endpoint ice0;       // ice model at depth 0 (.cc:1899)
   Endpoint ice_rx;     // ice model at the antenna depth (table: uniform)
+  int bot;             // lowest air layer (layer of the ice height, .cc:1815-1825)
+  int pad_;
+  SegConst lower[kMaxLayers];  // layer l as a lower layer: start[l] -> (l == bot ? ice : stop[l])
+  TopEnd topend[kMaxLayers];   // layer l as the Tx layer: its stop end
+  SegConst iceseg;             // ice surface -> antenna (table)
+  double n_air_ice, n_ice0;    // Getnz_air(ice), Getnz_ice(0) (Snell into the ice, Fresnel)
 };
+
+__host__ __device__ inline SegConst make_segconst(const Endpoint& T, const Endpoint& R) {
+  const double speedc = 299792458.0;
+  SegConst s;
+  s.Tn = T.n;
+  s.Ty2 = T.y2;
+  s.TAy = T.Ay;
+  s.Rn = R.n;
+  s.Ry2 = R.y2;
+  s.RAy = R.Ay;
+  s.ratio = T.n / R.n;
+  s.invC = R.invC;
+  s.invCc = R.invC * (1.0 / speedc);
+  s.dCx = R.Cx - T.Cx;
+  s.dACx = R.ACx - T.ACx;
+  return s;
+}
+
+__host__ __device__ inline TopEnd make_topend(const Endpoint& R) {
+  const double speedc = 299792458.0;
+  return TopEnd{R.x, R.n, R.y2, R.Ay, R.invC, R.invC * (1.0 / speedc), R.Cx, R.ACx};
+}
 
 __device__ __forceinline__ double sel5(const double (&a)[5], int l) {
   double r = a[0];
@@ -159,9 +204,39 @@ struct Segment {
 // 508-510).  A segment whose ends are at the same height is exactly 0 (or NaN) in the
 // reference: the same function of the same x at both ends.  Endpoints built on the host
 // and on the device can differ by an ulp, so one endpoint is reused.
+// Natural log of a positive normal finite x, < 1 ulp (the fdlibm e_log.c reduction
+// x = 2^k (1+f), sqrt(1/2) <= 1+f < sqrt(2), s = f/(2+f), degree-14 minimax in s):
+// ~45 VALU instead of ocml's ~85 (which also covers denormals and special values).
+// Any other x goes to ocml's log, so NaN / inf / 0 / negative behave exactly as log().
+// Checked against long double on 6e7 arguments: max error 0.84 ulp (tests/test_fastlog.py).
+__device__ __forceinline__ double fast_log(double x) {
+  if (!(x >= 2.2250738585072014e-308 && x <= 1.7976931348623157e308)) return log(x);
+  const double Lg1 = 6.666666666666735130e-01, Lg2 = 3.999999999940941908e-01,
+               Lg3 = 2.857142874366239149e-01, Lg4 = 2.222219843214978396e-01,
+               Lg5 = 1.818357216161805012e-01, Lg6 = 1.531383769920937332e-01,
+               Lg7 = 1.479819860511658591e-01;
+  const double ln2_hi = 6.93147180369123816490e-01, ln2_lo = 1.90821492927058770002e-10;
+  const unsigned long long b = (unsigned long long)__double_as_longlong(x);
+  int k = (int)(b >> 52) - 1023;
+  double m = __longlong_as_double((long long)((b & 0x000fffffffffffffULL) | 0x3ff0000000000000ULL));
+  if (m > 1.4142135623730951) {
+    m *= 0.5;
+    k += 1;
+  }
+  const double f = m - 1.0;
+  const double s = f / (2.0 + f);
+  const double z = s * s, w = z * z;
+  const double t1 = w * __builtin_fma(w, __builtin_fma(w, Lg6, Lg4), Lg2);
+  const double t2 = z * __builtin_fma(w, __builtin_fma(w, __builtin_fma(w, Lg7, Lg5), Lg3), Lg1);
+  const double R = t2 + t1;
+  const double hfsq = 0.5 * f * f;
+  const double dk = (double)k;
+  return dk * ln2_hi - ((hfsq - (s * (hfsq + R) + dk * ln2_lo)) - f);
+}
+
 __device__ __forceinline__ double log_ratio(double a, double b) {
   // log(a) - log(b) as one logarithm when both are in log's domain (identity (5))
-  return (a > 0.0 && b > 0.0) ? log(a / b) : log(a) - log(b);
+  return (a > 0.0 && b > 0.0) ? fast_log(a / b) : log(a) - log(b);
 }
 
 __device__ __forceinline__ Segment segment(const Endpoint& T, const Endpoint& R_, double A,
@@ -186,6 +261,28 @@ __device__ __forceinline__ Segment segment(const Endpoint& T, const Endpoint& R_
     s.t *= -1;
     s.geo *= -1;
   }
+  return s;
+}
+
+// Segment with both ends folded on the host (SegConst), identity (5).  sin_in is the sine of
+// the incidence inside the start end (sin(lang)); returns the sine of the receive angle.
+__device__ __forceinline__ Segment segment_const(const SegConst& S, double A, double A2, double sin_in,
+                                                 bool air, double& v_out) {
+  const double v2 = sin_asin(S.ratio * sin_in);
+  const RayL RL = ray_L(A2, S.Rn * v2);
+  const double syR = sqrt(S.Ry2 - RL.LL), syT = sqrt(S.Ty2 - RL.LL);
+  const double d1 = log_ratio(S.RAy - RL.LL + RL.sAL * syR, S.TAy - RL.LL + RL.sAL * syT);
+  const double d2 = log_ratio(S.Rn + syR, S.Tn + syT);
+  Segment s;
+  s.thd = (RL.L * S.invC) * RL.rsAL * (S.dCx - d1);
+  s.t = ((syR - syT) + A2 * RL.rsAL * (S.dCx - d1) + A * d2) * S.invCc;
+  s.geo = (d2 - (A * d1) * RL.rsAL + S.dACx * RL.rsAL) * S.invC;
+  if (air) {
+    s.thd *= -1;
+    s.t *= -1;
+    s.geo *= -1;
+  }
+  v_out = v2;
   return s;
 }
 

@@ -33,46 +33,112 @@ constexpr int kBlock = 256;
 // The layer loop follows the reference (each layer re-derives L from the incidence angle
 // it receives, .cc:1871) with the running sine of identity (2).
 // ---------------------------------------------------------------------------
+__device__ __forceinline__ Endpoint stop_of(const DevMedium& M, int l) {
+  Endpoint r = M.stop[0];
+  r = pick(l == 1, M.stop[1], r);
+  r = pick(l == 2, M.stop[2], r);
+  r = pick(l == 3, M.stop[3], r);
+  return r;
+}
+
+// Fresnel T_S, T_P (.cc:285-337) at the incidence whose sine is v (identity (2):
+// sin(asin(v) r2d d2r) = v, cos = sqrt(1 - v^2) on [0, 90] degrees).
+__device__ __forceinline__ void fresnel_from_sine(double n1, double n2, double v, double& tS,
+                                                  double& tP) {
+  const double st = v, ct = sqrt(1 - v * v);
+  const double a = (n1 / n2) * st;
+  const double sqterm = sqrt(1 - a * a);
+  double num = n1 * ct - n2 * sqterm;
+  double den = n1 * ct + n2 * sqterm;
+  tS = 1 + (num / den);
+  if (isnan(tS)) tS = 0;
+  num = n1 * sqterm - n2 * ct;
+  den = n1 * sqterm + n2 * ct;
+  tP = (1 - (num / den)) * (n1 / n2);
+  if (isnan(tP)) tP = 0;
+}
+
+// Stop end of the Tx layer `top`.  Rays of one wave almost always share their Tx layer (a
+// wave covers <= 2 table rows), so the entry is read with a wave-uniform (scalar) index;
+// a wave that straddles a layer boundary falls back to per-lane selects.
+__device__ __forceinline__ TopEnd topend_of(const IceConsts& I, int top) {
+  const int tu = __builtin_amdgcn_readfirstlane(top);
+  if (__ballot(top != tu) == 0) return I.topend[tu];
+  TopEnd r = I.topend[0];
+#pragma unroll
+  for (int l = 1; l < kMaxLayers; ++l) {
+    const bool c = (top == l);
+    const TopEnd& e = I.topend[l];
+    r = TopEnd{c ? e.x : r.x,       c ? e.n : r.n,       c ? e.y2 : r.y2, c ? e.Ay : r.Ay,
+               c ? e.invC : r.invC, c ? e.invCc : r.invCc, c ? e.Cx : r.Cx, c ? e.ACx : r.ACx};
+  }
+  return r;
+}
+
+// First (Tx) layer of a ray: per-lane start end T, stop end R; identity (5) as in segment().
+__device__ __forceinline__ Segment segment_top(const Endpoint& T, const TopEnd& R_, double A,
+                                               double A2, double sin_in, double& v_out) {
+  // zero-length (Tx exactly on the layer's lower bound / the ice): reuse the Tx end
+  const bool zl = (R_.x == T.x);
+  const double speedc = 299792458.0;
+  const TopEnd R = zl ? TopEnd{T.x, T.n, T.y2, T.Ay, T.invC, T.invC * (1.0 / speedc), T.Cx, T.ACx}
+                      : R_;
+  const double v2 = sin_asin((T.n * sin_in) / R.n);
+  const RayL RL = ray_L(A2, R.n * v2);
+  const double syR = sqrt(R.y2 - RL.LL), syT = sqrt(T.y2 - RL.LL);
+  const double d1 = log_ratio(R.Ay - RL.LL + RL.sAL * syR, T.Ay - RL.LL + RL.sAL * syT);
+  const double d2 = log_ratio(R.n + syR, T.n + syT);
+  const double dCx = R.Cx - T.Cx;
+  Segment s;
+  s.thd = -((RL.L * R.invC) * RL.rsAL * (dCx - d1));
+  s.t = -(((syR - syT) + A2 * RL.rsAL * (dCx - d1) + A * d2) * R.invCc);
+  s.geo = -((d2 - (A * d1) * RL.rsAL + (R.ACx - T.ACx) * RL.rsAL) * R.invC);
+  v_out = v2;
+  return s;
+}
+
 __device__ __forceinline__ void ray_solution(const DevMedium& M, const IceConsts& I, double theta,
-                                             double H, bool in_ice, int bot, double* d) {
+                                             double H, bool in_ice, double* d) {
   const int top = top_layer(M, H);
-  const Endpoint tx = air_endpoint(M, H);
+  const int bot = I.bot;
   const double A2 = M.A_air * M.A_air;
   double v = sin((180 - theta) * M.d2r);  // sine of StartAngle (.cc:1863)
   double thd_air = 0.0, t_air = 0.0, geo_air = 0.0;
-#pragma unroll
-  for (int il = kMaxLayers - 1; il >= 0; --il) {
-    if (il > top || il < bot) continue;
-    const Endpoint T = pick(il == top, tx, M.start[il]);
-    const Endpoint R = pick(il == bot, I.ice_air, M.stop[il]);
-    // n_layer1 == Getnz_air(StartHeight) == nzTx: Snell into the layer is the identity
-    const double v2 = sin_asin((T.n * sin_asin(v)) / R.n);
-    const RayL RL = ray_L(A2, R.n * v2);
-    const Segment s = segment(T, R, M.A_air, A2, RL, true);
+  const bool any = top >= bot;
+  if (any) {
+    // n_layer1 == Getnz_air(StartHeight) == nzTx: Snell into a layer is the identity
+    const Endpoint T = air_endpoint(M, H);
+    const Segment s = segment_top(T, topend_of(I, top), M.A_air, A2, sin_asin(v), v);
     thd_air += s.thd;
     t_air += s.t;
     geo_air += s.geo;
-    v = v2;
+  }
+  // lower layers: both ends folded on the host (I.lower, scalar reads)
+#pragma unroll
+  for (int il = kMaxLayers - 2; il >= 0; --il) {
+    if (il >= top || il < bot) continue;
+    const Segment s = segment_const(I.lower[il], M.A_air, A2, sin_asin(v), true, v);
+    thd_air += s.thd;
+    t_air += s.t;
+    geo_air += s.geo;
   }
   // IncidentAngleonIce = last layer's receive angle; 0 when no air layer (.cc:1832, 1881)
-  const bool any = top >= bot;
   const double inc = any ? asin(v) * M.r2d : 0.0;
   const double vinc = any ? v : 0.0;
   double thd_ice = 0.0, t_ice = 0.0, geo_ice = 0.0, recv_ice = 0.0;
   if (in_ice) {
     // .cc:1897-1922: n_layer1 = Getnz_air(IceLayerHeight), Rx = -AntennaDepth, Tx = 0
     const double A2i = M.A_ice * M.A_ice;
-    const double u = sin_asin((I.ice_air.n / I.ice0.n) * vinc);
-    const double v2 = sin_asin((I.ice0.n * u) / I.ice_rx.n);
-    const RayL RL = ray_L(A2i, I.ice_rx.n * v2);
-    const Segment s = segment(I.ice0, I.ice_rx, M.A_ice, A2i, RL, false);
+    const double u = sin_asin((I.n_air_ice / I.n_ice0) * vinc);
+    double v2;
+    const Segment s = segment_const(I.iceseg, M.A_ice, A2i, u, false, v2);
     thd_ice += s.thd;
     t_ice += s.t;
     geo_ice += s.geo;
     recv_ice = asin(v2) * M.r2d;
   }
   double tS, tP;
-  fresnel_trans(I.ice_air.n, I.ice0.n, inc * M.d2r, tS, tP);
+  fresnel_from_sine(I.n_air_ice, I.n_ice0, vinc, tS, tP);
   d[0] = 0;
   d[1] = H;
   d[2] = thd_air + thd_ice;
@@ -115,9 +181,8 @@ __global__ __launch_bounds__(kBlock) void table_kernel(DevMedium M, IceConsts I,
   double th = G.start_a + G.step_a * iang;
   if (H != G.stop_h && ihei == G.hsteps - 1) H = G.stop_h;
   if (iang == G.asteps - 1) th = G.stop_a;
-  const int bot = bottom_layer(M, I.ice_h);
   double d[18];
-  ray_solution(M, I, th, H, G.in_ice != 0, bot, d);
+  ray_solution(M, I, th, H, G.in_ice != 0, d);
   const size_t ld = G.ld;
   // AllTableAllAntData columns (.cc:2101-2111)
   table[0 * ld + k] = (float)d[1];
@@ -144,9 +209,8 @@ __global__ __launch_bounds__(kBlock) void rays_kernel(DevMedium M, IceConsts I,
                                                       size_t ld) {
   const long long k = (long long)blockIdx.x * kBlock + threadIdx.x;
   if (k >= n) return;
-  const int bot = bottom_layer(M, I.ice_h);
   double d[18];
-  ray_solution(M, I, launch[k], txh[k], in_ice != 0, bot, d);
+  ray_solution(M, I, launch[k], txh[k], in_ice != 0, d);
 #pragma unroll
   for (int c = 0; c < 18; ++c) out[c * ld + k] = d[c];
 }
@@ -162,13 +226,6 @@ struct AirPath {
   int top, bot;
 };
 
-__device__ __forceinline__ Endpoint stop_of(const DevMedium& M, int l) {
-  Endpoint r = M.stop[0];
-  r = pick(l == 1, M.stop[1], r);
-  r = pick(l == 2, M.stop[2], r);
-  r = pick(l == 3, M.stop[3], r);
-  return r;
-}
 
 __device__ __forceinline__ AirPath make_air_path(const DevMedium& M, double H, double ice) {
   AirPath P;

@@ -206,10 +206,30 @@ int build_dev_medium(const airice_medium* m, int variant, DevMedium* out) {
 }
 
 void build_ice_consts(const DevMedium& M, double ice_h, double rx_depth, IceConsts* out) {
+  std::memset(out, 0, sizeof(*out));
   out->ice_h = ice_h;
   out->ice_air = host_air_endpoint(M, ice_h);
   out->ice0 = host_ice_endpoint(M, 0.0);
   out->ice_rx = host_ice_endpoint(M, rx_depth);
+  out->n_air_ice = out->ice_air.n;
+  out->n_ice0 = out->ice0.n;
+  // lowest air layer: SkipLayersBelow scan (.cc:1815-1825)
+  int bot = 0;
+  for (int il = 0; il < M.ml; ++il) {
+    if (ice_h >= M.atm[il] && ice_h < M.atm[il + 1]) break;
+    ++bot;
+  }
+  out->bot = bot;
+  for (int l = 0; l < kMaxLayers; ++l) {
+    const Endpoint& T = M.start[l];
+    Endpoint R = (l == bot) ? out->ice_air : M.stop[l];
+    out->topend[l] = make_topend(R);
+    if (R.x == T.x) R = T;  // zero-length segment: the same function of the same x
+    out->lower[l] = make_segconst(T, R);
+  }
+  Endpoint rx = out->ice_rx;
+  if (rx.x == out->ice0.x) rx = out->ice0;
+  out->iceseg = make_segconst(out->ice0, rx);
 }
 
 }  // namespace airice
