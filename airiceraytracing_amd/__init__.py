@@ -5,12 +5,14 @@ A from-scratch HIP implementation of the uzairlatif90/AirIceRayTracing hot path
 the pythonwrapper ``Py_TraceIceToAir`` surface) behind a C-ABI (``include/airice.h``,
 ``libairice.so``).  See DESIGN.md.
 """
-from ._lib import (AirIceLibraryError, Grid, Medium, VARIANT_MULTIRAY, VARIANT_PYWRAPPER,
-                   build, default_atmosphere_path, lib, load_medium)
+from ._lib import (AirIceLibraryError, Grid, LOOKUP_FALLBACK, LOOKUP_UNPINNED, LookupTable,
+                   Medium, VARIANT_MULTIRAY, VARIANT_PYWRAPPER, build, default_atmosphere_path,
+                   lib, load_medium)
 from .solver import AirIceSolver, make_grid
 
 __all__ = [
-    "AirIceLibraryError", "AirIceSolver", "Grid", "Medium", "VARIANT_MULTIRAY",
+    "AirIceLibraryError", "AirIceSolver", "Grid", "LOOKUP_FALLBACK", "LOOKUP_UNPINNED",
+    "LookupTable", "Medium", "VARIANT_MULTIRAY",
     "VARIANT_PYWRAPPER", "build", "default_atmosphere_path", "lib", "load_medium", "make_grid",
 ]
 __version__ = "0.1.0"

@@ -81,12 +81,30 @@ class Grid(ctypes.Structure):
         return int(self.height_steps) * int(self.angle_steps)
 
 
+class LookupTable(ctypes.Structure):
+    """airice_lookup_table (include/airice.h): one antenna's HBM-resident table + the grid
+    globals the reference's lookup reads (MultiRayAirIceRefraction.cc:1035-1039)."""
+
+    _fields_ = [
+        ("table", ctypes.c_void_p),
+        ("ld", ctypes.c_size_t),
+        ("n_entries", ctypes.c_size_t),
+        ("loop_stop_height", ctypes.c_double),
+        ("height_step", ctypes.c_double),
+        ("total_height_steps", ctypes.c_int32),
+        ("total_angle_steps", ctypes.c_int32),
+    ]
+
+
+LOOKUP_FALLBACK = 1  # AIRICE_LOOKUP_FALLBACK
+LOOKUP_UNPINNED = 2  # AIRICE_LOOKUP_UNPINNED
+
 # Every symbol include/airice.h declares (checked by tests/test_capi.py).
 EXPORTED_SYMBOLS = (
     "airice_last_error", "airice_version", "airice_atmosphere_load", "airice_atmosphere_parse",
     "airice_nz_air", "airice_nz_ice", "airice_grid_init", "airice_table_launch",
     "airice_table_host", "airice_rays_launch", "airice_solve_launch", "airice_solve_host",
-    "airice_hdtip_launch", "airice_trace_ice_to_air_launch", "airice_trace_ice_to_air_host",
+    "airice_hdtip_launch", "airice_table_lookup_launch", "airice_trace_ice_to_air_launch", "airice_trace_ice_to_air_host",
     "Py_TraceIceToAir", "airice_device_count", "airice_set_device", "airice_malloc",
     "airice_free", "airice_memcpy_h2d", "airice_memcpy_d2h", "airice_synchronize",
 )
@@ -140,6 +158,8 @@ def lib() -> ctypes.CDLL:
         "airice_solve_launch": ([M, I, D, P, P, P, P, S, P, S, P, P], I),
         "airice_solve_host": ([M, I, D, P, P, P, P, S, P, S, P], I),
         "airice_hdtip_launch": ([M, P, P, P, D, S, P, S, P, P], I),
+        "airice_table_lookup_launch": ([M, ctypes.POINTER(LookupTable), P, P, P, D, S, P, S, P,
+                                        P, P], I),
         "airice_trace_ice_to_air_launch": ([M, P, P, P, P, S, P, P], I),
         "airice_trace_ice_to_air_host": ([M, P, P, P, P, S, P], I),
         "Py_TraceIceToAir": ([D, D, D, D, ctypes.POINTER(D)], None),

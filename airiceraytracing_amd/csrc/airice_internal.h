@@ -26,6 +26,15 @@ int launch_solve(const DevMedium& M, const IceConsts& I, int variant, const doub
 int launch_hdtip(const DevMedium& M, const IceConsts& I, const double* src, const double* dist,
                  const double* depth, double ice_cm, size_t n, double* out, size_t ld,
                  uint8_t* ok, hipStream_t st);
+// Table lookup: lookup_kernel, then the masked minimizer fallback for AIRICE_LOOKUP_FALLBACK
+// lanes (airice_lookup.hip / airice_kernels.hip).
+int launch_lookup(const DevMedium& M, const IceConsts& I, const airice_lookup_table* t,
+                  const double* src, const double* dist, const double* depth, double ice_cm,
+                  size_t n, double* out, size_t ld, uint8_t* ok, uint8_t* flags, hipStream_t st);
+int launch_lookup_fallback(const DevMedium& M, const IceConsts& I, const double* src,
+                           const double* dist, const double* depth, double ice_cm, size_t n,
+                           double* out, size_t ld, uint8_t* ok, const uint8_t* flags,
+                           hipStream_t st);
 int launch_trace(const DevMedium& M, const IceConsts& I, const double* depth, const double* ice,
                  const double* txh, const double* dist, size_t n, double* out10, hipStream_t st);
 

@@ -572,15 +572,18 @@ __device__ __forceinline__ double straight_angle(const DevMedium& M, double H, d
 // Query sources.  IN_M: metres, uniform ice (Air2IceRayTracing batch); IN_CM: centimetres
 // (GetHorizontalDistanceToIntersectionPoint, .cc:947-950); IN_TRACE: per-query ice, metres
 // (TraceIceToAir).
-enum { IN_M = 0, IN_CM = 1, IN_TRACE = 2 };
+// IN_CM100: the table lookup's minimizer fallback (.cc:1419), which hands the already-cm
+// source/distance/depth over multiplied by 100 again (and the ice height, already in m, x100).
+enum { IN_M = 0, IN_CM = 1, IN_TRACE = 2, IN_CM100 = 3 };
 
 struct QueryArgs {
-  const double* a;    // IN_M: txh    IN_CM: src_cm   IN_TRACE: depth
-  const double* b;    //       dist          dist_cm            ice
-  const double* c;    //       depth         depth_cm           txh
-  const double* d;    //       thR (opt.)    -                  dist
-  double ice;         // uniform ice height (m) or ice_cm for IN_CM
+  const double* a;    // IN_M: txh    IN_CM(100): src_cm   IN_TRACE: depth
+  const double* b;    //       dist               dist_cm            ice
+  const double* c;    //       depth              depth_cm           txh
+  const double* d;    //       thR (opt.)         -                  dist
+  double ice;         // uniform ice height (m) or ice_cm for IN_CM(100)
   long long n;
+  const uint8_t* mask;  // IN_CM100: only lanes with AIRICE_LOOKUP_FALLBACK set
 };
 
 template <int IN>
@@ -598,6 +601,12 @@ __device__ __forceinline__ Geometry load_query(const DevMedium& M, const QueryAr
     D = Q.b[k] / 100;
     ice = Q.ice / 100;
     dep = Q.c[k] / 100;
+    thR = straight_angle(M, H, D, ice, dep);
+  } else if (IN == IN_CM100) {
+    H = (Q.a[k] * 100) / 100;
+    D = (Q.b[k] * 100) / 100;
+    ice = Q.ice / 100;
+    dep = (Q.c[k] * 100) / 100;
     thR = straight_angle(M, H, D, ice, dep);
   } else {
     dep = Q.a[k];
@@ -621,6 +630,7 @@ __global__ __launch_bounds__(kBlock, 4) void roots_kernel(DevMedium M, IceConsts
                                                        Park park) {
   const long long k = (long long)blockIdx.x * kBlock + threadIdx.x;
   if (k >= Q.n) return;
+  if (IN == IN_CM100 && !(Q.mask[k] & AIRICE_LOOKUP_FALLBACK)) return;
   double thR;
   const Geometry g = load_query<IN>(M, Q, k, thR);
   const SolveResult r = solve_root(M, I, g, thR);
@@ -704,6 +714,39 @@ __global__ __launch_bounds__(kBlock) void hdtip_out_kernel(DevMedium M, IceConst
   out[7 * ld + k] = tP;
   out[8 * ld + k] = S.ant * M.d2r;
   ok[k] = check_solution(thd, g.D) ? 1 : 0;
+}
+
+// Stage 2 of the table lookup's minimizer fallback (.cc:1417-1456): the reference passes its
+// own output references to GetHorizontalDistanceToIntersectionPoint in the order
+// (geoIce, geoAir, optIce, optAir, ...), so the optical and geometric slots trade places;
+// `ok` arrives holding the lookup's checks and is completed with CheckSolBool and
+// launchAngle < 0, then the four zeroed slots of .cc:1451-1456.
+__global__ __launch_bounds__(kBlock) void lookup_fallback_out_kernel(
+    DevMedium M, IceConsts I, QueryArgs Q, double* __restrict__ out, size_t ld,
+    uint8_t* __restrict__ ok) {
+  const long long k = (long long)blockIdx.x * kBlock + threadIdx.x;
+  if (k >= Q.n) return;
+  if (!(Q.mask[k] & AIRICE_LOOKUP_FALLBACK)) return;
+  double thR;
+  const Geometry g = load_query<IN_CM100>(M, Q, k, thR);
+  const double x = out[4 * ld + k];
+  const int st = (int)out[0 * ld + k];
+  const Solved S = evaluate_root(M, I, g, x, st);
+  const double thd = S.thd_ice + S.thd_air;
+  double tS, tP;
+  fresnel_trans(S.ice_n, I.ice0.n, S.inc * M.d2r, tS, tP);
+  const double launch = S.launch * M.d2r;
+  const bool good = ok[k] != 0 && check_solution(thd, g.D) && !(launch < 0);
+  out[0 * ld + k] = good ? S.geo_ice * 100 : 0.0;
+  out[1 * ld + k] = good ? S.geo_air * 100 : 0.0;
+  out[2 * ld + k] = (S.t_ice * kSpeedC) * 100;
+  out[3 * ld + k] = (S.t_air * kSpeedC) * 100;
+  out[4 * ld + k] = good ? launch : 0.0;
+  out[5 * ld + k] = good ? S.thd_air * 100 : 0.0;
+  out[6 * ld + k] = tS;
+  out[7 * ld + k] = tP;
+  out[8 * ld + k] = S.ant * M.d2r;
+  ok[k] = good ? 1 : 0;
 }
 
 // Stage 2 of the pythonwrapper TraceIceToAir (TraceIceToAir.C:5-73), rows of 10.
@@ -799,6 +842,21 @@ int launch_hdtip(const DevMedium& M, const IceConsts& I, const double* src, cons
   const dim3 grid(grid_for((long long)n)), block(kBlock);
   hipLaunchKernelGGL(roots_kernel<IN_CM>, grid, block, 0, st, M, I, Q, park);
   hipLaunchKernelGGL(hdtip_out_kernel, grid, block, 0, st, M, I, Q, out, ld, ok);
+  return launch_ok();
+}
+
+int launch_lookup_fallback(const DevMedium& M, const IceConsts& I, const double* src,
+                           const double* dist, const double* depth, double ice_cm, size_t n,
+                           double* out, size_t ld, uint8_t* ok, const uint8_t* flags,
+                           hipStream_t st) {
+  if (n == 0) return AIRICE_OK;
+  // .cc:1309 turns IceLayerHeight into metres; .cc:1419 passes IceLayerHeight*100
+  const double ice_arg = (ice_cm / 100) * 100;
+  const QueryArgs Q{src, dist, depth, nullptr, ice_arg, (long long)n, flags};
+  const Park park{out + 4 * ld, out, 1};
+  const dim3 grid(grid_for((long long)n)), block(kBlock);
+  hipLaunchKernelGGL(roots_kernel<IN_CM100>, grid, block, 0, st, M, I, Q, park);
+  hipLaunchKernelGGL(lookup_fallback_out_kernel, grid, block, 0, st, M, I, Q, out, ld, ok);
   return launch_ok();
 }
 

@@ -461,6 +461,36 @@ int airice_hdtip_launch(const airice_medium* m, const double* d_src_cm, const do
                       (hipStream_t)stream);
 }
 
+int airice_table_lookup_launch(const airice_medium* m, const airice_lookup_table* t,
+                               const double* d_src_cm, const double* d_dist_cm,
+                               const double* d_depth_cm, double ice_cm, size_t n, double* d_out,
+                               size_t ld, uint8_t* d_ok, uint8_t* d_flags, void* stream) {
+  if (t == nullptr || t->table == nullptr ||
+      (n > 0 && (d_src_cm == nullptr || d_dist_cm == nullptr || d_depth_cm == nullptr ||
+                 d_out == nullptr || d_ok == nullptr || d_flags == nullptr))) {
+    set_error("null argument");
+    return AIRICE_EINVAL;
+  }
+  if (ld < n) {
+    set_error("ld < n");
+    return AIRICE_EINVAL;
+  }
+  if (t->n_entries == 0 || t->ld < t->n_entries || t->total_angle_steps < 1 ||
+      t->total_height_steps < 1 || !(t->height_step > 0)) {
+    set_error("invalid lookup table description");
+    return AIRICE_EINVAL;
+  }
+  DevMedium M;
+  int rc = build_dev_medium(m, AIRICE_VARIANT_MULTIRAY, &M);
+  if (rc) return rc;
+  IceConsts I;
+  build_ice_consts(M, ice_cm / 100, 0.0, &I);
+  rc = launch_lookup(M, I, t, d_src_cm, d_dist_cm, d_depth_cm, ice_cm, n, d_out, ld, d_ok,
+                     d_flags, (hipStream_t)stream);
+  if (rc) set_error("lookup launch failed: %s", hipGetErrorString(hipGetLastError()));
+  return rc;
+}
+
 int airice_trace_ice_to_air_launch(const airice_medium* m, const double* d_depth,
                                    const double* d_ice, const double* d_txh, const double* d_dist,
                                    size_t n, double* d_out10, void* stream) {

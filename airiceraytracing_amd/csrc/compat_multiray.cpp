@@ -49,6 +49,54 @@ double* scratch() {
   return g_scratch;
 }
 
+// HBM copy of AllTableAllAntData[i]: adopted from MakeRayTracingTable, or uploaded when the
+// host table at that index is not the one last seen (a caller-filled or replaced table).
+struct DevTable {
+  const float* host0 = nullptr;  // AllTableAllAntData[i][0].data() when mirrored
+  size_t n = 0;
+  float* dev = nullptr;
+};
+std::vector<DevTable> g_tables;
+
+const float* device_table(int index, size_t* n_out) {
+  if (index < 0 || index >= (int)AllTableAllAntData.size()) {
+    std::fprintf(stderr, "MultiRayAirIceRefraction: no table %d (%zu made)\n", index,
+                 AllTableAllAntData.size());
+    std::abort();  // the reference indexes out of range here (UB); fail loudly instead
+  }
+  const std::vector<std::vector<float>>& cols = AllTableAllAntData[index];
+  if (cols.size() < AIRICE_TABLE_COLUMNS || cols[0].empty()) die("table lookup (malformed table)");
+  const size_t n = cols[0].size();
+  if (g_tables.size() <= (size_t)index) g_tables.resize(index + 1);
+  DevTable& t = g_tables[index];
+  *n_out = n;
+  if (t.dev != nullptr && t.host0 == cols[0].data() && t.n == n) return t.dev;
+  if (t.dev != nullptr) (void)hipFree(t.dev);
+  t.dev = nullptr;
+  if (hipMalloc(&t.dev, sizeof(float) * AIRICE_TABLE_COLUMNS * n) != hipSuccess) die("hipMalloc");
+  for (int c = 0; c < AIRICE_TABLE_COLUMNS; ++c) {
+    if (cols[c].size() != n) die("table lookup (ragged table)");
+    if (hipMemcpy(t.dev + (size_t)c * n, cols[c].data(), sizeof(float) * n,
+                  hipMemcpyHostToDevice) != hipSuccess)
+      die("hipMemcpy table");
+  }
+  t.host0 = cols[0].data();
+  t.n = n;
+  return t.dev;
+}
+
+airice_lookup_table lookup_desc(const float* dev, size_t n) {
+  airice_lookup_table t;
+  t.table = dev;
+  t.ld = n;
+  t.n_entries = n;
+  t.loop_stop_height = LoopStopHeight;  // globals of the last table made (.cc:1035-1039)
+  t.height_step = HeightStepSize;
+  t.total_height_steps = TotalHeightSteps;
+  t.total_angle_steps = TotalAngleSteps;
+  return t;
+}
+
 }  // namespace
 
 namespace MultiRayAirIceRefraction {
@@ -190,9 +238,80 @@ int MakeRayTracingTable(double AntennaDepth, double IceLayerHeight, int AntennaN
     if (hipMemcpy(cols[c].data(), dt + (size_t)c * n, sizeof(float) * n, hipMemcpyDeviceToHost) !=
         hipSuccess)
       die("hipMemcpy table");
-  (void)hipFree(dt);
   AllTableAllAntData.push_back(std::move(cols));
+  // keep the HBM copy for the lookups (moving the column vectors keeps their storage)
+  const size_t index = AllTableAllAntData.size() - 1;
+  if (g_tables.size() <= index) g_tables.resize(index + 1);
+  if (g_tables[index].dev != nullptr) (void)hipFree(g_tables[index].dev);
+  g_tables[index].dev = dt;
+  g_tables[index].host0 = AllTableAllAntData[index][0].data();
+  g_tables[index].n = n;
   return 0;
+}
+
+bool TableLookup(double SrcHeightASL, double HorizontalDistanceToRx,
+                 double RxDepthBelowIceBoundary, double IceLayerHeight, int TableIndex,
+                 double& opticalPathLengthInIce, double& opticalPathLengthInAir,
+                 double& geometricalPathLengthInIce, double& geometricalPathLengthInAir,
+                 double& launchAngle, double& horizontalDistanceToIntersectionPoint,
+                 double& transmissionCoefficientS, double& transmissionCoefficientP,
+                 double& RecievedAngleInIce) {
+  const double src[1] = {SrcHeightASL}, dist[1] = {HorizontalDistanceToRx},
+               dep[1] = {RxDepthBelowIceBoundary};
+  double o[9];
+  bool ok = false;
+  TableLookupBatch(src, dist, dep, IceLayerHeight, TableIndex, 1, o, &ok);
+  opticalPathLengthInIce = o[0];
+  opticalPathLengthInAir = o[1];
+  geometricalPathLengthInIce = o[2];
+  geometricalPathLengthInAir = o[3];
+  launchAngle = o[4];
+  horizontalDistanceToIntersectionPoint = o[5];
+  transmissionCoefficientS = o[6];
+  transmissionCoefficientP = o[7];
+  RecievedAngleInIce = o[8];
+  return ok;
+}
+
+void TableLookupBatch(const double* SrcHeightASL, const double* HorizontalDistanceToRx,
+                      const double* RxDepthBelowIceBoundary, double IceLayerHeight, int TableIndex,
+                      size_t n, double* out9, bool* ok) {
+  const airice_medium& m = medium();
+  std::lock_guard<std::mutex> lock(g_mu);
+  size_t entries = 0;
+  const float* dev = device_table(TableIndex, &entries);
+  // MaxAirTxHeight / MinAirTxHeight globals (.cc:1359-1360)
+  MaxAirTxHeight = AllTableAllAntData[TableIndex][0][0];
+  MinAirTxHeight = AllTableAllAntData[TableIndex][0][entries - 1];
+  if (n == 0) return;
+  // one device block: src | dist | depth | out (9 columns) | ok | flags
+  const size_t bytes = sizeof(double) * 12 * n + 2 * n;
+  const bool small = bytes <= kScratch * sizeof(double);
+  double* d = small ? scratch() : nullptr;
+  if (!small && hipMalloc(&d, bytes) != hipSuccess) die("hipMalloc");
+  if (hipMemcpy(d, SrcHeightASL, sizeof(double) * n, hipMemcpyHostToDevice) != hipSuccess ||
+      hipMemcpy(d + n, HorizontalDistanceToRx, sizeof(double) * n, hipMemcpyHostToDevice) !=
+          hipSuccess ||
+      hipMemcpy(d + 2 * n, RxDepthBelowIceBoundary, sizeof(double) * n, hipMemcpyHostToDevice) !=
+          hipSuccess)
+    die("hipMemcpy");
+  uint8_t* dok = reinterpret_cast<uint8_t*>(d + 12 * n);
+  uint8_t* dfl = dok + n;
+  const airice_lookup_table t = lookup_desc(dev, entries);
+  if (airice_table_lookup_launch(&m, &t, d, d + n, d + 2 * n, IceLayerHeight, n, d + 3 * n, n,
+                                 dok, dfl, nullptr) != AIRICE_OK)
+    die("GetHorizontalDistanceToIntersectionPoint_Table");
+  std::vector<double> soa(9 * n);
+  std::vector<uint8_t> hok(n);
+  if (hipMemcpy(soa.data(), d + 3 * n, sizeof(double) * 9 * n, hipMemcpyDeviceToHost) !=
+          hipSuccess ||
+      hipMemcpy(hok.data(), dok, n, hipMemcpyDeviceToHost) != hipSuccess)
+    die("hipMemcpy");
+  if (!small) (void)hipFree(d);
+  for (size_t i = 0; i < n; ++i) {
+    for (int c = 0; c < 9; ++c) out9[i * 9 + c] = soa[(size_t)c * n + i];
+    ok[i] = hok[i] != 0;
+  }
 }
 
 }  // namespace MultiRayAirIceRefraction

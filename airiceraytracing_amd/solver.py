@@ -16,7 +16,8 @@ import ctypes
 import numpy as np
 
 from . import _lib
-from ._lib import (Grid, Medium, VARIANT_MULTIRAY, VARIANT_PYWRAPPER, check, lib, ptr)
+from ._lib import (Grid, LookupTable, Medium, VARIANT_MULTIRAY, VARIANT_PYWRAPPER, check, lib,
+                   ptr)
 
 
 def make_grid(antenna_depth_cm: float, ice_height_cm: float, height_step: float = 10.0,
@@ -112,6 +113,35 @@ class AirIceSolver:
                                         ptr(depth_cm), ice_cm, n, ptr(out),
                                         n if ld is None else ld, ptr(ok),
                                         _stream_handle(stream)), "airice_hdtip_launch")
+
+    # ------------------------------------------------------------------ table lookup
+    @staticmethod
+    def lookup_table(table, grid: Grid, n_entries: int | None = None,
+                     ld: int | None = None) -> LookupTable:
+        """Describe an HBM-resident table (11 float columns, column stride ``ld``) for
+        ``table_lookup_device``; ``grid`` supplies the globals of the last table made
+        (LoopStopHeight, HeightStepSize, TotalHeightSteps, TotalAngleSteps, .cc:1035-1039)."""
+        n = grid.n_rays if n_entries is None else n_entries
+        t = LookupTable()
+        t.table = ptr(table).value
+        t.ld = n if ld is None else ld
+        t.n_entries = n
+        t.loop_stop_height = grid.stop_height
+        t.height_step = grid.height_step
+        t.total_height_steps = grid.height_steps
+        t.total_angle_steps = grid.angle_steps
+        return t
+
+    def table_lookup_device(self, lt: LookupTable, src_cm, dist_cm, depth_cm, ice_cm: float,
+                            out, ok, flags, ld: int | None = None, stream=None) -> None:
+        """Batched GetHorizontalDistanceToIntersectionPoint_Table (.cc:1305-1462): out is the
+        9 double columns of ``hdtip_device``; ok the returned bool; flags AIRICE_LOOKUP_*."""
+        n = int(src_cm.numel())
+        check(lib().airice_table_lookup_launch(ctypes.byref(self.medium), ctypes.byref(lt),
+                                               ptr(src_cm), ptr(dist_cm), ptr(depth_cm), ice_cm,
+                                               n, ptr(out), n if ld is None else ld, ptr(ok),
+                                               ptr(flags), _stream_handle(stream)),
+              "airice_table_lookup_launch")
 
     # ------------------------------------------------------------------ pythonwrapper
     def trace_ice_to_air_device(self, depth, ice, txh, dist, out10, stream=None) -> None:

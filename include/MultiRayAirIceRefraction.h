@@ -6,7 +6,8 @@
  * (e.g. RunMultiRayCode.C:29-59) compile and link against libairice.so unchanged, minus the
  * `#include "MultiRayAirIceRefraction.cc"` line.  The hot path -- MakeRayTracingTable
  * (.cc:2019), GetRayTracingSolutions (.cc:1796), Air2IceRayTracing (.cc:1464),
- * GetHorizontalDistanceToIntersectionPoint (.cc:945) -- runs on the MI355X.
+ * GetHorizontalDistanceToIntersectionPoint (.cc:945) and its table variant _Table (.cc:1305)
+ * -- runs on the MI355X.
  *
  * Not provided: the GSL-typed internals (FindFunctionRoot, gsl_* statics) and the helpers
  * that return heap scratch arrays (GetLayerHitPointPar, Get{Air,Ice}PropagationPar,
@@ -21,6 +22,7 @@
 #ifndef AIRICE_MULTIRAYAIRICEREFRACTION_H
 #define AIRICE_MULTIRAYAIRICEREFRACTION_H
 
+#include <cstddef>
 #include <vector>
 
 /* Defined by the caller (reference .h:23-24, RunMultiRayCode.C:3-4). */
@@ -88,6 +90,47 @@ void GetRayTracingSolutions(double RayLaunchAngleInAir, double AirTxHeight, doub
  * AllTableAllAntData using the grid globals above (the reference's defaults: 100 km to the ice
  * in 10 m steps x 90.1..180 deg in 0.1 deg steps).  Returns 0. */
 int MakeRayTracingTable(double AntennaDepth, double IceLayerHeight, int AntennaNumber);
+
+/* Table lookup on an already-resolved table index (AllTableAllAntData[TableIndex]), run on the
+ * GPU against the table's HBM copy (kept from MakeRayTracingTable, or uploaded on first use
+ * when AllTableAllAntData[TableIndex] was filled by the caller).  Same outputs, units, globals
+ * (MaxAirTxHeight / MinAirTxHeight are set) and quirks as the reference (.cc:1305-1462). */
+bool TableLookup(double SrcHeightASL, double HorizontalDistanceToRx,
+                 double RxDepthBelowIceBoundary, double IceLayerHeight, int TableIndex,
+                 double& opticalPathLengthInIce, double& opticalPathLengthInAir,
+                 double& geometricalPathLengthInIce, double& geometricalPathLengthInAir,
+                 double& launchAngle, double& horizontalDistanceToIntersectionPoint,
+                 double& transmissionCoefficientS, double& transmissionCoefficientP,
+                 double& RecievedAngleInIce);
+
+/* Batched form: n queries (cm) against one resolved table; out is n rows of the 9 outputs in
+ * the reference's argument order; ok[i] the returned bool.  One launch for the whole batch. */
+void TableLookupBatch(const double* SrcHeightASL, const double* HorizontalDistanceToRx,
+                      const double* RxDepthBelowIceBoundary, double IceLayerHeight, int TableIndex,
+                      size_t n, double* out9, bool* ok);
+
+/* GetHorizontalDistanceToIntersectionPoint_Table (.cc:1305).  The antenna -> table remap reads
+ * the caller-owned AntennaDepths / AntennaTableAlreadyMade (.cc:1348-1352), so it is compiled
+ * into the caller here; the lookup itself runs in libairice.so. */
+inline bool GetHorizontalDistanceToIntersectionPoint_Table(
+    double SrcHeightASL, double HorizontalDistanceToRx, double RxDepthBelowIceBoundary,
+    double IceLayerHeight, int AntennaNumber, double& opticalPathLengthInIce,
+    double& opticalPathLengthInAir, double& geometricalPathLengthInIce,
+    double& geometricalPathLengthInAir, double& launchAngle,
+    double& horizontalDistanceToIntersectionPoint, double& transmissionCoefficientS,
+    double& transmissionCoefficientP, double& RecievedAngleInIce) {
+  for (int j = 0; j < (int)AntennaTableAlreadyMade.size(); j++) {
+    if (AntennaDepths[AntennaNumber] == AntennaDepths[AntennaTableAlreadyMade[j]]) {
+      AntennaNumber = j;
+    }
+  }
+  return TableLookup(SrcHeightASL, HorizontalDistanceToRx, RxDepthBelowIceBoundary,
+                     IceLayerHeight, AntennaNumber, opticalPathLengthInIce,
+                     opticalPathLengthInAir, geometricalPathLengthInIce,
+                     geometricalPathLengthInAir, launchAngle,
+                     horizontalDistanceToIntersectionPoint, transmissionCoefficientS,
+                     transmissionCoefficientP, RecievedAngleInIce);
+}
 
 }  // namespace MultiRayAirIceRefraction
 

@@ -142,6 +142,37 @@ int airice_hdtip_launch(const airice_medium *m, const double *d_src_cm, const do
                         const double *d_depth_cm, double ice_cm, size_t n, double *d_out,
                         size_t ld, uint8_t *d_ok, void *stream);
 
+/* --- table lookup (GetHorizontalDistanceToIntersectionPoint_Table) -------- */
+/* One antenna's table resident in HBM (the AllTableAllAntData[ant] a MakeRayTracingTable /
+ * airice_table_launch produced) plus the grid globals the reference reads at lookup time
+ * (LoopStopHeight, HeightStepSize, TotalHeightSteps, TotalAngleSteps of the LAST table made,
+ * .cc:1035-1039). */
+typedef struct airice_lookup_table {
+  const float *table;         /* device: column c of entry i at table[c*ld + i] */
+  size_t ld;                  /* column stride in floats */
+  size_t n_entries;           /* AllTableAllAntData[ant][0].size() */
+  double loop_stop_height;    /* m */
+  double height_step;         /* m */
+  int32_t total_height_steps;
+  int32_t total_angle_steps;
+} airice_lookup_table;
+
+#define AIRICE_LOOKUP_FALLBACK 1 /* the minimizer fallback ran (.cc:1418-1420) */
+#define AIRICE_LOOKUP_UNPINNED 2 /* the reference reads uninitialised/out-of-range memory here:
+                                    such slots are returned as 0 / NaN */
+
+/* Batched GetHorizontalDistanceToIntersectionPoint_Table (.cc:1305-1462) for one antenna
+ * (AntennaNumber already resolved by the caller, .cc:1348-1352): cm inputs, ice height
+ * uniform; d_out: the 9 double columns of airice_hdtip_launch, d_ok: the returned bool,
+ * d_flags (required): AIRICE_LOOKUP_* bits.  Lanes hitting the reference's one-sided
+ * extrapolation case run its minimizer fallback on the device, with the reference's
+ * argument handling (cm values scaled by 100 once more, optical/geometric slots swapped). */
+int airice_table_lookup_launch(const airice_medium *m, const airice_lookup_table *t,
+                               const double *d_src_cm, const double *d_dist_cm,
+                               const double *d_depth_cm, double ice_cm, size_t n,
+                               double *d_out, size_t ld, uint8_t *d_ok, uint8_t *d_flags,
+                               void *stream);
+
 /* pythonwrapper TraceIceToAir, batched: per-query (depth, ice, txh, dist) metres ->
  * ArrayParameters[10] rows (TraceIceToAir.C:46-68), row-major n x 10. */
 int airice_trace_ice_to_air_launch(const airice_medium *m, const double *d_depth,

@@ -31,6 +31,8 @@ SOLVE_PROBED = 8
 SOLVE_MAXITER = 16
 SOLVE_NO_AIR_LAYER = 32
 SOLVE_UNPINNED = SOLVE_NONFINITE_END | SOLVE_BAD_BRACKET | SOLVE_NO_AIR_LAYER
+LOOKUP_FALLBACK = 1  # minimizer fallback ran (.cc:1418-1420)
+LOOKUP_UNPINNED = 2  # the reference reads uninitialised / out-of-range memory
 
 
 class Medium(ctypes.Structure):
@@ -111,6 +113,11 @@ def lib():
         L.or_py_trace_ice_to_air.argtypes = [M, D, D, D, D, P]
         L.or_py_trace_ice_to_air.restype = I
         L.or_py_trace_batch.argtypes = [M, P, P, P, P, ctypes.c_size_t, P, I]
+        L.or_table_lookup.argtypes = [M, ctypes.POINTER(LookupTable), D, D, D, D, P,
+                                      ctypes.POINTER(I)]
+        L.or_table_lookup.restype = I
+        L.or_table_lookup_batch.argtypes = [M, ctypes.POINTER(LookupTable), P, P, P, D,
+                                            ctypes.c_size_t, P, ctypes.c_size_t, P, P, I]
         _lib = L
     return _lib
 
@@ -230,3 +237,49 @@ def py_trace_batch(m: Medium, depth, ice, txh, dist, nthreads: int = 0):
     out = np.zeros((n, 10))
     lib().or_py_trace_batch(ctypes.byref(m), *[_ptr(a) for a in arrs], n, _ptr(out), nthreads)
     return out
+
+
+class LookupTable(ctypes.Structure):
+    """or_lookup_table: one antenna's AllTableAllAntData[ant] + the grid globals (.cc:1035)."""
+    _fields_ = [("col", ctypes.c_void_p * 11), ("n", ctypes.c_long),
+                ("LoopStopHeight", ctypes.c_double), ("HeightStepSize", ctypes.c_double),
+                ("TotalHeightSteps", ctypes.c_int), ("TotalAngleSteps", ctypes.c_int)]
+
+
+def lookup_table(table: np.ndarray, g: Grid) -> LookupTable:
+    """table: (11, n) float32 (C-contiguous, kept alive by the caller); g: the grid of the
+    last table made (its stop height / step / row and angle counts)."""
+    assert table.dtype == np.float32 and table.flags.c_contiguous and table.shape[0] == 11
+    t = LookupTable()
+    for c in range(11):
+        t.col[c] = table[c].ctypes.data
+    t.n = table.shape[1]
+    t.LoopStopHeight = g.stop_height
+    t.HeightStepSize = g.height_step
+    t.TotalHeightSteps = g.height_steps
+    t.TotalAngleSteps = g.angle_steps
+    return t
+
+
+def table_lookup(m: Medium, t: LookupTable, src_cm, dist_cm, depth_cm, ice_cm):
+    """GetHorizontalDistanceToIntersectionPoint_Table (.cc:1305-1462) for one query:
+    (ok, outs[9], flags)."""
+    out = np.zeros(9)
+    fl = ctypes.c_int(0)
+    ok = lib().or_table_lookup(ctypes.byref(m), ctypes.byref(t), src_cm, dist_cm, depth_cm,
+                               ice_cm, _ptr(out), ctypes.byref(fl))
+    return bool(ok), out, fl.value
+
+
+def table_lookup_batch(m: Medium, t: LookupTable, src_cm, dist_cm, depth_cm, ice_cm,
+                       nthreads: int = 0):
+    """Vector form of ``table_lookup``: (out (9, n), ok (n,) uint8, flags (n,) uint8)."""
+    arrs = [np.ascontiguousarray(np.broadcast_to(a, np.shape(src_cm)), dtype=np.float64).ravel()
+            for a in (src_cm, dist_cm, depth_cm)]
+    n = arrs[0].size
+    out = np.zeros((9, n))
+    ok = np.zeros(n, dtype=np.uint8)
+    fl = np.zeros(n, dtype=np.uint8)
+    lib().or_table_lookup_batch(ctypes.byref(m), ctypes.byref(t), *[_ptr(a) for a in arrs],
+                                ice_cm, n, _ptr(out), n, _ptr(ok), _ptr(fl), nthreads)
+    return out, ok, fl

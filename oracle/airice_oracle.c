@@ -825,3 +825,223 @@ void or_py_trace_batch(const or_medium *m, const double *depth, const double *ic
   for (long i = 0; i < (long)n; i++)
     or_py_trace_ice_to_air(m, depth[i], ice[i], txh[i], dist[i], out10 + 10 * i);
 }
+
+/* ------------------------------------------------------------------------- */
+/* Table lookup (.cc:992-1462)                                                */
+/* ------------------------------------------------------------------------- */
+static double lk_interp(double x, double xa, double ya, double xb, double yb) {
+  return ya + (yb - ya) * ((x - xa) / (xb - xa)); /* .cc:992-995 */
+}
+
+/* bounded column read; out of range -> NaN and the UB flag (the reference reads past the vector) */
+static double lk_at(const or_lookup_table *t, int c, long i, int *flags) {
+  if (i < 0 || i >= t->n) { *flags |= OR_LK_UNPINNED; return NAN; }
+  return (double)t->col[c][i];
+}
+
+/* FindClosestAirTxHeight (.cc:1033-1126) */
+static void lk_closest_txh(const or_lookup_table *t, double P, long *s1, long *e1, double *c1,
+                           long *s2, long *e2, double *c2, int *flags) {
+  int CurrentHeightStep = (int)floor((P - t->LoopStopHeight) / t->HeightStepSize);
+  int Index = t->TotalHeightSteps - CurrentHeightStep - 1;
+  long MaxAngleBin = (long)Index * t->TotalAngleSteps + t->TotalAngleSteps - 1;
+  long MinAngleBin = (long)Index * t->TotalAngleSteps + 0;
+  double val = -0.001;
+  long StartBin = MaxAngleBin;
+  int went = 0;
+  while ((val != 0 && val < 0.01) || isnan(val)) {
+    if (StartBin < 0) { *flags |= OR_LK_UNPINNED; break; }
+    val = lk_at(t, 1, StartBin, flags);
+    StartBin--;
+    went = 1;
+  }
+  if (went) StartBin = StartBin + 1;
+  val = -0.001;
+  long EndBin = MinAngleBin;
+  went = 0;
+  while ((val != 0 && val < 0.01) || isnan(val)) {
+    if (EndBin >= t->n) { *flags |= OR_LK_UNPINNED; break; }
+    val = lk_at(t, 1, EndBin, flags);
+    EndBin++;
+    went = 1;
+  }
+  if (went) EndBin = EndBin - 1;
+  *s1 = EndBin;
+  *e1 = StartBin;
+  *c1 = fabs(lk_at(t, 0, Index, flags) - P); /* sic: row index used as a ray index */
+  *s2 = *s1 - t->TotalAngleSteps;
+  *e2 = *e1 - t->TotalAngleSteps;
+  if (*s2 < 0) *s2 = *s1 + t->TotalAngleSteps;
+  if (*e2 < 0) *e2 = *e1 + t->TotalAngleSteps;
+  *c2 = fabs(lk_at(t, 0, Index, flags) - P);
+}
+
+/* FindClosestTHD (.cc:1128-1169) */
+static void lk_closest_thd(const or_lookup_table *t, double P, long StartIndex, long EndIndex,
+                           long *rs, long *re, double *cv, int *flags) {
+  long MidIndex;
+  for (int i = 0; i < 8; i++) {
+    if (EndIndex - StartIndex >= 3) {
+      MidIndex = (long)floor((double)((StartIndex + EndIndex) / 2));
+      if (lk_at(t, 1, MidIndex, flags) - P > 0) StartIndex = MidIndex;
+      if (lk_at(t, 1, MidIndex, flags) - P < 0) EndIndex = MidIndex;
+    }
+  }
+  double minimum = 100000000000;
+  long index2 = 0;
+  for (long ipnt = StartIndex; ipnt < EndIndex + 1; ipnt++) {
+    double v = lk_at(t, 1, ipnt, flags);
+    double minval = fabs(v - P);
+    if (minval < minimum && v > P) {
+      minimum = minval;
+    } else {
+      index2 = ipnt;
+      break;
+    }
+  }
+  long index1 = index2 - 1;
+  minimum = fabs(P - lk_at(t, 1, index2, flags));
+  if (minimum > fabs(P - lk_at(t, 1, index1, flags))) minimum = fabs(P - lk_at(t, 1, index1, flags));
+  *rs = index1;
+  *re = index2;
+  *cv = minimum;
+}
+
+/* GetParValues (.cc:1172-1302) */
+static void lk_par_values(const or_lookup_table *t, double H, double D, double *H1, double Par1[10],
+                          double *H2, double Par2[10], int *flags) {
+  long TotalTableEntries = t->n - 1;
+  double MinAirTxHeight = lk_at(t, 0, TotalTableEntries, flags);
+  long si[4] = {0, 0, 0, 0}, ei[4] = {0, 0, 0, 0};
+  double cv[3] = {0, 0, 0};
+  lk_closest_txh(t, H, &si[0], &ei[0], &cv[0], &si[2], &ei[2], &cv[2], flags);
+  *H1 = lk_at(t, 0, si[0], flags);
+  double MaxTHD = lk_at(t, 1, si[0], flags);
+  if (D <= MaxTHD) {
+    lk_closest_thd(t, D, si[0], ei[0], &si[1], &ei[1], &cv[1], flags);
+    if (cv[1] != 0) {
+      double x1 = lk_at(t, 1, si[1], flags), x2 = lk_at(t, 1, ei[1], flags);
+      for (int ip = 0; ip < 10; ip++)
+        Par1[ip] = lk_interp(D, x1, lk_at(t, 1 + ip, si[1], flags), x2, lk_at(t, 1 + ip, ei[1], flags));
+    }
+    if (cv[1] == 0) {
+      si[1] = si[1] + 1;
+      ei[1] = si[1];
+      for (int ip = 0; ip < 10; ip++) Par1[ip] = lk_at(t, 1 + ip, si[1], flags);
+    }
+  } else {
+    for (int ip = 0; ip < 10; ip++) Par1[ip] = -1e9;
+  }
+  if (cv[0] != 0 && H > MinAirTxHeight && si[2] < TotalTableEntries) {
+    *H2 = lk_at(t, 0, si[2], flags);
+    MaxTHD = lk_at(t, 1, si[2], flags);
+    if (D <= MaxTHD) {
+      lk_closest_thd(t, D, si[2], ei[2], &si[3], &ei[3], &cv[2], flags);
+      if (cv[2] != 0) {
+        double x1 = lk_at(t, 1, si[3], flags), x2 = lk_at(t, 1, ei[3], flags);
+        for (int ip = 0; ip < 10; ip++)
+          Par2[ip] = lk_interp(D, x1, lk_at(t, 1 + ip, si[3], flags), x2, lk_at(t, 1 + ip, ei[3], flags));
+      }
+      if (cv[2] == 0) {
+        si[3] = si[3] + 1;
+        ei[3] = si[3];
+        for (int ip = 0; ip < 10; ip++) Par2[ip] = lk_at(t, 1 + ip, si[3], flags);
+      }
+    } else {
+      for (int ip = 0; ip < 10; ip++) Par2[ip] = -1e9;
+    }
+  } else {
+    *H2 = *H1;
+    for (int ip = 0; ip < 10; ip++) Par2[ip] = Par1[ip];
+  }
+}
+
+/* GetHorizontalDistanceToIntersectionPoint_Table (.cc:1305-1462); AntennaNumber already
+ * resolved to the table `t`.  Slots the reference leaves uninitialised are returned as 0
+ * with OR_LK_UNPINNED set. */
+int or_table_lookup(const or_medium *m, const or_lookup_table *t, double SrcHeightASL,
+                    double HorizontalDistanceToRx, double RxDepthBelowIceBoundary,
+                    double IceLayerHeight, double o[9], int *flags) {
+  const double pi = m->pi;
+  *flags = 0;
+  double AirTxHeight = SrcHeightASL / 100;
+  double HorizontalDistance = HorizontalDistanceToRx / 100;
+  IceLayerHeight = IceLayerHeight / 100;
+  int CheckSolution = 1;
+  long TotalTableEntries = t->n - 1;
+  double MaxAirTxHeight = lk_at(t, 0, 0, flags);
+  double MinAirTxHeight = lk_at(t, 0, TotalTableEntries, flags);
+  double x1 = 0, x2 = 0, y1 = 0, y2 = 0;
+  double Par1[15], Par2[15], piv[15];
+  int set[15];
+  for (int i = 0; i < 15; i++) { piv[i] = 0; set[i] = 0; }
+  if (AirTxHeight <= MaxAirTxHeight && AirTxHeight >= MinAirTxHeight && AirTxHeight > 0) {
+    double H1, H2;
+    lk_par_values(t, AirTxHeight, HorizontalDistance, &H1, Par1, &H2, Par2, flags);
+    x1 = H1;
+    x2 = H2;
+    for (int ipar = 0; ipar < 10; ipar++) {
+      y1 = Par1[ipar];
+      y2 = Par2[ipar];
+      double v = 0;
+      int checkval = (y1 == -1e9 || y2 == -1e9);
+      if (x1 != x2 && checkval == 0) {
+        v = lk_interp(AirTxHeight, x1, y1, x2, y2);
+      } else {
+        if (x1 == x2 && y1 == y2) v = Par1[ipar];
+        if (y2 == -1e9 && y1 == -1e9) ipar = 9;
+      }
+      piv[ipar] = v;
+      set[ipar] = 1;
+    }
+  }
+  for (int i = 0; i < 10; i++)
+    if (!set[i]) *flags |= OR_LK_UNPINNED;
+  double THD = piv[0];
+  o[0] = piv[1] * 100; /* opticalPathLengthInIce */
+  o[1] = piv[2] * 100; /* opticalPathLengthInAir */
+  o[2] = piv[8] * 100; /* geometricalPathLengthInIce */
+  o[3] = piv[7] * 100; /* geometricalPathLengthInAir */
+  o[4] = piv[3] * (pi / 180);
+  o[5] = piv[4] * 100;
+  o[6] = piv[5];
+  o[7] = piv[6];
+  o[8] = piv[9] * (pi / 180);
+  int CheckSolBool = 0;
+  int one = (y1 == -1e9 && y2 != -1e9) || (y2 == -1e9 && y1 != -1e9);
+  if (one) {
+    /* .cc:1419: cm arguments scaled by 100 again, optical/geometric slots swapped */
+    double f[9];
+    CheckSolBool = or_hdtip(m, SrcHeightASL * 100, HorizontalDistanceToRx * 100,
+                            RxDepthBelowIceBoundary * 100, IceLayerHeight * 100, f);
+    o[2] = f[0]; o[3] = f[1]; o[0] = f[2]; o[1] = f[3];
+    o[4] = f[4]; o[5] = f[5]; o[6] = f[6]; o[7] = f[7]; o[8] = f[8];
+    *flags |= OR_LK_FALLBACK;
+  }
+  if (y2 == -1e9 && y1 == -1e9) CheckSolution = 0;
+  if (one && CheckSolBool == 0) CheckSolution = 0;
+  if (AirTxHeight > MaxAirTxHeight) CheckSolution = 0;
+  if (AirTxHeight < MinAirTxHeight) CheckSolution = 0;
+  if (AirTxHeight < 0) CheckSolution = 0;
+  if (o[4] < 0) CheckSolution = 0;
+  if ((fabs(THD - HorizontalDistance) / HorizontalDistance > 0.01 && HorizontalDistance <= 100) ||
+      (fabs(THD - HorizontalDistance) > 1 && HorizontalDistance > 100))
+    CheckSolution = 0;
+  if (CheckSolution == 0) { o[0] = 0; o[1] = 0; o[4] = 0; o[5] = 0; }
+  return CheckSolution;
+}
+
+void or_table_lookup_batch(const or_medium *m, const or_lookup_table *t, const double *src_cm,
+                           const double *dist_cm, const double *depth_cm, double ice_cm, size_t n,
+                           double *out, size_t ld, unsigned char *ok, unsigned char *flags,
+                           int nthreads) {
+  if (nthreads <= 0) nthreads = omp_get_max_threads();
+#pragma omp parallel for schedule(dynamic, 256) num_threads(nthreads)
+  for (long i = 0; i < (long)n; ++i) {
+    double o[9];
+    int fl = 0;
+    ok[i] = (unsigned char)or_table_lookup(m, t, src_cm[i], dist_cm[i], depth_cm[i], ice_cm, o, &fl);
+    flags[i] = (unsigned char)fl;
+    for (int c = 0; c < 9; ++c) out[(size_t)c * ld + (size_t)i] = o[c];
+  }
+}

@@ -120,3 +120,28 @@ void or_py_trace_batch(const or_medium *m, const double *depth, const double *ic
 }
 #endif
 #endif
+
+/* ---- Table lookup: GetHorizontalDistanceToIntersectionPoint_Table ----------
+ * .cc:1305-1462 with GetParValues :1172-1302, FindClosestAirTxHeight :1033-1126,
+ * FindClosestTHD :1128-1169, oneDLinearInterpolation :992-995.  The table is one antenna's
+ * AllTableAllAntData[ant] (11 float columns of n entries); the grid globals are those of the
+ * LAST MakeRayTracingTable call (the reference reads them, .cc:1035). */
+typedef struct or_lookup_table {
+  const float *col[11];
+  long n;
+  double LoopStopHeight, HeightStepSize;
+  int TotalHeightSteps, TotalAngleSteps;
+} or_lookup_table;
+/* flags of one lookup */
+enum {
+  OR_LK_FALLBACK = 1, /* the minimizer fallback ran (.cc:1418-1420, with its x100 argument quirk) */
+  OR_LK_UNPINNED = 2  /* outputs read uninitialised / out-of-range memory in the reference */
+};
+/* outs[9] in the order of the reference's reference arguments; returns CheckSolution. */
+int or_table_lookup(const or_medium *m, const or_lookup_table *t, double src_cm, double dist_cm,
+                    double depth_cm, double ice_cm, double outs[9], int *flags);
+/* n queries (cm) against one table; out: 9 columns of stride ld; ok/flags per query. */
+void or_table_lookup_batch(const or_medium *m, const or_lookup_table *t, const double *src_cm,
+                           const double *dist_cm, const double *depth_cm, double ice_cm, size_t n,
+                           double *out, size_t ld, unsigned char *ok, unsigned char *flags,
+                           int nthreads);

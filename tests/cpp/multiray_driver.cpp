@@ -57,7 +57,38 @@ int main() {
   std::printf("\"LoopStopHeight\": %.17g,\n", LoopStopHeight);
   std::vector<double> t1;
   for (int c = 0; c < 11; ++c) t1.push_back(AllTableAllAntData[1][c][123]);
-  arr("table1_row123", t1.data(), 11, true);
+  arr("table1_row123", t1.data(), 11);
+  // table lookups through the reference entry (antenna 1 -> table 0, antenna 2 -> table 1)
+  const double q[][2] = {{5000e2, 1000e2},  {20000e2, 15000e2}, {3500e2, 100e2},
+                         {99999e2, 30000e2}, {200000e2, 1000e2}, {8000e2, 1e9},
+                         {60000e2, 42000e2}, {3000e2, 10e2}};
+  const int nq = sizeof(q) / sizeof(q[0]);
+  std::printf("\"lookup\": [\n");
+  for (int a = 0; a < 3; ++a)
+    for (int i = 0; i < nq; ++i) {
+      double r[10];
+      bool okl = M::GetHorizontalDistanceToIntersectionPoint_Table(
+          q[i][0], q[i][1], AntennaDepths[a], 3000 * 100., a, r[1], r[2], r[3], r[4], r[5], r[6],
+          r[7], r[8], r[9]);
+      r[0] = okl ? 1 : 0;
+      std::printf("[%d, %.17g, %.17g, ", a, q[i][0], q[i][1]);
+      for (int c = 0; c < 10; ++c) std::printf("%.17g%s", r[c], c < 9 ? ", " : "");
+      std::printf("]%s\n", (a == 2 && i == nq - 1) ? "" : ",");
+    }
+  std::printf("],\n");
+  std::printf("\"MaxAirTxHeight\": %.17g, \"MinAirTxHeight\": %.17g,\n", MaxAirTxHeight,
+              MinAirTxHeight);
+  for (int tbl = 0; tbl < 2; ++tbl) {
+    std::printf("\"table%d\": [", tbl);
+    for (int c = 0; c < 11; ++c) {
+      std::printf("[");
+      const std::vector<float>& col = AllTableAllAntData[tbl][c];
+      for (size_t i = 0; i < col.size(); ++i)
+        std::printf("%.9g%s", (double)col[i], i + 1 < col.size() ? ", " : "");
+      std::printf("]%s", c < 10 ? ", " : "");
+    }
+    std::printf("]%s\n", tbl == 0 ? "," : "");
+  }
   std::printf("}\n");
   return 0;
 }

@@ -92,3 +92,31 @@ def cfg5_queries(n: int, seed: int = 777):
     dist = rng.uniform(0.0, 30000.0, n)
     ice = np.full(n, 3000.0)
     return depth, ice, txh, dist
+
+
+def lookup_queries(table: np.ndarray, n: int, seed: int = 4242, max_dist: float = 60000.0):
+    """Table-lookup queries (cm) against one antenna table (11, N) float32: a random body
+    (TxH ~ U(table range), D ~ U(0, max_dist)) plus the edge cases the reference's code paths
+    branch on -- Tx heights exactly on rows (closestvalue == 0 is then decided by the
+    row-index quirk, .cc:1076), distances exactly on THD entries (the closestvalue[1] == 0
+    branch, .cc:1212), the table's max/min heights, heights just outside the range, H <= 0,
+    D = 0, D beyond every THD, and NaN inputs."""
+    rng = np.random.default_rng(seed)
+    hmax, hmin = float(table[0, 0]), float(table[0, -1])
+    thd = table[1].astype(np.float64)
+    h = table[0].astype(np.float64)
+    m = max(n // 8, 1)
+    body_h = rng.uniform(hmin, hmax, n)
+    body_d = rng.uniform(0.0, max_dist, n)
+    valid = np.flatnonzero(np.isfinite(thd) & (thd > 0.01))
+    pick = rng.choice(valid, m) if valid.size else np.zeros(0, dtype=np.int64)
+    on_entry_h, on_entry_d = h[pick], thd[pick]              # both exactly on a table entry
+    on_row_h = h[pick]                                        # row height, random distance
+    on_row_d = rng.uniform(0.0, max_dist, pick.size)
+    edge_h = np.array([hmax, hmin, hmax + 1e-3, hmin - 1e-3, 0.0, -5.0, hmax, hmin, np.nan,
+                       5000.0, 5000.0, 5000.0, hmin + 1e-7, hmax - 1e-7])
+    edge_d = np.array([100.0, 100.0, 100.0, 100.0, 100.0, 100.0, 0.0, 1e7, 100.0,
+                       np.nan, 0.0, 1e9, 50.0, 5000.0])
+    H = np.concatenate([body_h, on_entry_h, on_row_h, edge_h])
+    D = np.concatenate([body_d, on_entry_d, on_row_d, edge_d])
+    return H * 100.0, D * 100.0

@@ -5,6 +5,7 @@ import gzip
 import json
 import math
 import os
+import re
 import subprocess
 
 import numpy as np
@@ -43,7 +44,9 @@ def test_cpp_caller_against_oracle(tmp_path, oracle_medium):
         (tmp_path / "Atmosphere.dat").write_bytes(gzip.decompress(f.read()))
     out = subprocess.run([DRIVER], cwd=tmp_path, capture_output=True, text=True, timeout=120)
     assert out.returncode == 0, out.stderr
-    r = json.loads(out.stdout)
+    txt = re.sub(r"-?\b(nan|inf)\b", lambda mm: {"nan": "NaN", "-nan": "NaN", "inf": "Infinity",
+                                                   "-inf": "-Infinity"}[mm.group(0)], out.stdout)
+    r = json.loads(txt)
     m = oracle_medium
     ok, ref = oracle.hdtip(m, 5000e2, 1000e2, -200e2, 3000e2)
     assert r["hdtip_ok"] == int(ok) == 1
@@ -73,3 +76,25 @@ def test_cpp_caller_against_oracle(tmp_path, oracle_medium):
     ot = oracle.table_rows(m, og, 0, og.height_steps)
     got = np.array(r["table1_row123"], dtype=np.float32)
     assert parity.float_ulp_diff(got, ot[:, 123]) <= 1
+
+    # GetHorizontalDistanceToIntersectionPoint_Table through the reference entry: antenna 1
+    # shares antenna 0's depth -> table 0; antenna 2 -> table 1 (.cc:1348-1352).  The oracle
+    # runs on the very floats the library holds, so non-fallback outputs match bit for bit.
+    tabs = [np.array(r[f"table{i}"], dtype=np.float32) for i in (0, 1)]
+    assert parity.float_ulp_diff(tabs[1], ot) <= 1
+    lts = [oracle.lookup_table(np.ascontiguousarray(t), og) for t in tabs]
+    depths = [-200e2, -200e2, -100e2]
+    table_of = [0, 0, 1]
+    n_ok = 0
+    for row in r["lookup"]:
+        a, src, dist = int(row[0]), row[1], row[2]
+        ok_ref, o_ref, fl = oracle.table_lookup(m, lts[table_of[a]], src, dist, depths[a], 3000e2)
+        assert bool(row[3]) == ok_ref, row
+        if fl & oracle.LOOKUP_FALLBACK:
+            continue
+        got = np.array(row[4:13])
+        assert np.array_equal(got, o_ref, equal_nan=True), (row, o_ref)
+        n_ok += ok_ref
+    assert n_ok >= 6
+    assert r["MaxAirTxHeight"] == float(tabs[1][0, 0])
+    assert r["MinAirTxHeight"] == float(tabs[1][0, -1])

@@ -1,0 +1,105 @@
+"""GPU parity of the batched table lookup (airice_table_lookup_launch; reference
+MultiRayAirIceRefraction.cc:1305-1462) against the oracle restatement on the SAME table.
+
+The table is built on the GPU and copied to the host, so both sides read identical floats.
+The lookup itself is float->double interpolation arithmetic, so non-fallback lanes must be
+bit-identical (NaN positions included); lanes finished by the minimizer fallback
+(.cc:1418-1420) follow the minimizer tolerance (1e-9 relative, parity.HDTIP_FLOORS), with
+rows whose bracket set-up reads uninitialised GSL state masked as in test_gpu_parity.
+"""
+import os
+
+import numpy as np
+import pytest
+
+import oracle
+from tests import parity
+
+pytestmark = pytest.mark.gpu
+
+NTHREADS = min(16, os.cpu_count() or 1)
+ICE_CM = 300000.0
+
+
+@pytest.fixture(scope="module")
+def solver():
+    from airiceraytracing_amd import AirIceSolver
+    return AirIceSolver()
+
+
+def _device_table(solver, depth_cm, hstep, a0, a1, astep):
+    import torch
+    from airiceraytracing_amd import make_grid
+    g = make_grid(depth_cm, ICE_CM, hstep, a0, a1, astep)
+    table = torch.empty((11, g.n_rays), dtype=torch.float32, device="cuda:0")
+    solver.table_device(g, table, stream=torch.cuda.current_stream())
+    torch.cuda.synchronize()
+    return g, table
+
+
+def _run_case(solver, oracle_medium, depth_cm, hstep, a0, a1, astep, nq, seed):
+    import torch
+    g, table = _device_table(solver, depth_cm, hstep, a0, a1, astep)
+    host = table.cpu().numpy()
+    og = oracle.grid_init(depth_cm, ICE_CM, hstep, a0, a1, astep)
+    src, dist = parity.lookup_queries(host, nq, seed=seed)
+    dep = np.full(src.size, depth_cm)
+    n = src.size
+    dev = torch.device("cuda:0")
+    ts, td, tp = (torch.from_numpy(a).to(dev) for a in (src, dist, dep))
+    out = torch.empty((9, n), dtype=torch.float64, device=dev)
+    ok = torch.empty(n, dtype=torch.uint8, device=dev)
+    fl = torch.empty(n, dtype=torch.uint8, device=dev)
+    lt = solver.lookup_table(table, g)
+    solver.table_lookup_device(lt, ts, td, tp, ICE_CM, out, ok, fl,
+                               stream=torch.cuda.current_stream())
+    torch.cuda.synchronize()
+    out, ok, fl = out.cpu().numpy(), ok.cpu().numpy(), fl.cpu().numpy()
+    rout, rok, rfl = oracle.table_lookup_batch(oracle_medium, oracle.lookup_table(host, og),
+                                               src, dist, dep, ICE_CM, nthreads=NTHREADS)
+    assert np.array_equal(fl, rfl), np.flatnonzero(fl != rfl)[:10]
+    fb = (rfl & oracle.LOOKUP_FALLBACK) != 0
+    # non-fallback lanes: bit-identical
+    a, b = out[:, ~fb], rout[:, ~fb]
+    same = (a == b) | (np.isnan(a) & np.isnan(b))
+    assert same.all(), np.argwhere(~same)[:10]
+    assert np.array_equal(ok[~fb], rok[~fb])
+    # fallback lanes: the minimizer with the reference's x100 arguments
+    idx = np.flatnonzero(fb)
+    mask = np.ones(idx.size, dtype=bool)
+    for j, i in enumerate(idx):
+        _, st = oracle.air2ice(oracle_medium, src[i], dist[i], ICE_CM / 100, dep[i])
+        mask[j] = (st & oracle.SOLVE_UNPINNED) == 0
+    if idx.size:
+        assert np.array_equal(ok[idx][mask], rok[idx][mask])
+        rep = parity.compare_columns(out[:, idx], rout[:, idx], parity.HDTIP_FLOORS, mask=mask)
+        assert rep["ok"], rep
+    print(f"[lookup {depth_cm:+.0f}cm {hstep}m/{astep}deg] n={n} ok={int(ok.sum())} "
+          f"fallback={idx.size} (masked {int((~mask).sum())}) "
+          f"unpinned={int(np.count_nonzero(rfl & oracle.LOOKUP_UNPINNED))}")
+    return n
+
+
+def test_lookup_cfg2_table(solver, oracle_medium):
+    """BASELINE cfg2 table (20 m x 0.5 deg, Rx at -200 m)."""
+    _run_case(solver, oracle_medium, -20000.0, 20.0, 92.0, 180.0, 0.5, 100000, 4242)
+
+
+def test_lookup_reference_default_table(solver, oracle_medium):
+    """Reference default grid (10 m x 0.1 deg, 8.7M entries)."""
+    _run_case(solver, oracle_medium, -20000.0, 10.0, 90.1, 180.0, 0.1, 100000, 77)
+
+
+def test_lookup_rx_in_air(solver, oracle_medium):
+    """Antenna above the ice (InIce=false): LoopStopHeight = ice + depth (.cc:2058)."""
+    _run_case(solver, oracle_medium, 5000.0, 100.0, 90.1, 180.0, 0.3, 30000, 5)
+
+
+def test_lookup_empty_batch(solver):
+    import torch
+    g, table = _device_table(solver, -20000.0, 1000.0, 92.0, 180.0, 1.0)
+    e = torch.empty(0, dtype=torch.float64, device="cuda:0")
+    u = torch.empty(0, dtype=torch.uint8, device="cuda:0")
+    solver.table_lookup_device(solver.lookup_table(table, g), e, e, e, ICE_CM,
+                               torch.empty((9, 0), dtype=torch.float64, device="cuda:0"), u, u)
+    torch.cuda.synchronize()
