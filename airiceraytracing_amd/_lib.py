@@ -56,6 +56,7 @@ class Medium(ctypes.Structure):
         ("B_ice", ctypes.c_double),
         ("C_ice", ctypes.c_double),
         ("pi", ctypes.c_double),
+        ("h_top", ctypes.c_double),
     ]
 
 
@@ -96,6 +97,17 @@ class LookupTable(ctypes.Structure):
     ]
 
 
+class SingleRayInfo(ctypes.Structure):
+    """airice_single_ray_info (include/airice.h)."""
+
+    _fields_ = [("skip_above", ctypes.c_int32), ("skip_below", ctypes.c_int32),
+                ("n_layers", ctypes.c_int32), ("pad_", ctypes.c_int32),
+                ("n_air", ctypes.c_int64), ("n_ice", ctypes.c_int64)]
+
+
+SINGLE_RAY_FIELDS = 6  # AIRICE_SINGLE_RAY_FIELDS
+SINGLE_RAY_WORK = 32   # AIRICE_SINGLE_RAY_WORK
+
 LOOKUP_FALLBACK = 1  # AIRICE_LOOKUP_FALLBACK
 LOOKUP_UNPINNED = 2  # AIRICE_LOOKUP_UNPINNED
 
@@ -104,7 +116,8 @@ EXPORTED_SYMBOLS = (
     "airice_last_error", "airice_version", "airice_atmosphere_load", "airice_atmosphere_parse",
     "airice_nz_air", "airice_nz_ice", "airice_grid_init", "airice_table_launch",
     "airice_table_host", "airice_rays_launch", "airice_solve_launch", "airice_solve_host",
-    "airice_hdtip_launch", "airice_table_lookup_launch", "airice_trace_ice_to_air_launch", "airice_trace_ice_to_air_host",
+    "airice_hdtip_launch", "airice_table_lookup_launch", "airice_single_ray_plan",
+    "airice_single_ray_launch", "airice_single_ray_host", "airice_trace_ice_to_air_launch", "airice_trace_ice_to_air_host",
     "Py_TraceIceToAir", "airice_device_count", "airice_set_device", "airice_malloc",
     "airice_free", "airice_memcpy_h2d", "airice_memcpy_d2h", "airice_synchronize",
 )
@@ -160,6 +173,9 @@ def lib() -> ctypes.CDLL:
         "airice_hdtip_launch": ([M, P, P, P, D, S, P, S, P, P], I),
         "airice_table_lookup_launch": ([M, ctypes.POINTER(LookupTable), P, P, P, D, S, P, S, P,
                                         P, P], I),
+        "airice_single_ray_plan": ([M, D, D, D, D, ctypes.POINTER(SingleRayInfo)], I),
+        "airice_single_ray_launch": ([M, D, D, D, D, P, P, P, S, P], I),
+        "airice_single_ray_host": ([M, D, D, D, D, P, P, P, S], I),
         "airice_trace_ice_to_air_launch": ([M, P, P, P, P, S, P, P], I),
         "airice_trace_ice_to_air_host": ([M, P, P, P, P, S, P], I),
         "Py_TraceIceToAir": ([D, D, D, D, ctypes.POINTER(D)], None),

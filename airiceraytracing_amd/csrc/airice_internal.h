@@ -35,6 +35,12 @@ int launch_lookup_fallback(const DevMedium& M, const IceConsts& I, const double*
                            const double* dist, const double* depth, double ice_cm, size_t n,
                            double* out, size_t ld, uint8_t* ok, const uint8_t* flags,
                            hipStream_t st);
+// SingleRayAirIceRefraction (airice_path.hip).  d_work: AIRICE_SINGLE_RAY_WORK doubles.
+int plan_single_ray(const airice_medium* m, double depth, double launch, double txh, double ice,
+                    airice_single_ray_info* info);
+int launch_single_ray(const DevMedium& M, const airice_medium* m, double depth, double launch,
+                      double txh, double ice, double* d_work, double* d_x, double* d_z,
+                      size_t cap, hipStream_t st);
 int launch_trace(const DevMedium& M, const IceConsts& I, const double* depth, const double* ice,
                  const double* txh, const double* dist, size_t n, double* out10, hipStream_t st);
 

@@ -130,6 +130,7 @@ static int parse_gdas(const std::string& text, airice_medium* m) {
   ns.pop_back();
   m->max_layers = groups + 1;
   m->n_points = (int32_t)hs.size();
+  m->h_top = hs.back();
   if (m->max_layers > kMaxLayers) {
     set_error("atmosphere: %d layers exceed the 5 ATMLAY bounds", m->max_layers);
     return AIRICE_EINVAL;
@@ -488,6 +489,63 @@ int airice_table_lookup_launch(const airice_medium* m, const airice_lookup_table
   rc = launch_lookup(M, I, t, d_src_cm, d_dist_cm, d_depth_cm, ice_cm, n, d_out, ld, d_ok,
                      d_flags, (hipStream_t)stream);
   if (rc) set_error("lookup launch failed: %s", hipGetErrorString(hipGetLastError()));
+  return rc;
+}
+
+int airice_single_ray_plan(const airice_medium* m, double antenna_depth_m, double launch_deg,
+                           double txh_m, double ice_m, airice_single_ray_info* info) {
+  if (m == nullptr || info == nullptr) {
+    set_error("null argument");
+    return AIRICE_EINVAL;
+  }
+  return plan_single_ray(m, antenna_depth_m, launch_deg, txh_m, ice_m, info);
+}
+
+int airice_single_ray_launch(const airice_medium* m, double antenna_depth_m, double launch_deg,
+                             double txh_m, double ice_m, double* d_summary, double* d_x,
+                             double* d_z, size_t cap, void* stream) {
+  if (d_summary == nullptr || ((d_x == nullptr) != (d_z == nullptr))) {
+    set_error("single ray: d_summary required, d_x/d_z both or neither");
+    return AIRICE_EINVAL;
+  }
+  DevMedium M;
+  int rc = build_dev_medium(m, AIRICE_VARIANT_MULTIRAY, &M);  // RayTracingFunctions pi (.h:26)
+  if (rc) return rc;
+  rc = launch_single_ray(M, m, antenna_depth_m, launch_deg, txh_m, ice_m, d_summary, d_x, d_z,
+                         cap, (hipStream_t)stream);
+  if (rc == AIRICE_EHIP) set_error("single ray launch failed: %s", hipGetErrorString(hipGetLastError()));
+  return rc;
+}
+
+int airice_single_ray_host(const airice_medium* m, double antenna_depth_m, double launch_deg,
+                           double txh_m, double ice_m, double* summary, double* x, double* z,
+                           size_t cap) {
+  airice_single_ray_info info;
+  int rc = airice_single_ray_plan(m, antenna_depth_m, launch_deg, txh_m, ice_m, &info);
+  if (rc) return rc;
+  const size_t n = (size_t)(info.n_air + info.n_ice);
+  const bool path = x != nullptr && z != nullptr;
+  if (path && n > cap) {
+    set_error("single ray: %zu path samples exceed capacity %zu", n, cap);
+    return AIRICE_EINVAL;
+  }
+  double* d = nullptr;
+  const size_t words = AIRICE_SINGLE_RAY_WORK + (path ? 2 * n : 0);
+  HIP_TRY(hipMalloc(&d, sizeof(double) * words));
+  double* dx = path ? d + AIRICE_SINGLE_RAY_WORK : nullptr;
+  double* dz = path ? dx + n : nullptr;
+  rc = airice_single_ray_launch(m, antenna_depth_m, launch_deg, txh_m, ice_m, d, dx, dz, n, nullptr);
+  if (rc == AIRICE_OK) {
+    hipError_t e = hipMemcpy(summary, d, sizeof(double) * AIRICE_SINGLE_RAY_FIELDS,
+                             hipMemcpyDeviceToHost);
+    if (e == hipSuccess && path && n > 0) e = hipMemcpy(x, dx, sizeof(double) * n, hipMemcpyDeviceToHost);
+    if (e == hipSuccess && path && n > 0) e = hipMemcpy(z, dz, sizeof(double) * n, hipMemcpyDeviceToHost);
+    if (e != hipSuccess) {
+      set_error("single ray copy failed: %s", hipGetErrorString(e));
+      rc = AIRICE_EHIP;
+    }
+  }
+  (void)hipFree(d);
   return rc;
 }
 

@@ -143,6 +143,27 @@ class AirIceSolver:
                                                ptr(flags), _stream_handle(stream)),
               "airice_table_lookup_launch")
 
+    # ------------------------------------------------------------------ single ray (cfg1)
+    def single_ray_host(self, antenna_depth: float, launch_deg: float, txh: float, ice: float,
+                        path: bool = True):
+        """SingleRayAirIceRefraction (BASELINE cfg1) on the GPU: the forward trace of one launch
+        angle and, with ``path``, the RayPathinAirnIce.txt samples.  Inputs after the CLI's
+        clamps; antenna depth positive in ice (SingleRayAirIceRefraction.C:166).  Returns
+        (summary[6], x, z): thd_air, L, incident angle on ice, thd_ice, receive angle in ice,
+        ice propagation time."""
+        info = _lib.SingleRayInfo()
+        check(lib().airice_single_ray_plan(ctypes.byref(self.medium), antenna_depth, launch_deg,
+                                           txh, ice, ctypes.byref(info)), "airice_single_ray_plan")
+        n = int(info.n_air + info.n_ice) if path else 0
+        summary = np.empty(_lib.SINGLE_RAY_FIELDS)
+        x = np.empty(n)
+        z = np.empty(n)
+        check(lib().airice_single_ray_host(ctypes.byref(self.medium), antenna_depth, launch_deg,
+                                           txh, ice, ptr(summary), ptr(x) if path else None,
+                                           ptr(z) if path else None, n),
+              "airice_single_ray_host")
+        return summary, x, z, info
+
     # ------------------------------------------------------------------ pythonwrapper
     def trace_ice_to_air_device(self, depth, ice, txh, dist, out10, stream=None) -> None:
         n = int(depth.numel())

@@ -62,6 +62,8 @@ typedef struct airice_medium {
   double A_air;          /* 1.0 (.h:99) */
   double A_ice, B_ice, C_ice; /* 1.78, -0.43, 0.0132 (.h:64-66) */
   double pi;             /* variant constant */
+  double h_top;          /* h_data.back().back(): last tabulated height, m (the Tx clamp of
+                            SingleRayAirIceRefraction.C:40-45) */
 } airice_medium;
 
 /* MakeRayTracingTable grid (.cc:12-21 globals, .cc:2019-2061 set-up). */
@@ -172,6 +174,32 @@ int airice_table_lookup_launch(const airice_medium *m, const airice_lookup_table
                                const double *d_depth_cm, double ice_cm, size_t n,
                                double *d_out, size_t ld, uint8_t *d_ok, uint8_t *d_flags,
                                void *stream);
+
+/* --- single ray + path sampler (SingleRayAirIceRefraction, BASELINE cfg1) ---------------- */
+/* SingleRayAirIceRefraction.C:33-299 over RayTracingFunctions.cc: inputs are the CLI's values
+ * after its clamps (Tx <= h_top, launch > 90, .C:40-51), metres/degrees, antenna depth
+ * POSITIVE below the ice surface (.C:166).  Path samples are the lines of
+ * RayPathinAirnIce.txt in order: x (m) and height z (m). */
+typedef struct airice_single_ray_info {
+  int32_t skip_above, skip_below; /* SkipLayersAbove / SkipLayersBelow (.C:60-86) */
+  int32_t n_layers;               /* MaxLayers - SkipLayersAbove - SkipLayersBelow (.C:226) */
+  int32_t pad_;
+  int64_t n_air, n_ice;           /* path samples in air (.C:247) and ice (.C:292) */
+} airice_single_ray_info;
+/* summary: total horizontal distance in air (.C:157), L, incident angle on the ice (deg),
+ * horizontal distance / receive angle (deg) / propagation time (s) in ice (.C:167-170) */
+#define AIRICE_SINGLE_RAY_FIELDS 6
+#define AIRICE_SINGLE_RAY_WORK 32 /* doubles of d_summary: the summary, then sampler constants */
+int airice_single_ray_plan(const airice_medium *m, double antenna_depth_m, double launch_deg,
+                           double txh_m, double ice_m, airice_single_ray_info *info);
+/* d_summary: AIRICE_SINGLE_RAY_WORK doubles (summary in the first AIRICE_SINGLE_RAY_FIELDS);
+ * d_x/d_z (nullable together): cap >= n_air + n_ice */
+int airice_single_ray_launch(const airice_medium *m, double antenna_depth_m, double launch_deg,
+                             double txh_m, double ice_m, double *d_summary, double *d_x,
+                             double *d_z, size_t cap, void *stream);
+int airice_single_ray_host(const airice_medium *m, double antenna_depth_m, double launch_deg,
+                           double txh_m, double ice_m, double *summary, double *x, double *z,
+                           size_t cap);
 
 /* pythonwrapper TraceIceToAir, batched: per-query (depth, ice, txh, dist) metres ->
  * ArrayParameters[10] rows (TraceIceToAir.C:46-68), row-major n x 10. */

@@ -50,6 +50,7 @@ class Medium(ctypes.Structure):
         ("B_ice", ctypes.c_double),
         ("C_ice", ctypes.c_double),
         ("pi", ctypes.c_double),
+        ("h_top", ctypes.c_double),
     ]
 
 
@@ -283,3 +284,33 @@ def table_lookup_batch(m: Medium, t: LookupTable, src_cm, dist_cm, depth_cm, ice
     lib().or_table_lookup_batch(ctypes.byref(m), ctypes.byref(t), *[_ptr(a) for a in arrs],
                                 ice_cm, n, _ptr(out), n, _ptr(ok), _ptr(fl), nthreads)
     return out, ok, fl
+
+
+class SingleRay(ctypes.Structure):
+    """or_single_ray (SingleRayAirIceRefraction.C:33-299)."""
+    _fields_ = [("skip_above", ctypes.c_int), ("skip_below", ctypes.c_int),
+                ("n_layers", ctypes.c_int), ("thd_air", ctypes.c_double), ("L", ctypes.c_double),
+                ("inc_ice", ctypes.c_double), ("thd_ice", ctypes.c_double),
+                ("recv_ice", ctypes.c_double), ("t_ice", ctypes.c_double),
+                ("n_air", ctypes.c_long), ("n_ice", ctypes.c_long)]
+
+
+def single_ray(m: Medium, depth, launch_deg, txh, ice):
+    """cfg1 forward trace + RayPathinAirnIce.txt samples (after the CLI's clamps; depth > 0
+    in ice).  Returns (SingleRay, x, z)."""
+    L = lib()
+    if not getattr(L, "_single_ray_sig", False):
+        L.or_single_ray_trace.argtypes = [ctypes.POINTER(Medium), ctypes.c_double, ctypes.c_double,
+                                          ctypes.c_double, ctypes.c_double,
+                                          ctypes.POINTER(SingleRay), ctypes.c_void_p,
+                                          ctypes.c_void_p, ctypes.c_long]
+        L._single_ray_sig = True
+    r = SingleRay()
+    L.or_single_ray_trace(ctypes.byref(m), depth, launch_deg, txh, ice, ctypes.byref(r), None,
+                          None, 0)
+    n = r.n_air + r.n_ice
+    x = np.zeros(n)
+    z = np.zeros(n)
+    L.or_single_ray_trace(ctypes.byref(m), depth, launch_deg, txh, ice, ctypes.byref(r), _ptr(x),
+                          _ptr(z), n)
+    return r, x, z

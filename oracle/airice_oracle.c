@@ -203,6 +203,7 @@ int or_parse_atmosphere(const char *text, size_t len, double pi, or_medium *m) {
   group_end[ngroups - 1] -= 1;
   m->max_layers = ngroups + 1;
   m->n_points = (int)npts;
+  m->h_top = h[npts - 1];
   for (int i = 0; i < ngroups && i < 8; i++)
     m->layer_sizes[i] = group_end[i] - (i ? group_end[i - 1] : 0);
 
@@ -1044,4 +1045,83 @@ void or_table_lookup_batch(const or_medium *m, const or_lookup_table *t, const d
     flags[i] = (unsigned char)fl;
     for (int c = 0; c < 9; ++c) out[(size_t)c * ld + (size_t)i] = o[c];
   }
+}
+
+/* ------------------------------------------------------------------------- */
+/* SingleRayAirIceRefraction.C:33-299 (RayTracingFunctions.cc numerics)       */
+/* ------------------------------------------------------------------------- */
+int or_single_ray_trace(const or_medium *m, double AntennaDepth, double RayLaunchAngle,
+                        double AirTxHeight, double IceLayerHeight, or_single_ray *out, double *xs,
+                        double *zs, long cap) {
+  const double pi = m->pi;
+  memset(out, 0, sizeof(*out));
+  const int ML = m->max_layers;
+  const int SkipLayersAbove = skip_above(m, AirTxHeight);   /* :60-71 */
+  const int SkipLayersBelow = skip_below(m, IceLayerHeight); /* :75-86 */
+  out->skip_above = SkipLayersAbove;
+  out->skip_below = SkipLayersBelow;
+  /* air layer loop (:100-154) */
+  double StartHeight = 0, StopHeight = 0, StartAngle = 0, TotalHorizontalDistance = 0, Lvalue = 0;
+  for (int ilayer = ML - SkipLayersAbove - 1; ilayer > SkipLayersBelow - 1; ilayer--) {
+    if (ilayer == ML - SkipLayersAbove - 1) StartHeight = AirTxHeight;
+    else StartHeight = m->atmlay[ilayer + 1] / 100 - 0.00001;
+    double Start_nh = or_getnz_air(m, StartHeight);
+    if (ilayer == (SkipLayersBelow - 1) + 1) StopHeight = IceLayerHeight;
+    else StopHeight = m->atmlay[ilayer] / 100;
+    if (ilayer == ML - SkipLayersAbove - 1) {
+      StartAngle = 180 - RayLaunchAngle;
+      double hp[5];
+      or_layer_hit_point_par(m, Start_nh, StopHeight, StartHeight, StartAngle, 1, hp);
+      TotalHorizontalDistance += hp[0];
+      StartAngle = hp[1];
+      Lvalue = hp[2];
+    } else {
+      double nzStopHeight = or_getnz_air(m, StopHeight);
+      double RecAng = asin(Lvalue / nzStopHeight);
+      RecAng = RecAng * (180 / pi);
+      double THD = GetRayHorizontalPath(m, m->A_air, StopHeight, StartHeight, Lvalue, 1);
+      TotalHorizontalDistance += THD;
+      StartAngle = RecAng;
+    }
+  }
+  out->thd_air = TotalHorizontalDistance;
+  out->inc_ice = StartAngle;
+  out->L = Lvalue;
+  /* GetIcePropagationPar (RayTracingFunctions.cc:661-679) with positive depth */
+  {
+    double nzStopDepth = or_getnz_ice(m, AntennaDepth);
+    out->thd_ice = GetRayHorizontalPath(m, m->A_ice, AntennaDepth, 0.0, Lvalue, 0);
+    out->recv_ice = asin(Lvalue / nzStopDepth) * (180 / pi);
+    out->t_ice = GetRayPropagationTime(m, m->A_ice, AntennaDepth, 0.0, Lvalue, 0);
+  }
+  /* path sampler (:226-299) */
+  const int nl = ML - SkipLayersAbove - SkipLayersBelow;
+  out->n_layers = nl;
+  long ip = 0;
+  double LastRefracted_x = 0, LastHeight = 0, Refracted_x = 0;
+  for (int il = 0; il < nl; il++) {
+    double LayerStartHeight = (il == 0) ? AirTxHeight : LastHeight - 0.00001;
+    double LayerStopHeight = (il == nl - 1) ? IceLayerHeight : (m->atmlay[nl - il - 1] / 100);
+    for (double i = LayerStartHeight; i > LayerStopHeight - 1; i = i - 1) {
+      if (i < LayerStopHeight) i = LayerStopHeight;
+      double fa = fDnfR(-i, m->A_air, GetB_air(m, -i), GetC_air(m, -i), Lvalue);
+      double fb = fDnfR(-(LayerStartHeight), m->A_air, GetB_air(m, -(LayerStartHeight)),
+                        GetC_air(m, -(LayerStartHeight)), Lvalue);
+      Refracted_x = fa - fb + LastRefracted_x;
+      if (xs && ip < cap) { xs[ip] = Refracted_x; zs[ip] = i; }
+      ip++;
+      LastHeight = i;
+    }
+    LastRefracted_x = Refracted_x;
+  }
+  out->n_air = ip;
+  for (int i = 0; i > -(AntennaDepth + 1); i--) {
+    double fa = fDnfR((double)i, m->A_ice, GetB_ice(m, i), GetC_ice(m, i), Lvalue);
+    double fb = fDnfR(0, m->A_ice, GetB_ice(m, 0), GetC_ice(m, 0), Lvalue);
+    double refractedpath = LastRefracted_x - fa + fb;
+    if (xs && ip < cap) { xs[ip] = refractedpath; zs[ip] = (double)i + IceLayerHeight; }
+    ip++;
+  }
+  out->n_ice = ip - out->n_air;
+  return 0;
 }

@@ -39,6 +39,8 @@ typedef struct or_medium {
   double A_air;        /* .h:99 */
   double A_ice, B_ice, C_ice;  /* .h:64-66 */
   double pi;           /* 3.1415927 (MultiRay/RTF) or 4*atan(1) (pythonwrapper) */
+  double h_top;        /* h_data.back().back(): last tabulated height, m
+                          (SingleRayAirIceRefraction.C:40-45 clamps the Tx to it) */
 } or_medium;
 
 /* Status codes of one bisection solve (GSL 2.x bisection semantics). */
@@ -145,3 +147,20 @@ void or_table_lookup_batch(const or_medium *m, const or_lookup_table *t, const d
                            const double *dist_cm, const double *depth_cm, double ice_cm, size_t n,
                            double *out, size_t ld, unsigned char *ok, unsigned char *flags,
                            int nthreads);
+
+/* ---- SingleRayAirIceRefraction CLI (cfg1; SURVEY §8 a19 + the f4 path sampler) ----------
+ * SingleRayAirIceRefraction.C:33-299 over RayTracingFunctions.cc (same medium, pi 3.1415927):
+ * forward trace of one launch angle (the layer loop :100-154, GetIcePropagationPar :166) and
+ * the x(z) path at 1 m steps written to RayPathinAirnIce.txt (:226-299).  Inputs are the
+ * values after the CLI's clamps (:40-51); antenna depth is POSITIVE in ice (:166). */
+typedef struct or_single_ray {
+  int skip_above, skip_below, n_layers; /* n_layers = MaxLayers - SkipAbove - SkipBelow */
+  double thd_air;                       /* "Total horizontal distance ..." (:157) */
+  double L;                             /* Lvalue = layerLs[*] = LvalueIce */
+  double inc_ice;                       /* IncidentAngleonIce, deg (:156) */
+  double thd_ice, recv_ice, t_ice;      /* GetIcePropagationPar outputs (:166-170) */
+  long n_air, n_ice;                    /* path samples in air / ice */
+} or_single_ray;
+/* x/z (nullable): capacity cap >= n_air + n_ice samples, in file order (ipoints). */
+int or_single_ray_trace(const or_medium *m, double depth, double launch_deg, double txh,
+                        double ice, or_single_ray *out, double *x, double *z, long cap);
