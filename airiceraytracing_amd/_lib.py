@@ -57,6 +57,9 @@ class Medium(ctypes.Structure):
         ("C_ice", ctypes.c_double),
         ("pi", ctypes.c_double),
         ("h_top", ctypes.c_double),
+        ("constant_air_index", ctypes.c_int32),
+        ("reserved_", ctypes.c_int32),
+        ("A_const", ctypes.c_double),
     ]
 
 

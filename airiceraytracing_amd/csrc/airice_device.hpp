@@ -65,7 +65,7 @@ struct DevMedium {
   double d2r;       // pi/180.0   (.cc:537)
   double r2d;       // 180/pi     (.cc:640)
   int ml;           // MaxLayers
-  int pad_;
+  int const_air;   // pythonwrapper UseConstantRefractiveIndex: bracket [90, thR], no probe
   Endpoint start[kMaxLayers];  // layer l start: x = ATMLAY[l+1]/100 - 1e-5 (.cc:1846)
   Endpoint stop[kMaxLayers];   // layer l stop:  x = ATMLAY[l]/100          (.cc:1858)
 };

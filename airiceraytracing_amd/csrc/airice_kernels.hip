@@ -395,7 +395,8 @@ __device__ __forceinline__ SolveResult solve_root(const DevMedium& M, const IceC
   double lo = thR - 16;
   double hi = thR;
   int phase = PH_FLO;
-  if (lo < 90.001) {
+  if (M.const_air) lo = 90;  // pythonwrapper constant air index: [90, thR], no probe (.cc:978-980)
+  if (!M.const_air && lo < 90.001) {
     lo = 90.001;
     phase = PH_PROBE;
     // While n(Tx) sin(180-lo) exceeds 1 by a margin (1e-6) the ray parameter L > A_air = 1,

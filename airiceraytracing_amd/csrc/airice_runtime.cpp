@@ -87,6 +87,7 @@ static int parse_gdas(const std::string& text, airice_medium* m) {
   m->A_ice = 1.78;
   m->B_ice = -0.43;
   m->C_ice = 0.0132;
+  m->A_const = 1.00;
   {
     std::istringstream in(text);
     std::string line;
@@ -199,6 +200,21 @@ int build_dev_medium(const airice_medium* m, int variant, DevMedium* out) {
   M.d2r = pi / 180.0;
   M.r2d = 180 / pi;
   M.ml = m->max_layers;
+  if (variant == AIRICE_VARIANT_PYWRAPPER && m->constant_air_index) {
+    // UseConstantRefractiveIndex (pythonwrapper AirIceRayTracing.cc:173-238): GetB_air = 0,
+    // GetC_air = 1e-9 in every layer; Getnz_air = A_const, which A_air + 0*exp() reproduces
+    // exactly while A_const == A_air (both 1.00, .h:69-72)
+    if (m->A_const != m->A_air) {
+      set_error("constant air index: A_const (%g) != A_air (%g) is not supported", m->A_const,
+                m->A_air);
+      return AIRICE_EINVAL;
+    }
+    for (int i = 0; i < 5; ++i) {
+      M.B[i] = 0;
+      M.negC[i] = -1e-9;
+    }
+    M.const_air = 1;
+  }
   for (int l = 0; l < kMaxLayers; ++l) {
     M.start[l] = host_air_endpoint(M, M.atm[l + 1] - 0.00001);
     M.stop[l] = host_air_endpoint(M, M.atm[l]);

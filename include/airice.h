@@ -64,6 +64,12 @@ typedef struct airice_medium {
   double pi;             /* variant constant */
   double h_top;          /* h_data.back().back(): last tabulated height, m (the Tx clamp of
                             SingleRayAirIceRefraction.C:40-45) */
+  int32_t constant_air_index; /* pythonwrapper AirIceRayTracing::UseConstantRefractiveIndex
+                                 (.h:54, default 0): honoured by AIRICE_VARIANT_PYWRAPPER only --
+                                 GetB_air = 0, GetC_air = 1e-9, Getnz_air = A_const (.cc:173-238)
+                                 and the launch bracket [90, thR] without the probe (.cc:955-982) */
+  int32_t reserved_;
+  double A_const;        /* pythonwrapper .h:72 (1.00) */
 } airice_medium;
 
 /* MakeRayTracingTable grid (.cc:12-21 globals, .cc:2019-2061 set-up). */

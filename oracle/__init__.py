@@ -51,6 +51,8 @@ class Medium(ctypes.Structure):
         ("C_ice", ctypes.c_double),
         ("pi", ctypes.c_double),
         ("h_top", ctypes.c_double),
+        ("constant_air_index", ctypes.c_int),
+        ("A_const", ctypes.c_double),
     ]
 
 

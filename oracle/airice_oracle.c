@@ -151,6 +151,7 @@ int or_parse_atmosphere(const char *text, size_t len, double pi, or_medium *m) {
   m->pi = pi;
   m->A_air = 1.00;
   m->A_ice = 1.78; m->B_ice = -0.43; m->C_ice = 0.0132;
+  m->A_const = 1.00;
 
   /* readATMpar */
   {
@@ -256,10 +257,16 @@ static int air_layer(const or_medium *m, double z) {
   if (zabs >= m->atmlay[m->max_layers - 1] / 100) which = m->max_layers - 1;
   return which;
 }
-static double GetB_air(const or_medium *m, double z) { return m->B_air[air_layer(m, z)]; }
-static double GetC_air(const or_medium *m, double z) { return m->C_air[air_layer(m, z)]; }
+/* pythonwrapper AirIceRayTracing.cc:173-238 (UseConstantRefractiveIndex branches) */
+static double GetB_air(const or_medium *m, double z) {
+  return m->constant_air_index ? 0 : m->B_air[air_layer(m, z)];
+}
+static double GetC_air(const or_medium *m, double z) {
+  return m->constant_air_index ? 1e-9 : m->C_air[air_layer(m, z)];
+}
 double or_getnz_air(const or_medium *m, double z) {
   double zabs = fabs(z);
+  if (m->constant_air_index) return m->A_const;
   return m->A_air + GetB_air(m, zabs) * exp(-GetC_air(m, zabs) * zabs);
 }
 
@@ -652,7 +659,9 @@ static double bracket_and_solve(const or_medium *m, double AirTxHeight, double H
   }
   double lo = StraightAngle - 16;
   double hi = StraightAngle;
-  if (lo < 90.001) {
+  if (m->constant_air_index) {
+    lo = 90; /* pythonwrapper AirIceRayTracing.cc:978-980 */
+  } else if (lo < 90.001) {
     lo = 90.001;
     int checknan = 0;
     double out[5 * 8 + 2];

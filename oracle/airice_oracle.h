@@ -41,6 +41,10 @@ typedef struct or_medium {
   double pi;           /* 3.1415927 (MultiRay/RTF) or 4*atan(1) (pythonwrapper) */
   double h_top;        /* h_data.back().back(): last tabulated height, m
                           (SingleRayAirIceRefraction.C:40-45 clamps the Tx to it) */
+  int    constant_air_index; /* pythonwrapper AirIceRayTracing::UseConstantRefractiveIndex
+                                (.h:54): GetB_air = 0, GetC_air = 1e-9, Getnz_air = A_const,
+                                bracket [90, thR] without the probe loop (.cc:178-239, 955-982) */
+  double A_const;      /* pythonwrapper .h:72 */
 } or_medium;
 
 /* Status codes of one bisection solve (GSL 2.x bisection semantics). */

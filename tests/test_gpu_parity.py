@@ -184,3 +184,28 @@ def test_single_ray_kat_device(solver):
            14: 0.847773642727253, 15: 0.848652266629523}
     for k, v in kat.items():
         assert abs(d[k] - v) <= 1e-9 * abs(v), (k, d[k], v)
+
+
+def test_pywrapper_constant_air_index(oracle_medium_py):
+    """UseConstantRefractiveIndex (pythonwrapper AirIceRayTracing.h:54, .cc:173-238, 955-982).
+    The bracket then starts at exactly 90 deg, where L = A_air and f is non-finite, so the
+    reference's GSL set-up fails on every query and reads uninitialised state: every row is
+    unpinned (status NONFINITE_END) and is compared under the oracle's zeroed-state model."""
+    import copy
+    from airiceraytracing_amd import AirIceSolver, VARIANT_PYWRAPPER
+    s = AirIceSolver(variant=VARIANT_PYWRAPPER)
+    s.medium.constant_air_index = 1
+    m = copy.copy(oracle_medium_py)
+    m.constant_air_index = 1
+    txh, dist, depth = parity.cfg3_queries(500, seed=31)
+    out, st = s.solve_host(txh, dist, depth, 3000.0)
+    ref = np.empty_like(out)
+    rst = np.empty(out.shape[1], dtype=np.int64)
+    for i in range(out.shape[1]):
+        thr = oracle.straight_angle_of(m, txh[i], dist[i], 3000.0, depth[i])
+        ref[:, i], rst[i] = oracle.py_air2ice(m, txh[i], dist[i], 3000.0, depth[i], thr)
+    assert np.all(rst & oracle.SOLVE_NONFINITE_END)
+    assert np.array_equal(st.astype(np.int64), rst)
+    rep = parity.compare_columns(out, ref, parity.PYSOLVE_FLOORS)
+    _report("py-const-index", rep)
+    assert rep["ok"], rep
