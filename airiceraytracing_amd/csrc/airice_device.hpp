@@ -187,12 +187,45 @@ struct RayL {
   double L, LL, sAL, rsAL;  // L, L^2, sqrt(A^2-L^2), 1/sqrt(A^2-L^2)
 };
 
+// sqrt(q) and 1/sqrt(q) together from one v_rsq_f64 and Goldschmidt/Newton refinement (the
+// iteration ocml's sqrt uses, without its denormal rescaling: q here is a difference of squares of
+// O(1) refractive indices); both within ~1 ulp.  q = 0 gives (0, +inf) and q < 0 / NaN gives NaNs,
+// as sqrt() and 1/sqrt() do.
+__device__ __forceinline__ void sqrt_rsqrt(double q, double& s, double& rs) {
+  const double y = __builtin_amdgcn_rsq(q);
+  double g = q * y, h = 0.5 * y;
+  double e = __builtin_fma(-h, g, 0.5);
+  g = __builtin_fma(g, e, g);
+  h = __builtin_fma(h, e, h);
+  double d = __builtin_fma(-g, g, q);
+  g = __builtin_fma(d, h, g);
+  e = __builtin_fma(-h, g, 0.5);
+  h = __builtin_fma(h, e, h);
+  d = __builtin_fma(-g, g, q);
+  g = __builtin_fma(d, h, g);
+  s = (q == 0.0) ? q : g;
+  rs = (q == 0.0) ? __builtin_inf() : 2.0 * h;
+}
+
+// sqrt(q) (same iteration, no reciprocal): within ~1 ulp; q = 0 -> 0, q < 0 / NaN -> NaN.
+__device__ __forceinline__ double fast_sqrt(double q) {
+  const double y = __builtin_amdgcn_rsq(q);
+  double g = q * y, h = 0.5 * y;
+  const double e = __builtin_fma(-h, g, 0.5);
+  g = __builtin_fma(g, e, g);
+  h = __builtin_fma(h, e, h);
+  double d = __builtin_fma(-g, g, q);
+  g = __builtin_fma(d, h, g);
+  d = __builtin_fma(-g, g, q);
+  g = __builtin_fma(d, h, g);
+  return (q == 0.0) ? q : g;
+}
+
 __device__ __forceinline__ RayL ray_L(double A2, double L) {
   RayL r;
   r.L = L;
   r.LL = L * L;
-  r.sAL = sqrt(A2 - r.LL);
-  r.rsAL = 1.0 / r.sAL;
+  sqrt_rsqrt(A2 - r.LL, r.sAL, r.rsAL);
   return r;
 }
 
@@ -209,15 +242,18 @@ struct Segment {
 // ~45 VALU instead of ocml's ~85 (which also covers denormals and special values).
 // Any other x goes to ocml's log, so NaN / inf / 0 / negative behave exactly as log().
 // Checked against long double on 6e7 arguments: max error 0.84 ulp (tests/test_fastlog.py).
-__device__ __forceinline__ double fast_log(double x) {
-  if (!(x >= 2.2250738585072014e-308 && x <= 1.7976931348623157e308)) return log(x);
+__device__ __forceinline__ double fast_log(double x_in) {
+  // branch-free: denormals are scaled by 2^54 (k corrected below); 0, negative, NaN and inf
+  // take log()'s IEEE results by select at the end
+  const bool tiny = x_in < 2.2250738585072014e-308;
+  const double x = tiny ? x_in * 18014398509481984.0 : x_in;
   const double Lg1 = 6.666666666666735130e-01, Lg2 = 3.999999999940941908e-01,
                Lg3 = 2.857142874366239149e-01, Lg4 = 2.222219843214978396e-01,
                Lg5 = 1.818357216161805012e-01, Lg6 = 1.531383769920937332e-01,
                Lg7 = 1.479819860511658591e-01;
   const double ln2_hi = 6.93147180369123816490e-01, ln2_lo = 1.90821492927058770002e-10;
   const unsigned long long b = (unsigned long long)__double_as_longlong(x);
-  int k = (int)(b >> 52) - 1023;
+  int k = (int)(b >> 52) - (tiny ? 1023 + 54 : 1023);
   double m = __longlong_as_double((long long)((b & 0x000fffffffffffffULL) | 0x3ff0000000000000ULL));
   if (m > 1.4142135623730951) {
     m *= 0.5;
@@ -231,12 +267,19 @@ __device__ __forceinline__ double fast_log(double x) {
   const double R = t2 + t1;
   const double hfsq = 0.5 * f * f;
   const double dk = (double)k;
-  return dk * ln2_hi - ((hfsq - (s * (hfsq + R) + dk * ln2_lo)) - f);
+  const double r = dk * ln2_hi - ((hfsq - (s * (hfsq + R) + dk * ln2_lo)) - f);
+  // log(+-0) = -inf, log(+inf) = +inf, log(<0) = log(NaN) = NaN
+  const double special = (x_in == 0.0) ? -__builtin_inf() : (x_in > 0.0 ? x_in : __builtin_nan(""));
+  return (x_in > 0.0 && x_in < __builtin_inf()) ? r : special;
 }
 
 __device__ __forceinline__ double log_ratio(double a, double b) {
-  // log(a) - log(b) as one logarithm when both are in log's domain (identity (5))
-  return (a > 0.0 && b > 0.0) ? fast_log(a / b) : log(a) - log(b);
+  // log(a) - log(b) as one logarithm when both are in log's domain (identity (5)); outside it,
+  // the IEEE value of log(a) - log(b): -inf - finite, finite - (-inf), NaN otherwise
+  const double special = (a == 0.0 && b > 0.0)   ? -__builtin_inf()
+                         : (b == 0.0 && a > 0.0) ? __builtin_inf()
+                                                 : __builtin_nan("");
+  return (a > 0.0 && b > 0.0) ? fast_log(a / b) : special;
 }
 
 __device__ __forceinline__ Segment segment(const Endpoint& T, const Endpoint& R_, double A,
@@ -249,7 +292,7 @@ __device__ __forceinline__ Segment segment(const Endpoint& T, const Endpoint& R_
   // log(a_R/a_T) instead of two logarithms, and
   // ftimeD = (s + A^2 (Cx - lg1)/sqrt(A^2-L^2) + A lg2) / (c C) since (n^2-L^2)/s = s.
   Segment s;
-  const double syR = sqrt(R.y2 - RL.LL), syT = sqrt(T.y2 - RL.LL);
+  const double syR = fast_sqrt(R.y2 - RL.LL), syT = fast_sqrt(T.y2 - RL.LL);
   const double d1 = log_ratio(R.Ay - RL.LL + RL.sAL * syR, T.Ay - RL.LL + RL.sAL * syT);
   const double d2 = log_ratio(R.n + syR, T.n + syT);
   const double dCx = R.Cx - T.Cx;
@@ -270,7 +313,7 @@ __device__ __forceinline__ Segment segment_const(const SegConst& S, double A, do
                                                  bool air, double& v_out) {
   const double v2 = sin_asin(S.ratio * sin_in);
   const RayL RL = ray_L(A2, S.Rn * v2);
-  const double syR = sqrt(S.Ry2 - RL.LL), syT = sqrt(S.Ty2 - RL.LL);
+  const double syR = fast_sqrt(S.Ry2 - RL.LL), syT = fast_sqrt(S.Ty2 - RL.LL);
   const double d1 = log_ratio(S.RAy - RL.LL + RL.sAL * syR, S.TAy - RL.LL + RL.sAL * syT);
   const double d2 = log_ratio(S.Rn + syR, S.Tn + syT);
   Segment s;

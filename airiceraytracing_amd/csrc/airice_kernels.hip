@@ -18,6 +18,9 @@
 
 #include <cmath>
 #include <cstdint>
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
 
 #include "airice.h"
 #include "airice_device.hpp"
@@ -85,7 +88,7 @@ __device__ __forceinline__ Segment segment_top(const Endpoint& T, const TopEnd& 
                       : R_;
   const double v2 = sin_asin((T.n * sin_in) / R.n);
   const RayL RL = ray_L(A2, R.n * v2);
-  const double syR = sqrt(R.y2 - RL.LL), syT = sqrt(T.y2 - RL.LL);
+  const double syR = fast_sqrt(R.y2 - RL.LL), syT = fast_sqrt(T.y2 - RL.LL);
   const double d1 = log_ratio(R.Ay - RL.LL + RL.sAL * syR, T.Ay - RL.LL + RL.sAL * syT);
   const double d2 = log_ratio(R.n + syR, T.n + syT);
   const double dCx = R.Cx - T.Cx;
@@ -97,8 +100,11 @@ __device__ __forceinline__ Segment segment_top(const Endpoint& T, const TopEnd& 
   return s;
 }
 
+// want_inc: dummy[12] (the incidence angle on the ice, one asin) is not a table column
+// (.cc:2101-2111), so table launches without the double output skip it.
 __device__ __forceinline__ void ray_solution(const DevMedium& M, const IceConsts& I, double theta,
-                                             double H, bool in_ice, double* d) {
+                                             double H, bool in_ice, double* d,
+                                             bool want_inc = true) {
   const int top = top_layer(M, H);
   const int bot = I.bot;
   const double A2 = M.A_air * M.A_air;
@@ -123,7 +129,8 @@ __device__ __forceinline__ void ray_solution(const DevMedium& M, const IceConsts
     geo_air += s.geo;
   }
   // IncidentAngleonIce = last layer's receive angle; 0 when no air layer (.cc:1832, 1881)
-  const double inc = any ? asin(v) * M.r2d : 0.0;
+  double inc = 0.0;
+  if (want_inc) inc = any ? asin(v) * M.r2d : 0.0;
   const double vinc = any ? v : 0.0;
   double thd_ice = 0.0, t_ice = 0.0, geo_ice = 0.0, recv_ice = 0.0;
   if (in_ice) {
@@ -162,27 +169,37 @@ __device__ __forceinline__ void ray_solution(const DevMedium& M, const IceConsts
 struct TableArgs {
   double start_h, stop_h, step_h;
   double start_a, stop_a, step_a;
+  double inv_asteps;  // 1.0 / asteps (row of ray k without a 64-bit division)
   int hsteps, asteps;
   int row0, in_ice;
   long long n;
   size_t ld;
 };
 
-__global__ __launch_bounds__(kBlock) void table_kernel(DevMedium M, IceConsts I, TableArgs G,
-                                                       float* __restrict__ table,
-                                                       double* __restrict__ full) {
-  const long long k = (long long)blockIdx.x * kBlock + threadIdx.x;
-  if (k >= G.n) return;
-  const int r = (int)(k / G.asteps);
-  const int iang = (int)(k - (long long)r * G.asteps);
-  const int ihei = G.row0 + r;
+// Debug timeline (AIRICE_TABLE_TRACE=<file>, tools/wave_timeline.py): per wave, the 100 MHz
+// s_memrealtime at entry and exit plus HW_ID / XCC_ID.  Not part of the API.
+struct WaveTrace {
+  unsigned long long t0, t1;
+  unsigned hw_id, xcc_id;
+};
+
+// One table entry: ray k of the launch (row-major over TxH rows x launch angles).
+__device__ __forceinline__ void table_ray(const DevMedium& M, const IceConsts& I,
+                                          const TableArgs& G, long long k,
+                                          float* __restrict__ table, double* __restrict__ full) {
+  // r = k / asteps: the double quotient is within 1 of the true one (k < 2^52), then fixed up
+  long long r = (long long)((double)k * G.inv_asteps);
+  if (r * G.asteps > k) --r;
+  if ((r + 1) * G.asteps <= k) ++r;
+  const int iang = (int)(k - r * G.asteps);
+  const int ihei = G.row0 + (int)r;
   // .cc:2080, 2085, 2089-2094 (separate mul and add: no contraction)
   double H = G.start_h - G.step_h * ihei;
   double th = G.start_a + G.step_a * iang;
   if (H != G.stop_h && ihei == G.hsteps - 1) H = G.stop_h;
   if (iang == G.asteps - 1) th = G.stop_a;
   double d[18];
-  ray_solution(M, I, th, H, G.in_ice != 0, d);
+  ray_solution(M, I, th, H, G.in_ice != 0, d, full != nullptr);
   const size_t ld = G.ld;
   // AllTableAllAntData columns (.cc:2101-2111)
   table[0 * ld + k] = (float)d[1];
@@ -199,6 +216,26 @@ __global__ __launch_bounds__(kBlock) void table_kernel(DevMedium M, IceConsts I,
   if (full != nullptr) {
 #pragma unroll
     for (int c = 0; c < 18; ++c) full[c * ld + k] = d[c];
+  }
+}
+
+// Table launch: one ray per lane.  (Persistent grid-stride and atomic-chunk schedules were
+// measured and rejected: the loop around the inlined ray body raises register pressure to
+// 160 VGPRs, or 330 B/lane of scratch when capped at 64, and run 2.7x / 7x slower.)
+template <int BS, bool TRACE = false>
+__global__ __launch_bounds__(BS) void table_kernel(DevMedium M, IceConsts I, TableArgs G,
+                                                   float* __restrict__ table,
+                                                   double* __restrict__ full,
+                                                   WaveTrace* __restrict__ trace) {
+  const unsigned wave = blockIdx.x * (BS / 64) + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (TRACE && lane == 0) trace[wave].t0 = __builtin_amdgcn_s_memrealtime();
+  const long long k = (long long)blockIdx.x * BS + threadIdx.x;
+  if (k < G.n) table_ray(M, I, G, k, table, full);
+  if (TRACE && lane == 0) {
+    trace[wave].t1 = __builtin_amdgcn_s_memrealtime();
+    trace[wave].hw_id = __builtin_amdgcn_s_getreg((4 << 0) | (0 << 6) | (31 << 11));  // HW_ID
+    trace[wave].xcc_id = __builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (31 << 11));
   }
 }
 
@@ -287,7 +324,7 @@ __device__ __forceinline__ double stop_n(const DevMedium& M, int l) {
 
 // fDnfR(R) - fDnfR(T) with one logarithm when both ends share C (identity (5)).
 __device__ __forceinline__ double delta_D(const Slim& T, const Slim& R, const RayL& RL) {
-  const double syR = sqrt(R.y2 - RL.LL), syT = sqrt(T.y2 - RL.LL);
+  const double syR = fast_sqrt(R.y2 - RL.LL), syT = fast_sqrt(T.y2 - RL.LL);
   const double d1 = log_ratio(R.Ay - RL.LL + RL.sAL * syR, T.Ay - RL.LL + RL.sAL * syT);
   return (RL.L * R.invC) * RL.rsAL * ((R.Cx - T.Cx) - d1);
 }
@@ -803,9 +840,30 @@ int launch_table(const DevMedium& M, const IceConsts& I, const airice_grid* g, i
   A.in_ice = g->in_ice;
   A.n = (long long)row_count * g->angle_steps;
   A.ld = ld;
+  A.inv_asteps = 1.0 / (double)g->angle_steps;
   if (A.n == 0) return AIRICE_OK;
-  hipLaunchKernelGGL(table_kernel, dim3(grid_for(A.n)), dim3(kBlock), 0, st, M, I, A, d_table,
-                     d_full);
+  static const char* trace_path = getenv("AIRICE_TABLE_TRACE");
+  const unsigned blocks = grid_for(A.n);
+  if (trace_path == nullptr) {
+    hipLaunchKernelGGL((table_kernel<kBlock, false>), dim3(blocks), dim3(kBlock), 0, st, M, I, A,
+                       d_table, d_full, nullptr);
+    return launch_ok();
+  }
+  // debug timeline (tools/wave_timeline.py): synchronous, one record per wave appended to the file
+  const long long nw = (long long)blocks * (kBlock / 64);
+  WaveTrace* dtr = nullptr;
+  if (hipMalloc(&dtr, sizeof(WaveTrace) * nw) != hipSuccess) return AIRICE_EHIP;
+  hipLaunchKernelGGL((table_kernel<kBlock, true>), dim3(blocks), dim3(kBlock), 0, st, M, I, A,
+                     d_table, d_full, dtr);
+  std::vector<WaveTrace> h(nw);
+  if (hipStreamSynchronize(st) != hipSuccess ||
+      hipMemcpy(h.data(), dtr, sizeof(WaveTrace) * nw, hipMemcpyDeviceToHost) != hipSuccess)
+    return AIRICE_EHIP;
+  (void)hipFree(dtr);
+  if (FILE* f = fopen(trace_path, "ab")) {
+    fwrite(h.data(), sizeof(WaveTrace), nw, f);
+    fclose(f);
+  }
   return launch_ok();
 }
 
