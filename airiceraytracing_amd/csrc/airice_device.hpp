@@ -28,6 +28,8 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include "airice_tlog.hpp"
+
 namespace airice {
 
 constexpr int kMaxLayers = 4;  // ATMLAY has 5 bounds -> at most 4 air layers
@@ -237,41 +239,9 @@ struct Segment {
 // 508-510).  A segment whose ends are at the same height is exactly 0 (or NaN) in the
 // reference: the same function of the same x at both ends.  Endpoints built on the host
 // and on the device can differ by an ulp, so one endpoint is reused.
-// Natural log of a positive normal finite x, < 1 ulp (the fdlibm e_log.c reduction
-// x = 2^k (1+f), sqrt(1/2) <= 1+f < sqrt(2), s = f/(2+f), degree-14 minimax in s):
-// ~45 VALU instead of ocml's ~85 (which also covers denormals and special values).
-// Any other x goes to ocml's log, so NaN / inf / 0 / negative behave exactly as log().
-// Checked against long double on 6e7 arguments: max error 0.84 ulp (tests/test_fastlog.py).
-__device__ __forceinline__ double fast_log(double x_in) {
-  // branch-free: denormals are scaled by 2^54 (k corrected below); 0, negative, NaN and inf
-  // take log()'s IEEE results by select at the end
-  const bool tiny = x_in < 2.2250738585072014e-308;
-  const double x = tiny ? x_in * 18014398509481984.0 : x_in;
-  const double Lg1 = 6.666666666666735130e-01, Lg2 = 3.999999999940941908e-01,
-               Lg3 = 2.857142874366239149e-01, Lg4 = 2.222219843214978396e-01,
-               Lg5 = 1.818357216161805012e-01, Lg6 = 1.531383769920937332e-01,
-               Lg7 = 1.479819860511658591e-01;
-  const double ln2_hi = 6.93147180369123816490e-01, ln2_lo = 1.90821492927058770002e-10;
-  const unsigned long long b = (unsigned long long)__double_as_longlong(x);
-  int k = (int)(b >> 52) - (tiny ? 1023 + 54 : 1023);
-  double m = __longlong_as_double((long long)((b & 0x000fffffffffffffULL) | 0x3ff0000000000000ULL));
-  if (m > 1.4142135623730951) {
-    m *= 0.5;
-    k += 1;
-  }
-  const double f = m - 1.0;
-  const double s = f / (2.0 + f);
-  const double z = s * s, w = z * z;
-  const double t1 = w * __builtin_fma(w, __builtin_fma(w, Lg6, Lg4), Lg2);
-  const double t2 = z * __builtin_fma(w, __builtin_fma(w, __builtin_fma(w, Lg7, Lg5), Lg3), Lg1);
-  const double R = t2 + t1;
-  const double hfsq = 0.5 * f * f;
-  const double dk = (double)k;
-  const double r = dk * ln2_hi - ((hfsq - (s * (hfsq + R) + dk * ln2_lo)) - f);
-  // log(+-0) = -inf, log(+inf) = +inf, log(<0) = log(NaN) = NaN
-  const double special = (x_in == 0.0) ? -__builtin_inf() : (x_in > 0.0 ? x_in : __builtin_nan(""));
-  return (x_in > 0.0 && x_in < __builtin_inf()) ? r : special;
-}
+// Natural log: the table-driven tlog() of airice_tlog.hpp (< 1 ulp, no division, IEEE special
+// values; its g++-compiled twin is the bit reference in tests/test_tlog.py).
+__device__ __forceinline__ double fast_log(double x) { return tlog(x); }
 
 __device__ __forceinline__ double log_ratio(double a, double b) {
   // log(a) - log(b) as one logarithm when both are in log's domain (identity (5)); outside it,

@@ -1,0 +1,82 @@
+// airice_tlog.hpp -- table-driven natural logarithm for the device (and, compiled by g++, its
+// bit-exact CPU twin used by tests/cpp/tlog_check.cpp).
+//
+// x = 2^k z, z in [0.6875, 1.375) (bit offset 0x3fe6000000000000); i = top 8 bits of the offset
+// mantissa; r = fma(z, 1/c_i, -1) (|r| <= 2^-8, one rounding); log x = k ln2 + log c_i + log1p(r)
+// with log1p(r) - r by a degree-7 Taylor polynomial (truncation <= 2^-67) and the k ln2 + log c_i
+// + r sum kept in hi + lo form.  No division; ~16 FP64 + ~6 integer VALU ops and one 16-byte table
+// load (airice_logtab.h, tools/gen_log_table.py) against ~45 for the fdlibm form with its divide.
+// Error < 1 ulp (tests/test_tlog.py measures it against mpmath on the CPU twin and checks that
+// the GPU returns the same bits).
+#pragma once
+
+#include <cstdint>
+#include <cstring>
+
+#ifndef __HIPCC__
+#include <cmath>
+#define __host__
+#define __device__
+#define AIRICE_FMA(a, b, c) std::fma((a), (b), (c))
+#define AIRICE_INLINE inline
+#else
+#define AIRICE_FMA(a, b, c) __builtin_fma((a), (b), (c))
+#define AIRICE_INLINE __forceinline__
+#endif
+
+#include "airice_logtab.h"
+
+namespace airice {
+
+__host__ __device__ AIRICE_INLINE uint64_t dbits(double x) {
+  uint64_t u;
+  std::memcpy(&u, &x, sizeof(u));
+  return u;
+}
+
+__host__ __device__ AIRICE_INLINE double bitsd(uint64_t u) {
+  double x;
+  std::memcpy(&x, &u, sizeof(x));
+  return x;
+}
+
+// log(x) for x positive, normal and finite.
+__host__ __device__ AIRICE_INLINE double tlog_pos(double x) {
+  const double Ln2hi = 0x1.62e42fefa3800p-1;  // ln 2 with 11 low zero bits: k*Ln2hi is exact
+  const double Ln2lo = 0x1.ef35793c76730p-45;
+  const double A0 = -0x1p-1, A1 = 0x1.5555555555555p-2, A2 = -0x1p-2, A3 = 0x1.999999999999ap-3,
+               A4 = -0x1.5555555555555p-3, A5 = 0x1.2492492492492p-3;  // -1/2, 1/3, ..., 1/7
+  const uint64_t ix = dbits(x);
+  const uint64_t tmp = ix - 0x3fe6000000000000ULL;
+  const int i = (int)((tmp >> (52 - kLogTableBits)) & ((1u << kLogTableBits) - 1));
+  const int k = (int)((int64_t)tmp >> 52);
+  const double z = bitsd(ix - (tmp & 0xfff0000000000000ULL));
+  const double invc = kLogTable[i][0], logc = kLogTable[i][1];
+  const double r = AIRICE_FMA(z, invc, -1.0);
+  const double kd = (double)k;
+  // w = k Ln2hi + logc in hi + lo form: k Ln2hi is exact and, when k != 0, larger than |logc|
+  // (< 0.38), so Fast2Sum gives the rounding error of w exactly
+  const double t = kd * Ln2hi;
+  const double w = t + logc;
+  const double we = (t - w) + logc;
+  const double hi = w + r;
+  const double lo = AIRICE_FMA(kd, Ln2lo, ((w - hi) + r) + we);
+  const double r2 = r * r;
+  double q = AIRICE_FMA(r, A5, A4);
+  q = AIRICE_FMA(r2, q, AIRICE_FMA(r, A3, A2));
+  q = AIRICE_FMA(r2, q, AIRICE_FMA(r, A1, A0));
+  return AIRICE_FMA(r2, q, lo) + hi;
+}
+
+// log(x) for any x with log()'s IEEE special values: denormals are scaled by 2^54 (exact) and
+// 0 / negative / NaN / inf are selected at the end, so the code is branch-free.
+__host__ __device__ AIRICE_INLINE double tlog(double x_in) {
+  const bool tiny = x_in < 0x1p-1022;
+  const double x = tiny ? x_in * 0x1p54 : x_in;
+  const double y = tlog_pos(x) - (tiny ? 54 * 0x1.62e42fefa39efp-1 : 0.0);
+  const double inf = __builtin_inf();
+  const double special = (x_in == 0.0) ? -inf : (x_in > 0.0 ? x_in : __builtin_nan(""));
+  return (x_in > 0.0 && x_in < inf) ? y : special;
+}
+
+}  // namespace airice

@@ -1,0 +1,32 @@
+// GPU side of the tlog check: the device tlog() (airice_tlog.hpp, as the kernels inline it) over
+// the same deterministic inputs as tests/cpp/tlog_check.cpp, written for a bitwise comparison.
+//   tlog_gpu N seed out.bin
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+
+#include "../../airiceraytracing_amd/csrc/airice_tlog.hpp"
+#include "tlog_inputs.hpp"
+
+__global__ void tlog_kernel(uint64_t n, uint64_t seed, double* y) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) y[i] = airice::tlog(tlog_input(i, seed));
+}
+
+int main(int argc, char** argv) {
+  if (argc < 4) return 2;
+  const uint64_t n = std::strtoull(argv[1], nullptr, 10), seed = std::strtoull(argv[2], nullptr, 10);
+  double* d = nullptr;
+  if (hipMalloc(&d, sizeof(double) * n) != hipSuccess) return 3;
+  hipLaunchKernelGGL(tlog_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, 0, n, seed, d);
+  std::vector<double> y(n);
+  if (hipMemcpy(y.data(), d, sizeof(double) * n, hipMemcpyDeviceToHost) != hipSuccess) return 4;
+  (void)hipFree(d);
+  std::FILE* f = std::fopen(argv[3], "wb");
+  if (!f) return 5;
+  std::fwrite(y.data(), sizeof(double), n, f);
+  std::fclose(f);
+  return 0;
+}

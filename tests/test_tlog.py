@@ -1,0 +1,80 @@
+"""The device logarithm tlog() (airiceraytracing_amd/csrc/airice_tlog.hpp, table from
+tools/gen_log_table.py), which every log_ratio of the ray kernels evaluates.
+
+CPU: its g++-compiled twin (tests/cpp/tlog_check) is within 1 ulp of long double logl over 4e6
+deterministic inputs (normals over the whole range, |x-1| < 2^-6, the kernels' [0.5, 4) range,
+denormals) and returns log()'s special values; a sample is also checked against mpmath.
+GPU: the device returns the same bits as the twin (every step is an IEEE op or an fma)."""
+import json
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+from tests.conftest import ROOT
+
+CPU = os.path.join(ROOT, "tests", "cpp", "tlog_check")
+GPU = os.path.join(ROOT, "tests", "cpp", "tlog_gpu")
+N = 4_000_000
+
+
+def _cpu(tmp_path, n=N, seed=12345):
+    assert os.path.exists(CPU), "build with __graft_entry__.build()"
+    out = tmp_path / "cpu.bin"
+    r = subprocess.run([CPU, str(n), str(seed), str(out)], capture_output=True, text=True,
+                       timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    return json.loads(r.stdout), np.fromfile(out, dtype=np.float64)
+
+
+def test_twin_within_one_ulp(tmp_path):
+    rep, y = _cpu(tmp_path)
+    assert rep["max_ulp"] < 1.0, rep
+    assert y.size == N
+
+
+def test_twin_against_mpmath(tmp_path):
+    mpmath = pytest.importorskip("mpmath")
+    import struct
+    _, y = _cpu(tmp_path, n=40000, seed=77)
+    # regenerate the inputs exactly as tlog_inputs.hpp does, for the finite positive ones
+    mask64 = (1 << 64) - 1
+
+    def splitmix(s):
+        s = (s + 0x9E3779B97F4A7C15) & mask64
+        z = s
+        z = ((z ^ (z >> 30)) * 0xBF58476D1CE4E5B9) & mask64
+        z = ((z ^ (z >> 27)) * 0x94D049BB133111EB) & mask64
+        return z ^ (z >> 31)
+
+    worst = 0.0
+    mpmath.mp.prec = 120
+    for i in range(0, 40000, 7):
+        if i % 4 == 3:
+            continue
+        u = splitmix((77 ^ ((i * 0x632BE59BD9B4E019) & mask64)) & mask64)
+        if i % 4 == 0:
+            b = (u % (0x7FEFFFFFFFFFFFFF - 0x0010000000000000)) + 0x0010000000000000
+            x = struct.unpack("<d", struct.pack("<Q", b))[0]
+        elif i % 4 == 1:
+            x = 1.0 + ((u >> 11) * 2.0**-53 - 0.5) * 2.0**-5
+        else:
+            x = 0.5 + (u >> 11) * 2.0**-53 * 3.5
+        ref = mpmath.log(mpmath.mpf(x))
+        ulp = np.spacing(abs(float(ref)))
+        worst = max(worst, float(abs(mpmath.mpf(float(y[i])) - ref)) / ulp)
+    assert worst < 1.0, worst
+
+
+@pytest.mark.gpu
+def test_device_matches_twin_bitwise(tmp_path):
+    assert os.path.exists(GPU), "build with __graft_entry__.build()"
+    _, y_cpu = _cpu(tmp_path)
+    out = tmp_path / "gpu.bin"
+    r = subprocess.run([GPU, str(N), "12345", str(out)], capture_output=True, text=True,
+                       timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    y_gpu = np.fromfile(out, dtype=np.float64)
+    same = (y_gpu.view(np.uint64) == y_cpu.view(np.uint64)) | (np.isnan(y_gpu) & np.isnan(y_cpu))
+    assert same.all(), np.flatnonzero(~same)[:10]
