@@ -243,13 +243,24 @@ struct Segment {
 // values; its g++-compiled twin is the bit reference in tests/test_tlog.py).
 __device__ __forceinline__ double fast_log(double x) { return tlog(x); }
 
+// log(a) - log(b) as one logarithm (identity (5)).  Fast path -- a, b and a/b positive and
+// within 2^+-1000, i.e. every ray except special values -- takes the quotient from v_rcp_f64
+// refined by two Newton steps and one residual correction (Markstein; the IEEE quotient in all
+// but rare last-bit cases) and the table log without its special-value handling.  Otherwise:
+// the IEEE division and the IEEE value of log(a) - log(b) (-inf - finite, finite - (-inf), NaN).
 __device__ __forceinline__ double log_ratio(double a, double b) {
-  // log(a) - log(b) as one logarithm when both are in log's domain (identity (5)); outside it,
-  // the IEEE value of log(a) - log(b): -inf - finite, finite - (-inf), NaN otherwise
+  double y = __builtin_amdgcn_rcp(b);
+  y = __builtin_fma(y, __builtin_fma(-b, y, 1.0), y);
+  y = __builtin_fma(y, __builtin_fma(-b, y, 1.0), y);
+  const double q0 = a * y;
+  const double q = __builtin_fma(__builtin_fma(-b, q0, a), y, q0);
+  if (a > 0x1p-1000 && a < 0x1p1000 && b > 0x1p-1000 && b < 0x1p1000 && q > 0x1p-1000 &&
+      q < 0x1p1000)
+    return tlog_pos(q);
   const double special = (a == 0.0 && b > 0.0)   ? -__builtin_inf()
                          : (b == 0.0 && a > 0.0) ? __builtin_inf()
                                                  : __builtin_nan("");
-  return (a > 0.0 && b > 0.0) ? fast_log(a / b) : special;
+  return (a > 0.0 && b > 0.0) ? tlog(a / b) : special;
 }
 
 __device__ __forceinline__ Segment segment(const Endpoint& T, const Endpoint& R_, double A,

@@ -48,9 +48,9 @@ __device__ __forceinline__ Endpoint stop_of(const DevMedium& M, int l) {
 // sin(asin(v) r2d d2r) = v, cos = sqrt(1 - v^2) on [0, 90] degrees).
 __device__ __forceinline__ void fresnel_from_sine(double n1, double n2, double v, double& tS,
                                                   double& tP) {
-  const double st = v, ct = sqrt(1 - v * v);
+  const double st = v, ct = fast_sqrt(1 - v * v);
   const double a = (n1 / n2) * st;
-  const double sqterm = sqrt(1 - a * a);
+  const double sqterm = fast_sqrt(1 - a * a);
   double num = n1 * ct - n2 * sqterm;
   double den = n1 * ct + n2 * sqterm;
   tS = 1 + (num / den);
