@@ -254,8 +254,9 @@ __device__ __forceinline__ double log_ratio(double a, double b) {
   y = __builtin_fma(y, __builtin_fma(-b, y, 1.0), y);
   const double q0 = a * y;
   const double q = __builtin_fma(__builtin_fma(-b, q0, a), y, q0);
-  if (a > 0x1p-1000 && a < 0x1p1000 && b > 0x1p-1000 && b < 0x1p1000 && q > 0x1p-1000 &&
-      q < 0x1p1000)
+  // a > 0 and q in range cover a (a tiny / huge / inf / NaN shows in q or in a > 0); b in range
+  // keeps v_rcp_f64 and the Newton steps clear of overflow and denormals
+  if (a > 0.0 && b > 0x1p-1000 && b < 0x1p1000 && q > 0x1p-1000 && q < 0x1p1000)
     return tlog_pos(q);
   const double special = (a == 0.0 && b > 0.0)   ? -__builtin_inf()
                          : (b == 0.0 && a > 0.0) ? __builtin_inf()

@@ -46,11 +46,14 @@ __host__ __device__ AIRICE_INLINE double tlog_pos(double x) {
   const double Ln2lo = 0x1.ef35793c76730p-45;
   const double A0 = -0x1p-1, A1 = 0x1.5555555555555p-2, A2 = -0x1p-2, A3 = 0x1.999999999999ap-3,
                A4 = -0x1.5555555555555p-3, A5 = 0x1.2492492492492p-3;  // -1/2, 1/3, ..., 1/7
+  // the reduction touches only the high word (the offset has a zero low word); 32-bit integer
+  // ops throughout so the exponent converts with one v_cvt_f64_i32
   const uint64_t ix = dbits(x);
-  const uint64_t tmp = ix - 0x3fe6000000000000ULL;
-  const int i = (int)((tmp >> (52 - kLogTableBits)) & ((1u << kLogTableBits) - 1));
-  const int k = (int)((int64_t)tmp >> 52);
-  const double z = bitsd(ix - (tmp & 0xfff0000000000000ULL));
+  const uint32_t hx = (uint32_t)(ix >> 32);
+  const uint32_t htmp = hx - 0x3fe60000u;
+  const int i = (int)((htmp >> (20 - kLogTableBits)) & ((1u << kLogTableBits) - 1));
+  const int k = (int32_t)htmp >> 20;
+  const double z = bitsd(((uint64_t)(hx - (htmp & 0xfff00000u)) << 32) | (ix & 0xffffffffULL));
   const double invc = kLogTable[i][0], logc = kLogTable[i][1];
   const double r = AIRICE_FMA(z, invc, -1.0);
   const double kd = (double)k;
@@ -62,9 +65,12 @@ __host__ __device__ AIRICE_INLINE double tlog_pos(double x) {
   const double hi = w + r;
   const double lo = AIRICE_FMA(kd, Ln2lo, ((w - hi) + r) + we);
   const double r2 = r * r;
+  // Horner: one constant per fma (no constant materialised in VGPRs but A5)
   double q = AIRICE_FMA(r, A5, A4);
-  q = AIRICE_FMA(r2, q, AIRICE_FMA(r, A3, A2));
-  q = AIRICE_FMA(r2, q, AIRICE_FMA(r, A1, A0));
+  q = AIRICE_FMA(r, q, A3);
+  q = AIRICE_FMA(r, q, A2);
+  q = AIRICE_FMA(r, q, A1);
+  q = AIRICE_FMA(r, q, A0);
   return AIRICE_FMA(r2, q, lo) + hi;
 }
 
