@@ -19,6 +19,7 @@
 #include <cmath>
 #include <cstdint>
 #include <cstdio>
+#include <algorithm>
 #include <cstdlib>
 #include <vector>
 
@@ -78,43 +79,75 @@ __device__ __forceinline__ TopEnd topend_of(const IceConsts& I, int top) {
   return r;
 }
 
-// First (Tx) layer of a ray: per-lane start end T, stop end R; identity (5) as in segment().
-__device__ __forceinline__ Segment segment_top(const Endpoint& T, const TopEnd& R_, double A,
-                                               double A2, double sin_in, double& v_out) {
+// Everything of a ray that depends on its Tx height only: the Tx layer and the Tx layer's
+// segment folded like the lower layers' (Tx endpoint -> the layer's stop end, or the ice).  The
+// table computes it once per row into LDS (a block spans few rows); other launches per lane.
+struct RowConst {
+  SegConst seg;  // Tx endpoint -> stop end of the Tx layer (zero-length case resolved)
+  double H;
+  int top;       // MaxLayers - SkipLayersAbove - 1
+  int any;       // top >= bot: at least one air layer
+};
+
+__device__ __forceinline__ RowConst row_const(const DevMedium& M, const IceConsts& I, double H) {
+  RowConst rc;
+  rc.H = H;
+  rc.top = top_layer(M, H);
+  rc.any = rc.top >= I.bot;
+  const Endpoint T = air_endpoint(M, H);
+  const TopEnd R_ = topend_of(I, rc.top);
   // zero-length (Tx exactly on the layer's lower bound / the ice): reuse the Tx end
   const bool zl = (R_.x == T.x);
-  const double speedc = 299792458.0;
-  const TopEnd R = zl ? TopEnd{T.x, T.n, T.y2, T.Ay, T.invC, T.invC * (1.0 / speedc), T.Cx, T.ACx}
-                      : R_;
-  const double v2 = sin_asin((T.n * sin_in) / R.n);
-  const RayL RL = ray_L(A2, R.n * v2);
-  const double syR = fast_sqrt(R.y2 - RL.LL), syT = fast_sqrt(T.y2 - RL.LL);
-  const double d1 = log_ratio(R.Ay - RL.LL + RL.sAL * syR, T.Ay - RL.LL + RL.sAL * syT);
-  const double d2 = log_ratio(R.n + syR, T.n + syT);
-  const double dCx = R.Cx - T.Cx;
-  Segment s;
-  s.thd = -((RL.L * R.invC) * RL.rsAL * (dCx - d1));
-  s.t = -(((syR - syT) + A2 * RL.rsAL * (dCx - d1) + A * d2) * R.invCc);
-  s.geo = -((d2 - (A * d1) * RL.rsAL + (R.ACx - T.ACx) * RL.rsAL) * R.invC);
-  v_out = v2;
-  return s;
+  SegConst& s = rc.seg;
+  s.Tn = T.n;
+  s.Ty2 = T.y2;
+  s.TAy = T.Ay;
+  s.Rn = zl ? T.n : R_.n;
+  s.Ry2 = zl ? T.y2 : R_.y2;
+  s.RAy = zl ? T.Ay : R_.Ay;
+  s.ratio = T.n / s.Rn;
+  s.invC = zl ? T.invC : R_.invC;
+  s.invCc = zl ? T.invC * (1.0 / kSpeedC) : R_.invCc;
+  s.dCx = zl ? 0.0 : R_.Cx - T.Cx;
+  s.dACx = zl ? 0.0 : R_.ACx - T.ACx;
+  return rc;
+}
+
+// sin(x) for the start angle's radians, x = (180 - theta) pi/180 in [0, pi/2] for every launch
+// angle in [90, 180]: odd Taylor polynomial to x^23 (truncation < 2^-59 relative on the range);
+// other arguments go to ocml's sin.
+__device__ __forceinline__ double sin_start(double x) {
+  if (!(x >= 0.0 && x <= 1.5707963267948966)) return sin(x);
+  const double x2 = x * x;
+  // (-1)^k / (2k+1)!, k = 11 .. 1, as doubles
+  double p = __builtin_fma(x2, -0x1.761b41316381ap-75, 0x1.71b8ef6dcf572p-66);  // 1/23!, 1/21!
+  p = __builtin_fma(x2, p, -0x1.2f49b46814157p-57);                             // 1/19!
+  p = __builtin_fma(x2, p, 0x1.952c77030ad4ap-49);                              // 1/17!
+  p = __builtin_fma(x2, p, -0x1.ae7f3e733b81fp-41);                             // 1/15!
+  p = __builtin_fma(x2, p, 0x1.6124613a86d09p-33);                              // 1/13!
+  p = __builtin_fma(x2, p, -0x1.ae64567f544e4p-26);                             // 1/11!
+  p = __builtin_fma(x2, p, 0x1.71de3a556c734p-19);                              // 1/9!
+  p = __builtin_fma(x2, p, -0x1.a01a01a01a01ap-13);                             // 1/7!
+  p = __builtin_fma(x2, p, 0x1.1111111111111p-7);                               // 1/5!
+  p = __builtin_fma(x2, p, -0x1.5555555555555p-3);                              // 1/3!
+  return __builtin_fma(x * x2, p, x);
 }
 
 // want_inc: dummy[12] (the incidence angle on the ice, one asin) is not a table column
 // (.cc:2101-2111), so table launches without the double output skip it.
-__device__ __forceinline__ void ray_solution(const DevMedium& M, const IceConsts& I, double theta,
-                                             double H, bool in_ice, double* d,
-                                             bool want_inc = true) {
-  const int top = top_layer(M, H);
+__device__ __forceinline__ void ray_solution_row(const DevMedium& M, const IceConsts& I,
+                                                 const RowConst& rc, double theta, bool in_ice,
+                                                 double* d, bool want_inc) {
+  const double H = rc.H;
+  const int top = rc.top;
   const int bot = I.bot;
   const double A2 = M.A_air * M.A_air;
-  double v = sin((180 - theta) * M.d2r);  // sine of StartAngle (.cc:1863)
+  double v = sin_start((180 - theta) * M.d2r);  // sine of StartAngle (.cc:1863)
   double thd_air = 0.0, t_air = 0.0, geo_air = 0.0;
-  const bool any = top >= bot;
+  const bool any = rc.any != 0;
   if (any) {
     // n_layer1 == Getnz_air(StartHeight) == nzTx: Snell into a layer is the identity
-    const Endpoint T = air_endpoint(M, H);
-    const Segment s = segment_top(T, topend_of(I, top), M.A_air, A2, sin_asin(v), v);
+    const Segment s = segment_const(rc.seg, M.A_air, A2, sin_asin(v), true, v);
     thd_air += s.thd;
     t_air += s.t;
     geo_air += s.geo;
@@ -166,13 +199,22 @@ __device__ __forceinline__ void ray_solution(const DevMedium& M, const IceConsts
   d[17] = geo_ice;
 }
 
+// Per-lane form (rays, minimizer evaluations): the row constants of its own Tx height.
+__device__ __forceinline__ void ray_solution(const DevMedium& M, const IceConsts& I, double theta,
+                                             double H, bool in_ice, double* d,
+                                             bool want_inc = true) {
+  const RowConst rc = row_const(M, I, H);
+  ray_solution_row(M, I, rc, theta, in_ice, d, want_inc);
+}
+
 struct TableArgs {
   double start_h, stop_h, step_h;
   double start_a, stop_a, step_a;
-  double inv_asteps;  // 1.0 / asteps (row of ray k without a 64-bit division)
+  double inv_asteps;  // 1.0 / asteps (row of ray k without an integer division)
   int hsteps, asteps;
   int row0, in_ice;
-  long long n;
+  int n;              // rays of this launch (< 2^31; launch_table splits larger grids)
+  int rows_per_block; // LDS rows a block may span
   size_t ld;
 };
 
@@ -183,23 +225,32 @@ struct WaveTrace {
   unsigned hw_id, xcc_id;
 };
 
-// One table entry: ray k of the launch (row-major over TxH rows x launch angles).
-__device__ __forceinline__ void table_ray(const DevMedium& M, const IceConsts& I,
-                                          const TableArgs& G, long long k,
-                                          float* __restrict__ table, double* __restrict__ full) {
-  // r = k / asteps: the double quotient is within 1 of the true one (k < 2^52), then fixed up
-  long long r = (long long)((double)k * G.inv_asteps);
+// Tx height of grid row ihei (.cc:2080, 2089-2091; separate mul and add, no contraction).
+__device__ __forceinline__ double row_height(const TableArgs& G, int ihei) {
+  double H = G.start_h - G.step_h * ihei;
+  if (H != G.stop_h && ihei == G.hsteps - 1) H = G.stop_h;
+  return H;
+}
+
+// Row (within the launch) of ray k: the double quotient k / asteps is within 1 of the integer
+// one for k < 2^31, then fixed up.
+__device__ __forceinline__ int ray_row(const TableArgs& G, int k) {
+  int r = (int)((double)k * G.inv_asteps);
   if (r * G.asteps > k) --r;
   if ((r + 1) * G.asteps <= k) ++r;
-  const int iang = (int)(k - r * G.asteps);
-  const int ihei = G.row0 + (int)r;
-  // .cc:2080, 2085, 2089-2094 (separate mul and add: no contraction)
-  double H = G.start_h - G.step_h * ihei;
+  return r;
+}
+
+// One table entry: ray k of the launch (row r, row-major over TxH rows x launch angles).
+__device__ __forceinline__ void table_ray(const DevMedium& M, const IceConsts& I,
+                                          const TableArgs& G, const RowConst& rc, int r, int k,
+                                          float* __restrict__ table, double* __restrict__ full) {
+  const int iang = k - r * G.asteps;
+  // .cc:2085, 2092-2094
   double th = G.start_a + G.step_a * iang;
-  if (H != G.stop_h && ihei == G.hsteps - 1) H = G.stop_h;
   if (iang == G.asteps - 1) th = G.stop_a;
   double d[18];
-  ray_solution(M, I, th, H, G.in_ice != 0, d, full != nullptr);
+  ray_solution_row(M, I, rc, th, G.in_ice != 0, d, full != nullptr);
   const size_t ld = G.ld;
   // AllTableAllAntData columns (.cc:2101-2111)
   table[0 * ld + k] = (float)d[1];
@@ -219,19 +270,33 @@ __device__ __forceinline__ void table_ray(const DevMedium& M, const IceConsts& I
   }
 }
 
-// Table launch: one ray per lane.  (Persistent grid-stride and atomic-chunk schedules were
-// measured and rejected: the loop around the inlined ray body raises register pressure to
-// 160 VGPRs, or 330 B/lane of scratch when capped at 64, and run 2.7x / 7x slower.)
+// Table launch: one ray per lane.  The block first evaluates the Tx-height-only constants of the
+// (few) rows it spans into LDS -- one lane per row, so the exp / layer scans / top-layer folding
+// run once per row instead of once per wave -- then every lane traces its ray.  (Persistent
+// grid-stride and atomic-chunk schedules were measured and rejected: the loop around the inlined
+// ray body raises register pressure to 160 VGPRs, or 330 B/lane of scratch when capped at 64,
+// and runs 2.7x / 7x slower.)
 template <int BS, bool TRACE = false>
 __global__ __launch_bounds__(BS) void table_kernel(DevMedium M, IceConsts I, TableArgs G,
                                                    float* __restrict__ table,
                                                    double* __restrict__ full,
                                                    WaveTrace* __restrict__ trace) {
+  extern __shared__ __align__(16) unsigned char smem[];
+  RowConst* rows = reinterpret_cast<RowConst*>(smem);
   const unsigned wave = blockIdx.x * (BS / 64) + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   if (TRACE && lane == 0) trace[wave].t0 = __builtin_amdgcn_s_memrealtime();
-  const long long k = (long long)blockIdx.x * BS + threadIdx.x;
-  if (k < G.n) table_ray(M, I, G, k, table, full);
+  const int k0 = (int)blockIdx.x * BS;
+  const int r0 = ray_row(G, k0);
+  const int nrows = ray_row(G, min(k0 + BS, G.n) - 1) - r0 + 1;
+  for (int t = threadIdx.x; t < nrows; t += BS)
+    rows[t] = row_const(M, I, row_height(G, G.row0 + r0 + t));
+  __syncthreads();
+  const int k = k0 + (int)threadIdx.x;
+  if (k < G.n) {
+    const int r = ray_row(G, k);
+    table_ray(M, I, G, rows[r - r0], r, k, table, full);
+  }
   if (TRACE && lane == 0) {
     trace[wave].t1 = __builtin_amdgcn_s_memrealtime();
     trace[wave].hw_id = __builtin_amdgcn_s_getreg((4 << 0) | (0 << 6) | (31 << 11));  // HW_ID
@@ -827,6 +892,7 @@ static inline int launch_ok() { return hipGetLastError() == hipSuccess ? AIRICE_
 
 int launch_table(const DevMedium& M, const IceConsts& I, const airice_grid* g, int row_begin,
                  int row_count, float* d_table, double* d_full, size_t ld, hipStream_t st) {
+  if (row_count <= 0 || g->angle_steps <= 0) return AIRICE_OK;
   TableArgs A;
   A.start_h = g->start_height;
   A.stop_h = g->stop_height;
@@ -836,33 +902,45 @@ int launch_table(const DevMedium& M, const IceConsts& I, const airice_grid* g, i
   A.step_a = g->angle_step;
   A.hsteps = g->height_steps;
   A.asteps = g->angle_steps;
-  A.row0 = row_begin;
   A.in_ice = g->in_ice;
-  A.n = (long long)row_count * g->angle_steps;
   A.ld = ld;
   A.inv_asteps = 1.0 / (double)g->angle_steps;
-  if (A.n == 0) return AIRICE_OK;
+  // rows a 256-ray block can touch, for the LDS row constants
+  A.rows_per_block = std::min(kBlock, (kBlock - 1) / g->angle_steps + 2);
+  const size_t lds = sizeof(RowConst) * (size_t)A.rows_per_block;
   static const char* trace_path = getenv("AIRICE_TABLE_TRACE");
-  const unsigned blocks = grid_for(A.n);
-  if (trace_path == nullptr) {
-    hipLaunchKernelGGL((table_kernel<kBlock, false>), dim3(blocks), dim3(kBlock), 0, st, M, I, A,
-                       d_table, d_full, nullptr);
-    return launch_ok();
-  }
-  // debug timeline (tools/wave_timeline.py): synchronous, one record per wave appended to the file
-  const long long nw = (long long)blocks * (kBlock / 64);
-  WaveTrace* dtr = nullptr;
-  if (hipMalloc(&dtr, sizeof(WaveTrace) * nw) != hipSuccess) return AIRICE_EHIP;
-  hipLaunchKernelGGL((table_kernel<kBlock, true>), dim3(blocks), dim3(kBlock), 0, st, M, I, A,
-                     d_table, d_full, dtr);
-  std::vector<WaveTrace> h(nw);
-  if (hipStreamSynchronize(st) != hipSuccess ||
-      hipMemcpy(h.data(), dtr, sizeof(WaveTrace) * nw, hipMemcpyDeviceToHost) != hipSuccess)
-    return AIRICE_EHIP;
-  (void)hipFree(dtr);
-  if (FILE* f = fopen(trace_path, "ab")) {
-    fwrite(h.data(), sizeof(WaveTrace), nw, f);
-    fclose(f);
+  // ray indices are 32-bit inside a launch: grids of 2^31 rays or more go in row slabs
+  const int max_rows = (int)std::max<long long>(1, ((1LL << 31) - kBlock) / g->angle_steps);
+  for (int done = 0; done < row_count;) {
+    const int rows = std::min(max_rows, row_count - done);
+    const size_t off = (size_t)done * (size_t)g->angle_steps;
+    A.row0 = row_begin + done;
+    A.n = rows * g->angle_steps;
+    float* tab = d_table + off;
+    double* full = d_full ? d_full + off : nullptr;
+    const unsigned blocks = grid_for(A.n);
+    done += rows;
+    if (trace_path == nullptr) {
+      hipLaunchKernelGGL((table_kernel<kBlock, false>), dim3(blocks), dim3(kBlock), lds, st, M, I,
+                         A, tab, full, nullptr);
+      if (hipGetLastError() != hipSuccess) return AIRICE_EHIP;
+      continue;
+    }
+    // debug timeline (tools/wave_timeline.py): synchronous, one record per wave appended
+    const long long nw = (long long)blocks * (kBlock / 64);
+    WaveTrace* dtr = nullptr;
+    if (hipMalloc(&dtr, sizeof(WaveTrace) * nw) != hipSuccess) return AIRICE_EHIP;
+    hipLaunchKernelGGL((table_kernel<kBlock, true>), dim3(blocks), dim3(kBlock), lds, st, M, I, A,
+                       tab, full, dtr);
+    std::vector<WaveTrace> h(nw);
+    if (hipStreamSynchronize(st) != hipSuccess ||
+        hipMemcpy(h.data(), dtr, sizeof(WaveTrace) * nw, hipMemcpyDeviceToHost) != hipSuccess)
+      return AIRICE_EHIP;
+    (void)hipFree(dtr);
+    if (FILE* f = fopen(trace_path, "ab")) {
+      fwrite(h.data(), sizeof(WaveTrace), nw, f);
+      fclose(f);
+    }
   }
   return launch_ok();
 }
