@@ -248,7 +248,7 @@ __device__ __forceinline__ double fast_log(double x) { return tlog(x); }
 // refined by two Newton steps and one residual correction (Markstein; the IEEE quotient in all
 // but rare last-bit cases) and the table log without its special-value handling.  Otherwise:
 // the IEEE division and the IEEE value of log(a) - log(b) (-inf - finite, finite - (-inf), NaN).
-__device__ __forceinline__ double log_ratio(double a, double b) {
+__device__ __forceinline__ double log_ratio_fast(double a, double b, const double* tab, bool& ok) {
   double y = __builtin_amdgcn_rcp(b);
   y = __builtin_fma(y, __builtin_fma(-b, y, 1.0), y);
   y = __builtin_fma(y, __builtin_fma(-b, y, 1.0), y);
@@ -256,16 +256,40 @@ __device__ __forceinline__ double log_ratio(double a, double b) {
   const double q = __builtin_fma(__builtin_fma(-b, q0, a), y, q0);
   // a > 0 and q in range cover a (a tiny / huge / inf / NaN shows in q or in a > 0); b in range
   // keeps v_rcp_f64 and the Newton steps clear of overflow and denormals
-  if (a > 0.0 && b > 0x1p-1000 && b < 0x1p1000 && q > 0x1p-1000 && q < 0x1p1000)
-    return tlog_pos(q);
+  ok = a > 0.0 && b > 0x1p-1000 && b < 0x1p1000 && q > 0x1p-1000 && q < 0x1p1000;
+  return tlog_pos(q, tab);  // garbage, and unused, when !ok
+}
+
+__device__ __forceinline__ double log_ratio_ieee(double a, double b) {
   const double special = (a == 0.0 && b > 0.0)   ? -__builtin_inf()
                          : (b == 0.0 && a > 0.0) ? __builtin_inf()
                                                  : __builtin_nan("");
   return (a > 0.0 && b > 0.0) ? tlog(a / b) : special;
 }
 
+__device__ __forceinline__ double log_ratio(double a, double b) {
+  bool ok;
+  const double r = log_ratio_fast(a, b, &kLogTable[0][0], ok);
+  if (ok) return r;
+  return log_ratio_ieee(a, b);
+}
+
+// The two log-ratios of a segment: both fast paths straight-line (so their table loads and
+// polynomials overlap), then one rarely taken branch for special values.
+__device__ __forceinline__ void log_ratio2(double a1, double b1, double a2, double b2,
+                                           const double* tab, double& d1, double& d2) {
+  bool ok1, ok2;
+  d1 = log_ratio_fast(a1, b1, tab, ok1);
+  d2 = log_ratio_fast(a2, b2, tab, ok2);
+  if (!(ok1 && ok2)) {
+    if (!ok1) d1 = log_ratio_ieee(a1, b1);
+    if (!ok2) d2 = log_ratio_ieee(a2, b2);
+  }
+}
+
 __device__ __forceinline__ Segment segment(const Endpoint& T, const Endpoint& R_, double A,
-                                           double A2, const RayL& RL, bool air) {
+                                           double A2, const RayL& RL, bool air,
+                                           const double* tab = &kLogTable[0][0]) {
   const double speedc = 299792458.0;
   const Endpoint R = pick(R_.x == T.x, T, R_);
   // Both ends lie in one layer (same C) at x >= 0 -- true of every segment the table and
@@ -275,8 +299,9 @@ __device__ __forceinline__ Segment segment(const Endpoint& T, const Endpoint& R_
   // ftimeD = (s + A^2 (Cx - lg1)/sqrt(A^2-L^2) + A lg2) / (c C) since (n^2-L^2)/s = s.
   Segment s;
   const double syR = fast_sqrt(R.y2 - RL.LL), syT = fast_sqrt(T.y2 - RL.LL);
-  const double d1 = log_ratio(R.Ay - RL.LL + RL.sAL * syR, T.Ay - RL.LL + RL.sAL * syT);
-  const double d2 = log_ratio(R.n + syR, T.n + syT);
+  double d1, d2;
+  log_ratio2(R.Ay - RL.LL + RL.sAL * syR, T.Ay - RL.LL + RL.sAL * syT, R.n + syR, T.n + syT, tab,
+             d1, d2);
   const double dCx = R.Cx - T.Cx;
   s.thd = (RL.L * R.invC) * RL.rsAL * (dCx - d1);
   s.t = ((syR - syT) + A2 * RL.rsAL * (dCx - d1) + A * d2) * (R.invC * (1.0 / speedc));
@@ -292,12 +317,14 @@ __device__ __forceinline__ Segment segment(const Endpoint& T, const Endpoint& R_
 // Segment with both ends folded on the host (SegConst), identity (5).  sin_in is the sine of
 // the incidence inside the start end (sin(lang)); returns the sine of the receive angle.
 __device__ __forceinline__ Segment segment_const(const SegConst& S, double A, double A2, double sin_in,
-                                                 bool air, double& v_out) {
+                                                 bool air, double& v_out,
+                                                 const double* tab = &kLogTable[0][0]) {
   const double v2 = sin_asin(S.ratio * sin_in);
   const RayL RL = ray_L(A2, S.Rn * v2);
   const double syR = fast_sqrt(S.Ry2 - RL.LL), syT = fast_sqrt(S.Ty2 - RL.LL);
-  const double d1 = log_ratio(S.RAy - RL.LL + RL.sAL * syR, S.TAy - RL.LL + RL.sAL * syT);
-  const double d2 = log_ratio(S.Rn + syR, S.Tn + syT);
+  double d1, d2;
+  log_ratio2(S.RAy - RL.LL + RL.sAL * syR, S.TAy - RL.LL + RL.sAL * syT, S.Rn + syR, S.Tn + syT,
+             tab, d1, d2);
   Segment s;
   s.thd = (RL.L * S.invC) * RL.rsAL * (S.dCx - d1);
   s.t = ((syR - syT) + A2 * RL.rsAL * (S.dCx - d1) + A * d2) * S.invCc;

@@ -137,7 +137,8 @@ __device__ __forceinline__ double sin_start(double x) {
 // (.cc:2101-2111), so table launches without the double output skip it.
 __device__ __forceinline__ void ray_solution_row(const DevMedium& M, const IceConsts& I,
                                                  const RowConst& rc, double theta, bool in_ice,
-                                                 double* d, bool want_inc) {
+                                                 double* d, bool want_inc,
+                                                 const double* tab = &kLogTable[0][0]) {
   const double H = rc.H;
   const int top = rc.top;
   const int bot = I.bot;
@@ -147,7 +148,7 @@ __device__ __forceinline__ void ray_solution_row(const DevMedium& M, const IceCo
   const bool any = rc.any != 0;
   if (any) {
     // n_layer1 == Getnz_air(StartHeight) == nzTx: Snell into a layer is the identity
-    const Segment s = segment_const(rc.seg, M.A_air, A2, sin_asin(v), true, v);
+    const Segment s = segment_const(rc.seg, M.A_air, A2, sin_asin(v), true, v, tab);
     thd_air += s.thd;
     t_air += s.t;
     geo_air += s.geo;
@@ -156,7 +157,7 @@ __device__ __forceinline__ void ray_solution_row(const DevMedium& M, const IceCo
 #pragma unroll
   for (int il = kMaxLayers - 2; il >= 0; --il) {
     if (il >= top || il < bot) continue;
-    const Segment s = segment_const(I.lower[il], M.A_air, A2, sin_asin(v), true, v);
+    const Segment s = segment_const(I.lower[il], M.A_air, A2, sin_asin(v), true, v, tab);
     thd_air += s.thd;
     t_air += s.t;
     geo_air += s.geo;
@@ -171,7 +172,7 @@ __device__ __forceinline__ void ray_solution_row(const DevMedium& M, const IceCo
     const double A2i = M.A_ice * M.A_ice;
     const double u = sin_asin((I.n_air_ice / I.n_ice0) * vinc);
     double v2;
-    const Segment s = segment_const(I.iceseg, M.A_ice, A2i, u, false, v2);
+    const Segment s = segment_const(I.iceseg, M.A_ice, A2i, u, false, v2, tab);
     thd_ice += s.thd;
     t_ice += s.t;
     geo_ice += s.geo;
@@ -244,13 +245,14 @@ __device__ __forceinline__ int ray_row(const TableArgs& G, int k) {
 // One table entry: ray k of the launch (row r, row-major over TxH rows x launch angles).
 __device__ __forceinline__ void table_ray(const DevMedium& M, const IceConsts& I,
                                           const TableArgs& G, const RowConst& rc, int r, int k,
-                                          float* __restrict__ table, double* __restrict__ full) {
+                                          float* __restrict__ table, double* __restrict__ full,
+                                          const double* tab) {
   const int iang = k - r * G.asteps;
   // .cc:2085, 2092-2094
   double th = G.start_a + G.step_a * iang;
   if (iang == G.asteps - 1) th = G.stop_a;
   double d[18];
-  ray_solution_row(M, I, rc, th, G.in_ice != 0, d, full != nullptr);
+  ray_solution_row(M, I, rc, th, G.in_ice != 0, d, full != nullptr, tab);
   const size_t ld = G.ld;
   // AllTableAllAntData columns (.cc:2101-2111)
   table[0 * ld + k] = (float)d[1];
@@ -277,12 +279,22 @@ __device__ __forceinline__ void table_ray(const DevMedium& M, const IceConsts& I
 // ray body raises register pressure to 160 VGPRs, or 330 B/lane of scratch when capped at 64,
 // and runs 2.7x / 7x slower.)
 template <int BS, bool TRACE = false>
-__global__ __launch_bounds__(BS) void table_kernel(DevMedium M, IceConsts I, TableArgs G,
+// waves_per_eu(8): 64 VGPRs (12 B/lane spilled) at 8 waves/SIMD measured on par or slightly
+// ahead of 67 VGPRs at 7 (bench 42.0 vs 42.9 us for cfg2).
+__global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(8, 8))) void table_kernel(
+                                                   DevMedium M, IceConsts I, TableArgs G,
                                                    float* __restrict__ table,
                                                    double* __restrict__ full,
                                                    WaveTrace* __restrict__ trace) {
   extern __shared__ __align__(16) unsigned char smem[];
   RowConst* rows = reinterpret_cast<RowConst*>(smem);
+  // the log table (4 KB) staged in LDS: one 16-byte entry per thread
+  __shared__ __align__(16) double s_logtab[1 << kLogTableBits][2];
+  static_assert(BS >= (1 << kLogTableBits), "one table entry per thread");
+  if (threadIdx.x < (1u << kLogTableBits)) {
+    s_logtab[threadIdx.x][0] = kLogTable[threadIdx.x][0];
+    s_logtab[threadIdx.x][1] = kLogTable[threadIdx.x][1];
+  }
   const unsigned wave = blockIdx.x * (BS / 64) + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   if (TRACE && lane == 0) trace[wave].t0 = __builtin_amdgcn_s_memrealtime();
@@ -295,7 +307,7 @@ __global__ __launch_bounds__(BS) void table_kernel(DevMedium M, IceConsts I, Tab
   const int k = k0 + (int)threadIdx.x;
   if (k < G.n) {
     const int r = ray_row(G, k);
-    table_ray(M, I, G, rows[r - r0], r, k, table, full);
+    table_ray(M, I, G, rows[r - r0], r, k, table, full, &s_logtab[0][0]);
   }
   if (TRACE && lane == 0) {
     trace[wave].t1 = __builtin_amdgcn_s_memrealtime();

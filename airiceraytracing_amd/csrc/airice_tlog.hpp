@@ -40,8 +40,9 @@ __host__ __device__ AIRICE_INLINE double bitsd(uint64_t u) {
   return x;
 }
 
-// log(x) for x positive, normal and finite.
-__host__ __device__ AIRICE_INLINE double tlog_pos(double x) {
+// log(x) for x positive, normal and finite.  `tab` is kLogTable or a copy of it (the table
+// kernel stages it in LDS); any other x returns garbage without reading outside the table.
+__host__ __device__ AIRICE_INLINE double tlog_pos(double x, const double* tab = &kLogTable[0][0]) {
   const double Ln2hi = 0x1.62e42fefa3800p-1;  // ln 2 with 11 low zero bits: k*Ln2hi is exact
   const double Ln2lo = 0x1.ef35793c76730p-45;
   const double A0 = -0x1p-1, A1 = 0x1.5555555555555p-2, A2 = -0x1p-2, A3 = 0x1.999999999999ap-3,
@@ -54,7 +55,7 @@ __host__ __device__ AIRICE_INLINE double tlog_pos(double x) {
   const int i = (int)((htmp >> (20 - kLogTableBits)) & ((1u << kLogTableBits) - 1));
   const int k = (int32_t)htmp >> 20;
   const double z = bitsd(((uint64_t)(hx - (htmp & 0xfff00000u)) << 32) | (ix & 0xffffffffULL));
-  const double invc = kLogTable[i][0], logc = kLogTable[i][1];
+  const double invc = tab[2 * i], logc = tab[2 * i + 1];
   const double r = AIRICE_FMA(z, invc, -1.0);
   const double kd = (double)k;
   // w = k Ln2hi + logc in hi + lo form: k Ln2hi is exact and, when k != 0, larger than |logc|
