@@ -347,9 +347,30 @@ static int table_prepare(const airice_medium* m, const airice_grid* g, int32_t r
     set_error("ld smaller than the number of rays");
     return AIRICE_EINVAL;
   }
+  // The launch constants are a pure function of (medium, grid): repeated launches (one table
+  // per antenna, bench steps) reuse the last set instead of re-deriving ~20 host exp()s.
+  struct Prepared {
+    airice_medium m;
+    airice_grid g;
+    DevMedium M;
+    IceConsts I;
+    bool valid = false;
+  };
+  static thread_local Prepared last;
+  if (last.valid && std::memcmp(&last.m, m, sizeof(*m)) == 0 &&
+      std::memcmp(&last.g, g, sizeof(*g)) == 0) {
+    *M = last.M;
+    *I = last.I;
+    return AIRICE_OK;
+  }
   int rc = build_dev_medium(m, AIRICE_VARIANT_MULTIRAY, M);
   if (rc) return rc;
   build_ice_consts(*M, g->stop_height, -g->depth_m, I);
+  last.m = *m;
+  last.g = *g;
+  last.M = *M;
+  last.I = *I;
+  last.valid = true;
   return AIRICE_OK;
 }
 

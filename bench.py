@@ -44,6 +44,11 @@ def parse():
     p.add_argument("--solve-steps", type=int, default=5)
     p.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     p.add_argument("--no-solve", action="store_true", help="skip the minimizer line item")
+    p.add_argument("--no-lookup", action="store_true", help="skip the table-lookup line item")
+    p.add_argument("--default-grid", action="store_true",
+                   help="also time the reference default grid (8.7M rays; off by default so "
+                        "every table_kernel launch of the run is the cfg2 workload)")
+    p.add_argument("--lookup-n", type=int, default=1_000_000)
     p.add_argument("--cpu-threads", type=int, default=16)
     return p.parse_args()
 
@@ -58,7 +63,7 @@ def table_work_per_ray(grid, weights) -> tuple[float, dict]:
     the CSE'd kernel x the number of segments of each ray of the grid, + per-ray terms."""
     from tools.workmodel import segments_per_ray, ray_ops
     segs = segments_per_ray(grid)
-    ops = ray_ops(segs, weights)
+    ops = ray_ops(segs, weights, rays_per_row=grid.angle_steps)
     return ops["W"], {"mean_air_segments": segs["mean_air"], **ops}
 
 
@@ -74,6 +79,7 @@ def pmc_traffic(kernel: str):
 
 def main():
     args = parse()
+    os.environ.setdefault("NCCL_DEBUG", "WARN")  # keep RCCL's banner off stdout
     import torch
     import torch.distributed as dist
 
@@ -113,18 +119,19 @@ def main():
     torch.cuda.synchronize()
     barrier()
     torch.cuda.synchronize()
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-          for _ in range(args.steps)]
+    # HIP events on the launch stream around the K steps: the GPU time per step (kernel plus the
+    # in-stream gap to the next launch); no event packets between the launches themselves
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
+    ev0.record(stream)
     for i in range(args.steps):
-        ev[i][0].record(stream)
         step()
-        ev[i][1].record(stream)
+    ev1.record(stream)
     torch.cuda.synchronize()
     barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
-    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+    kern_ms = ev0.elapsed_time(ev1) / args.steps
     el = torch.tensor([elapsed], dtype=torch.float64, device=coll_dev)
     if distributed:
         dist.all_reduce(el, op=dist.ReduceOp.MAX)
@@ -161,8 +168,65 @@ def main():
             "value": world * args.solve_n * args.solve_steps / float(se.item()),
             "unit": "solves/s",
             "kernel_ms": e0.elapsed_time(e1) / args.solve_steps,
-            "solved_fraction": float((stt.cpu().numpy() & 3 == 0).mean()),
         }
+        # CheckSolution (.cc:978-983) on the last batch, and the rows whose bracket set-up
+        # reads uninitialised GSL state in the reference (AIRICE_SOLVE 1|2|32)
+        thd = out[1].cpu().numpy()
+        err = np.abs(thd - dst)
+        solved = (((err / dst < 0.01) & (dst <= 100)) | ((err < 1) & (dst > 100))) & (thd >= 0)
+        solve["solved_fraction"] = float(solved.mean())
+        solve["unpinned_fraction"] = float(((stt.cpu().numpy() & 35) != 0).mean())
+
+    extra = {}
+    if not args.no_lookup:
+        # batched GetHorizontalDistanceToIntersectionPoint_Table on this step's table (HBM
+        # resident), cfg3-distributed queries (cm) for the table's own antenna
+        from tests.parity import cfg3_queries
+        txh, dst, _ = cfg3_queries(args.lookup_n, seed=4242 + rank)
+        src = torch.from_numpy(txh * 100).to(dev)
+        dcm = torch.from_numpy(dst * 100).to(dev)
+        dep = torch.full((args.lookup_n,), depth_cm, dtype=torch.float64, device=dev)
+        lout = torch.empty((9, args.lookup_n), dtype=torch.float64, device=dev)
+        lok = torch.empty(args.lookup_n, dtype=torch.uint8, device=dev)
+        lfl = torch.empty(args.lookup_n, dtype=torch.uint8, device=dev)
+        lt = solver.lookup_table(table, grid)
+
+        def lookup():
+            solver.table_lookup_device(lt, src, dcm, dep, CFG2["ice_cm"], lout, lok, lfl,
+                                       stream=stream)
+
+        lookup()
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        reps = 10
+        e0.record(stream)
+        for _ in range(reps):
+            lookup()
+        e1.record(stream)
+        torch.cuda.synchronize()
+        lms = e0.elapsed_time(e1) / reps
+        extra["table_lookup"] = {
+            "metric": "GetHorizontalDistanceToIntersectionPoint_Table lookups/s (1e6 cfg3 "
+                      "queries on the cfg2 table, incl. the minimizer fallback pass)",
+            "value": args.lookup_n / (lms * 1e-3), "unit": "lookups/s", "ms": lms,
+            "ok_fraction": float(lok.cpu().numpy().mean())}
+    if args.default_grid:
+        # the reference's default grid (10 m x 0.1 deg, 8,730,900 rays): throughput at a size
+        # where launch ramp and tail are amortised
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        gd = make_grid(depth_cm, CFG2["ice_cm"])
+        td = torch.empty((11, gd.n_rays), dtype=torch.float32, device=dev)
+        solver.table_device(gd, td, None, stream=stream)
+        torch.cuda.synchronize()
+        e0.record(stream)
+        for _ in range(5):
+            solver.table_device(gd, td, None, stream=stream)
+        e1.record(stream)
+        torch.cuda.synchronize()
+        dms = e0.elapsed_time(e1) / 5
+        extra["table_default_grid"] = {"rays": gd.n_rays, "ms": dms,
+                                       "value": gd.n_rays / (dms * 1e-3), "unit": "rays/s"}
+        del td
 
     # parity of this step's table vs the CPU path + CPU baseline (rank 0, N=1 only)
     cpu = None
@@ -230,6 +294,7 @@ def main():
             "cpu_baseline": cpu,
             "parity_vs_cpu": parity_rep,
             "minimizer": solve,
+            **extra,
             "work_model": work,
         }
         print(json.dumps(line))

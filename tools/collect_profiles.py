@@ -1,0 +1,50 @@
+"""Copy one GPU session's evidence (tools/gpu_round_profile.sh) from gpurun_out/ into profiles/,
+named per round, and check that rocprofv3's average table_kernel duration agrees with the
+HIP-event kernel time bench.py measured in the same command.
+
+    python tools/collect_profiles.py r01
+"""
+import csv
+import glob
+import json
+import os
+import shutil
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+SRC = os.path.join(ROOT, "gpurun_out")
+DST = os.path.join(ROOT, "profiles")
+
+
+def main():
+    rnd = sys.argv[1] if len(sys.argv) > 1 else "r01"
+    os.makedirs(os.path.join(DST, f"{rnd}_pmc"), exist_ok=True)
+    copies = {
+        "bench.json": f"{rnd}_bench.json",
+        "prof_bench.json": f"{rnd}_bench_under_rocprof.json",
+        "pmc/pmc_summary.json": "pmc_summary.json",
+        "pmc/bench_pmc.json": f"{rnd}_pmc/bench_pmc.json",
+        "pmc/opweights_pmc.json": f"{rnd}_pmc/opweights_pmc.json",
+    }
+    for s, d in copies.items():
+        shutil.copy(os.path.join(SRC, s), os.path.join(DST, d))
+    stats = glob.glob(os.path.join(SRC, "prof", "**", "*kernel_stats.csv"), recursive=True)
+    shutil.copy(stats[0], os.path.join(DST, f"{rnd}_kernel_stats.csv"))
+    with open(stats[0]) as f:
+        rows = list(csv.DictReader(f))
+    with open(os.path.join(SRC, "prof_bench.json")) as f:
+        bench = json.loads(f.read().strip().splitlines()[-1])
+    check = {}
+    for r in rows:
+        if "::table_kernel<" in r["Name"]:
+            check["rocprof_table_kernel_avg_ms"] = float(r["AverageNs"]) / 1e6
+            check["rocprof_table_kernel_calls"] = int(r["Calls"])
+    check["bench_hip_event_kernel_ms"] = bench["roofline"]["kernel_ms"]
+    check["ratio"] = check["rocprof_table_kernel_avg_ms"] / check["bench_hip_event_kernel_ms"]
+    with open(os.path.join(DST, f"{rnd}_timing_check.json"), "w") as f:
+        json.dump(check, f, indent=1)
+    print(json.dumps(check, indent=1))
+
+
+if __name__ == "__main__":
+    main()

@@ -20,4 +20,5 @@ run bench_b "$P2" python $R/bench.py --no-cpu --steps 3 --warmup 1 --solve-steps
 run bench_w "WRITE_SIZE" python $R/bench.py --no-cpu --steps 3 --warmup 1 --solve-steps 1 && \
 run bench_f "FETCH_SIZE" python $R/bench.py --no-cpu --steps 3 --warmup 1 --solve-steps 1 && \
 python $R/tools/pmc_summarize.py $OUT/opweights_pmc.json $OUT/ow_a && \
-python $R/tools/pmc_summarize.py $OUT/bench_pmc.json $OUT/bench_a $OUT/bench_b $OUT/bench_w $OUT/bench_f
+python $R/tools/pmc_summarize.py $OUT/bench_pmc.json $OUT/bench_a $OUT/bench_b $OUT/bench_w $OUT/bench_f && \
+python $R/tools/make_pmc_summary.py $OUT/bench_pmc.json $OUT/pmc_summary.json > /dev/null

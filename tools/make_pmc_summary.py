@@ -11,7 +11,11 @@ import sys
 SIMDS = 256 * 4
 XCDS = 8
 
-units = {"table_kernel": 858627, "solve_kernel<0>": 1000000}
+# kernel-name prefix -> (summary key, units per launch) for `bench.py --no-cpu`
+UNITS = [("table_kernel", "table_kernel", 858627),
+         ("roots_kernel<0>", "roots_kernel", 1000000),
+         ("solve_out_kernel<0>", "solve_out_kernel", 1000000),
+         ("lookup_kernel", "lookup_kernel", 1000000)]
 
 
 def derive(name, c, n_units, kernel_ns=None):
@@ -38,12 +42,13 @@ if __name__ == "__main__":
     src, dst = sys.argv[1], sys.argv[2]
     with open(src) as f:
         raw = json.load(f)
-    out = {"_source": "rocprofv3 --pmc passes of `python bench.py --no-cpu --steps 3` "
-                      "(tools/gpu_pmc.sh), mean per dispatch"}
+    out = {"_source": "rocprofv3 --pmc passes of `python bench.py --no-cpu --steps 3 "
+                      "--warmup 1 --solve-steps 1` (tools/gpu_pmc.sh), mean per dispatch"}
     for k, c in raw.items():
-        if k in units:
-            out[k.replace("<0>", "")] = {**derive(k, c, units[k]),
-                                         "raw": {a: b for a, b in c.items() if not a.startswith("_")}}
+        for prefix, key, n in UNITS:
+            if k.startswith(prefix):
+                out[key] = {**derive(k, c, n), "kernel": k,
+                            "raw": {a: b for a, b in c.items() if not a.startswith("_")}}
     with open(dst, "w") as f:
         json.dump(out, f, indent=1)
     print(json.dumps(out, indent=1)[:3000])

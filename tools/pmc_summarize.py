@@ -14,7 +14,7 @@ from collections import defaultdict
 
 
 def short(name: str) -> str:
-    base = name.split("(")[0]
+    base = name.replace("(anonymous namespace)::", "").split("(")[0]
     base = re.sub(r"<.*>", lambda m: m.group(0), base)
     return base.split("::")[-1].strip()
 

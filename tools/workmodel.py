@@ -1,22 +1,27 @@
-"""Algorithmic FP64 work per table ray (DESIGN.md §5).
+"""Algorithmic FP64 work per table ray (DESIGN.md §5, SURVEY.md §8(d)).
 
 W_ray = sum_f n_f * w_f + n_arith, where n_f counts the UNIQUE transcendental / divide
-evaluations of the CSE'd device code per ray (airice_device.hpp: segment_full, prim_all,
-air_endpoint, fresnel_trans) and w_f is the gfx950 ocml lane-op cost of f
-(tools/opweights.json).  Selects, compares and integer index math are not counted.
+evaluations a table ray needs for its 11 output columns (airice_kernels.hip ray_solution_row,
+airice_device.hpp segment_const), w_f is the gfx950 ocml FP64 instruction cost of f
+(tools/opweights.json, measured with rocprofv3 --pmc) and n_arith the add/mul/fma count.
+Work that depends on the Tx height only (row constants) is amortised over the row's angles;
+per-launch constants (Snell ratios between fixed layer bounds, n_air/n_ice) count zero.
+Selects, compares and integer index math are not counted.
 """
 from __future__ import annotations
 
 import numpy as np
 
-# per air/ice segment (airice_device.hpp segment(), identities (1)-(5)): Snell step 1 div,
-# ray parameter 1 sqrt + 1 div, two ends x (1 sqrt), two log ratios (2 div + 2 log), and
-# ~40 add/mul forming THD, time and geometric path from them
-SEGMENT = {"sqrt": 3, "log": 2, "div": 4, "arith": 40}
-# per ray: Tx endpoint (1 exp + 1 div + 8 products), launch sine, incidence asin, ice-segment
-# Snell ratio and receive asin, Fresnel T_S/T_P (sin, cos, sqrt, 4 div), output scaling
-PER_RAY = {"exp": 1, "sin": 2, "cos": 1, "asin": 2, "sqrt": 1, "div": 6, "arith": 40}
+# per air/ice segment (identities (1)-(5)): sqrt(A^2-L^2) and its reciprocal (1 sqrt + 1 div),
+# the two ends' sqrt(y^2-L^2) (2 sqrt), two log ratios (2 div + 2 log), ~31 add/mul forming
+# the Snell step, L, the log arguments and THD / time / geometric path
+SEGMENT = {"sqrt": 3, "log": 2, "div": 3, "arith": 31}
 PER_SEGMENT_ACC = {"arith": 3}  # THD/time/geo accumulation
+# per ray: launch sine, receive asin in ice, Fresnel T_S / T_P (2 sqrt, 2 div), launch angle
+# and output scaling (the incidence asin is dummy[12], not a table column)
+PER_RAY = {"sin": 1, "asin": 1, "sqrt": 2, "div": 2, "arith": 24}
+# per table row (Tx height): Tx endpoint exp, 1/C and the top segment's Snell ratio, ~20 ops
+PER_ROW = {"exp": 1, "div": 2, "arith": 20}
 
 
 def _layers_m(medium):
@@ -53,9 +58,11 @@ def segments_per_ray(grid, medium=None) -> dict:
     return {"mean_air": float(n_air.mean()), "ice": 1.0 if grid.in_ice else 0.0}
 
 
-def ray_ops(segs: dict, w: dict) -> dict:
+def ray_ops(segs: dict, w: dict, rays_per_row: int = 1) -> dict:
     nseg = segs["mean_air"] + segs["ice"]
     counts = {}
+    for k, v in PER_ROW.items():
+        counts[k] = counts.get(k, 0.0) + v / max(1, rays_per_row)
     for k, v in SEGMENT.items():
         counts[k] = counts.get(k, 0.0) + v * nseg
     for k, v in PER_SEGMENT_ACC.items():
