@@ -31,6 +31,14 @@ namespace airice {
 
 constexpr double kSpeedC = 299792458.0;  // .h:30
 constexpr int kBlock = 256;
+// table launch shape (tuning knobs for tools/ab_table.py builds; the defaults are the measured best)
+#ifndef AIRICE_TABLE_BS
+#define AIRICE_TABLE_BS 256
+#endif
+#ifndef AIRICE_TABLE_WAVES
+#define AIRICE_TABLE_WAVES 8
+#endif
+constexpr int kTableBlock = AIRICE_TABLE_BS;
 
 // ---------------------------------------------------------------------------
 // Forward ray: GetRayTracingSolutions (.cc:1796-2017).  d[] = dummy[0..17].
@@ -120,25 +128,30 @@ __device__ __forceinline__ double sin_start(double x) {
   if (!(x >= 0.0 && x <= 1.5707963267948966)) return sin(x);
   const double x2 = x * x;
   // (-1)^k / (2k+1)!, k = 11 .. 1, as doubles
-  double p = __builtin_fma(x2, -0x1.761b41316381ap-75, 0x1.71b8ef6dcf572p-66);  // 1/23!, 1/21!
-  p = __builtin_fma(x2, p, -0x1.2f49b46814157p-57);                             // 1/19!
-  p = __builtin_fma(x2, p, 0x1.952c77030ad4ap-49);                              // 1/17!
-  p = __builtin_fma(x2, p, -0x1.ae7f3e733b81fp-41);                             // 1/15!
-  p = __builtin_fma(x2, p, 0x1.6124613a86d09p-33);                              // 1/13!
-  p = __builtin_fma(x2, p, -0x1.ae64567f544e4p-26);                             // 1/11!
-  p = __builtin_fma(x2, p, 0x1.71de3a556c734p-19);                              // 1/9!
-  p = __builtin_fma(x2, p, -0x1.a01a01a01a01ap-13);                             // 1/7!
-  p = __builtin_fma(x2, p, 0x1.1111111111111p-7);                               // 1/5!
-  p = __builtin_fma(x2, p, -0x1.5555555555555p-3);                              // 1/3!
+  double p = __builtin_fma(x2, -0x1.761b41316381ap-75, kc(0x1.71b8ef6dcf572p-66));  // 1/23!, 1/21!
+  p = __builtin_fma(x2, p, kc(-0x1.2f49b46814157p-57));                             // 1/19!
+  p = __builtin_fma(x2, p, kc(0x1.952c77030ad4ap-49));                              // 1/17!
+  p = __builtin_fma(x2, p, kc(-0x1.ae7f3e733b81fp-41));                             // 1/15!
+  p = __builtin_fma(x2, p, kc(0x1.6124613a86d09p-33));                              // 1/13!
+  p = __builtin_fma(x2, p, kc(-0x1.ae64567f544e4p-26));                             // 1/11!
+  p = __builtin_fma(x2, p, kc(0x1.71de3a556c734p-19));                              // 1/9!
+  p = __builtin_fma(x2, p, kc(-0x1.a01a01a01a01ap-13));                             // 1/7!
+  p = __builtin_fma(x2, p, kc(0x1.1111111111111p-7));                               // 1/5!
+  p = __builtin_fma(x2, p, kc(-0x1.5555555555555p-3));                              // 1/3!
   return __builtin_fma(x * x2, p, x);
 }
 
 // want_inc: dummy[12] (the incidence angle on the ice, one asin) is not a table column
 // (.cc:2101-2111), so table launches without the double output skip it.
+// top_hi >= 0: a wave-uniform upper bound of the lanes' Tx layers (the table block's first row);
+// the lower layers then run as one loop over a uniform layer index, their SegConst read with
+// scalar loads one layer at a time, instead of one inlined copy per layer.  Same operations in
+// the same order either way.
 __device__ __forceinline__ void ray_solution_row(const DevMedium& M, const IceConsts& I,
                                                  const RowConst& rc, double theta, bool in_ice,
                                                  double* d, bool want_inc,
-                                                 const double* tab = &kLogTable[0][0]) {
+                                                 const double* tab = &kLogTable[0][0],
+                                                 int top_hi = -1) {
   const double H = rc.H;
   const int top = rc.top;
   const int bot = I.bot;
@@ -154,13 +167,25 @@ __device__ __forceinline__ void ray_solution_row(const DevMedium& M, const IceCo
     geo_air += s.geo;
   }
   // lower layers: both ends folded on the host (I.lower, scalar reads)
+  if (top_hi >= 0) {
+#pragma clang loop unroll(disable)
+    for (int il = top_hi - 1; il >= bot; --il) {
+      if (il < top) {
+        const Segment s = segment_const(I.lower[il], M.A_air, A2, sin_asin(v), true, v, tab);
+        thd_air += s.thd;
+        t_air += s.t;
+        geo_air += s.geo;
+      }
+    }
+  } else {
 #pragma unroll
-  for (int il = kMaxLayers - 2; il >= 0; --il) {
-    if (il >= top || il < bot) continue;
-    const Segment s = segment_const(I.lower[il], M.A_air, A2, sin_asin(v), true, v, tab);
-    thd_air += s.thd;
-    t_air += s.t;
-    geo_air += s.geo;
+    for (int il = kMaxLayers - 2; il >= 0; --il) {
+      if (il >= top || il < bot) continue;
+      const Segment s = segment_const(I.lower[il], M.A_air, A2, sin_asin(v), true, v, tab);
+      thd_air += s.thd;
+      t_air += s.t;
+      geo_air += s.geo;
+    }
   }
   // IncidentAngleonIce = last layer's receive angle; 0 when no air layer (.cc:1832, 1881)
   double inc = 0.0;
@@ -246,13 +271,13 @@ __device__ __forceinline__ int ray_row(const TableArgs& G, int k) {
 __device__ __forceinline__ void table_ray(const DevMedium& M, const IceConsts& I,
                                           const TableArgs& G, const RowConst& rc, int r, int k,
                                           float* __restrict__ table, double* __restrict__ full,
-                                          const double* tab) {
+                                          const double* tab, int top_hi) {
   const int iang = k - r * G.asteps;
   // .cc:2085, 2092-2094
   double th = G.start_a + G.step_a * iang;
   if (iang == G.asteps - 1) th = G.stop_a;
   double d[18];
-  ray_solution_row(M, I, rc, th, G.in_ice != 0, d, full != nullptr, tab);
+  ray_solution_row(M, I, rc, th, G.in_ice != 0, d, full != nullptr, tab, top_hi);
   const size_t ld = G.ld;
   // AllTableAllAntData columns (.cc:2101-2111)
   table[0 * ld + k] = (float)d[1];
@@ -281,7 +306,7 @@ __device__ __forceinline__ void table_ray(const DevMedium& M, const IceConsts& I
 template <int BS, bool TRACE = false>
 // waves_per_eu(8): 64 VGPRs (12 B/lane spilled) at 8 waves/SIMD measured on par or slightly
 // ahead of 67 VGPRs at 7 (bench 42.0 vs 42.9 us for cfg2).
-__global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(8, 8))) void table_kernel(
+__global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(AIRICE_TABLE_WAVES, AIRICE_TABLE_WAVES))) void table_kernel(
                                                    DevMedium M, IceConsts I, TableArgs G,
                                                    float* __restrict__ table,
                                                    double* __restrict__ full,
@@ -304,10 +329,14 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(8, 8))) void
   for (int t = threadIdx.x; t < nrows; t += BS)
     rows[t] = row_const(M, I, row_height(G, G.row0 + r0 + t));
   __syncthreads();
+  // the block's first row has the highest Tx, so its Tx layer bounds every lane's (top_layer is
+  // monotone in the height)
+  const int top_hi = __builtin_amdgcn_readfirstlane(rows[0].top);
+  __builtin_assume(top_hi >= 0);
   const int k = k0 + (int)threadIdx.x;
   if (k < G.n) {
     const int r = ray_row(G, k);
-    table_ray(M, I, G, rows[r - r0], r, k, table, full, &s_logtab[0][0]);
+    table_ray(M, I, G, rows[r - r0], r, k, table, full, &s_logtab[0][0], top_hi);
   }
   if (TRACE && lane == 0) {
     trace[wave].t1 = __builtin_amdgcn_s_memrealtime();
@@ -918,11 +947,11 @@ int launch_table(const DevMedium& M, const IceConsts& I, const airice_grid* g, i
   A.ld = ld;
   A.inv_asteps = 1.0 / (double)g->angle_steps;
   // rows a 256-ray block can touch, for the LDS row constants
-  A.rows_per_block = std::min(kBlock, (kBlock - 1) / g->angle_steps + 2);
+  A.rows_per_block = std::min(kTableBlock, (kTableBlock - 1) / g->angle_steps + 2);
   const size_t lds = sizeof(RowConst) * (size_t)A.rows_per_block;
   static const char* trace_path = getenv("AIRICE_TABLE_TRACE");
   // ray indices are 32-bit inside a launch: grids of 2^31 rays or more go in row slabs
-  const int max_rows = (int)std::max<long long>(1, ((1LL << 31) - kBlock) / g->angle_steps);
+  const int max_rows = (int)std::max<long long>(1, ((1LL << 31) - kTableBlock) / g->angle_steps);
   for (int done = 0; done < row_count;) {
     const int rows = std::min(max_rows, row_count - done);
     const size_t off = (size_t)done * (size_t)g->angle_steps;
@@ -930,19 +959,19 @@ int launch_table(const DevMedium& M, const IceConsts& I, const airice_grid* g, i
     A.n = rows * g->angle_steps;
     float* tab = d_table + off;
     double* full = d_full ? d_full + off : nullptr;
-    const unsigned blocks = grid_for(A.n);
+    const unsigned blocks = (unsigned)((A.n + kTableBlock - 1) / kTableBlock);
     done += rows;
     if (trace_path == nullptr) {
-      hipLaunchKernelGGL((table_kernel<kBlock, false>), dim3(blocks), dim3(kBlock), lds, st, M, I,
+      hipLaunchKernelGGL((table_kernel<kTableBlock, false>), dim3(blocks), dim3(kTableBlock), lds, st, M, I,
                          A, tab, full, nullptr);
       if (hipGetLastError() != hipSuccess) return AIRICE_EHIP;
       continue;
     }
     // debug timeline (tools/wave_timeline.py): synchronous, one record per wave appended
-    const long long nw = (long long)blocks * (kBlock / 64);
+    const long long nw = (long long)blocks * (kTableBlock / 64);
     WaveTrace* dtr = nullptr;
     if (hipMalloc(&dtr, sizeof(WaveTrace) * nw) != hipSuccess) return AIRICE_EHIP;
-    hipLaunchKernelGGL((table_kernel<kBlock, true>), dim3(blocks), dim3(kBlock), lds, st, M, I, A,
+    hipLaunchKernelGGL((table_kernel<kTableBlock, true>), dim3(blocks), dim3(kTableBlock), lds, st, M, I, A,
                        tab, full, dtr);
     std::vector<WaveTrace> h(nw);
     if (hipStreamSynchronize(st) != hipSuccess ||

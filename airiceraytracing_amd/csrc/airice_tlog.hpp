@@ -28,6 +28,18 @@
 
 namespace airice {
 
+// A polynomial coefficient held in an SGPR pair: the fma then issues as one VOP3 v_fma_f64 with the
+// scalar operand, instead of two v_mov_b32 materialising the constant for v_fmac_f64 (what the
+// compiler otherwise emits for Horner steps).  Value unchanged.
+#if defined(__HIP_DEVICE_COMPILE__)
+__device__ __forceinline__ double kc(double c) {
+  asm("" : "+s"(c));
+  return c;
+}
+#else
+__host__ __device__ AIRICE_INLINE constexpr double kc(double c) { return c; }
+#endif
+
 __host__ __device__ AIRICE_INLINE uint64_t dbits(double x) {
   uint64_t u;
   std::memcpy(&u, &x, sizeof(u));
@@ -67,11 +79,11 @@ __host__ __device__ AIRICE_INLINE double tlog_pos(double x, const double* tab = 
   const double lo = AIRICE_FMA(kd, Ln2lo, ((w - hi) + r) + we);
   const double r2 = r * r;
   // Horner: one constant per fma (no constant materialised in VGPRs but A5)
-  double q = AIRICE_FMA(r, A5, A4);
-  q = AIRICE_FMA(r, q, A3);
-  q = AIRICE_FMA(r, q, A2);
-  q = AIRICE_FMA(r, q, A1);
-  q = AIRICE_FMA(r, q, A0);
+  double q = AIRICE_FMA(r, A5, kc(A4));
+  q = AIRICE_FMA(r, q, kc(A3));
+  q = AIRICE_FMA(r, q, kc(A2));
+  q = AIRICE_FMA(r, q, kc(A1));
+  q = AIRICE_FMA(r, q, kc(A0));
   return AIRICE_FMA(r2, q, lo) + hi;
 }
 

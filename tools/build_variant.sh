@@ -1,0 +1,10 @@
+#!/bin/bash
+# Build a libairice.so variant for tools/ab_table.py from a csrc directory:
+#   tools/build_variant.sh <csrc_dir> <out.so> [extra hipcc flags...]
+set -e
+SRC=$1; OUT=$2; shift 2
+ROOT=$(cd "$(dirname "$0")/.." && pwd)
+cd "$SRC"
+/opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -ffp-contract=off -fno-fast-math \
+  -Wno-unused-result -I"$ROOT/include" -I. "$@" -shared -o "$OUT" \
+  airice_kernels.hip airice_lookup.hip airice_path.hip airice_runtime.cpp compat_multiray.cpp
