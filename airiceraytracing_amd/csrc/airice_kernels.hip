@@ -505,12 +505,14 @@ __device__ __forceinline__ Geometry shift(double H, double D, double ice, double
 struct SolveResult {
   double root;
   int status;
+  int n_eval, n_est, n_inside;  // evaluations: all, secant search, bisection midpoints (stats)
 };
 
-enum { PH_PROBE = 0, PH_FLO = 1, PH_FHI = 2, PH_BISECT = 3, PH_DONE = 4 };
+enum { PH_PROBE = 0, PH_FLO = 1, PH_FHI = 2, PH_EST = 3, PH_G1 = 4, PH_G2 = 5, PH_BISECT = 6,
+       PH_DONE = 7 };
 
 __device__ __forceinline__ SolveResult solve_root(const DevMedium& M, const IceConsts& I,
-                                                  const Geometry& g, double thR) {
+                                                  const Geometry& g, double thR, bool exact) {
   int status = 0;
   Query q;
   q.depth_pos = g.depth_pos;
@@ -538,6 +540,7 @@ __device__ __forceinline__ SolveResult solve_root(const DevMedium& M, const IceC
   double lo = thR - 16;
   double hi = thR;
   int phase = PH_FLO;
+  bool probe_bad = false;  // the probe ended with lo > hi: the reference then reports root 0
   if (M.const_air) lo = 90;  // pythonwrapper constant air index: [90, thR], no probe (.cc:978-980)
   if (!M.const_air && lo < 90.001) {
     lo = 90.001;
@@ -551,6 +554,21 @@ __device__ __forceinline__ SolveResult solve_root(const DevMedium& M, const IceC
         lo = lo + 0.05;
         status |= AIRICE_SOLVE_PROBED;
       }
+    } else {
+      // no air layer (Tx above the atmosphere, e.g. the table lookup's x100 fallback): THD in
+      // air is 0 at every angle, so the probe only stops at lo > hi - 0.1 -- up to ~300 steps
+      // whose outcome needs no evaluation
+      while (!(lo > hi - 0.1)) {
+        lo = lo + 0.05;
+        status |= AIRICE_SOLVE_PROBED;
+      }
+      if (hi < 90.001 && hi > 90.00) hi = 90.05;
+      phase = PH_FLO;
+      if (lo > hi) {
+        status |= AIRICE_SOLVE_BAD_BRACKET;
+        probe_bad = true;
+        phase = PH_DONE;
+      }
     }
   } else {
     if (hi < 90.001 && hi > 90.00) hi = 90.05;
@@ -559,24 +577,116 @@ __device__ __forceinline__ SolveResult solve_root(const DevMedium& M, const IceC
       phase = PH_DONE;
     }
   }
-  double root = 0.5 * (lo + hi);
-  double f_lower = 0.0, f_upper = 0.0, f_lo_set = 0.0;
+  double root = probe_bad ? 0.0 : 0.5 * (lo + hi);
+  double f_lower = 0.0, f_upper = 0.0;
   const double tol = 0.000000001;
   int iter = 0;
-  while (phase != PH_DONE) {
-    const bool shortcut = phase == PH_BISECT && (f_lower == 0.0 || f_upper == 0.0);
-    const double x = (phase == PH_FHI) ? hi : (phase == PH_BISECT) ? (lo + hi) / 2.0 : lo;
-    double thd_air = 0.0, f = 0.0;
-    if (!shortcut) {  // the single evaluation site: MinimizeforLaunchAngle (.cc:873-917)
-      double L;
-      thd_air = air_thd(M, q, x, L);
-      double thd_ice = 0;
-      if (q.depth_pos != 0) {
-        const RayL RL = ray_L(M.A_ice * M.A_ice, L);
-        thd_ice += delta_D(slim(I.ice0), q.rx, RL);
-      }
-      f = (q.dist - (thd_ice + thd_air));
+  // Sign guards.  f(theta) = D - THD(theta) is monotone in theta wherever it is finite, so
+  // between two exactly evaluated points with the same sign and |f| >= tau (far above the
+  // evaluation's rounding noise) every point has that sign.  gL / gR: the innermost evaluated
+  // points with the sign of f(lo) / f(hi); okL / okR: |f(lo)| / |f(hi)| >= tau, so the guard
+  // regions [lo, gL] / [gR, hi] are safe.  A secant search finds the root, two guard
+  // evaluations straddle it, and the bisection then evaluates f only at midpoints between the
+  // guards: the same midpoints, signs and root as evaluating every one
+  // (tests/test_gpu_bisect_replay.py checks this bit for bit against AIRICE_BISECT_EXACT=1).
+  const double tau = 1e-6 + 1e-10 * fabs(g.D);
+  bool okL = false, okR = false;
+  double gL = 0.0, fL = 0.0, gR = 0.0, fR = 0.0;  // fL holds f(lo) between PH_FLO and PH_FHI
+  // secant search for the root: the first step in u = tan(180 - theta), where THD is close to
+  // linear (a straight ray's is exactly H u; single precision is plenty for a first guess), then
+  // secant steps in theta on the last two points (x1, f1), (x2, f2)
+  double x1 = 0.0, f1 = 0.0, x2 = 0.0, f2 = 0.0;
+  double xg = 0.0, dlt = 0.0;  // PH_G1/G2: guards at xg -/+ dlt
+  int est = 0, n_eval = 0, n_inside = 0;
+  auto guard = [&](double x, double f) {
+    if (!(fabs(f) >= tau) || !(x > gL && x < gR)) return;
+    if ((f < 0.0) == (fL < 0.0)) {
+      gL = x;
+      fL = f;
+    } else {
+      gR = x;
+      fR = f;
     }
+  };
+  // gsl_root_test_interval(lo, hi, 0, 1e-9) and the driver's max_iter (.cc:355-371)
+  auto finish = [&](bool frozen) {
+    bool cont;
+    if (lo > hi) {
+      cont = false;
+    } else {
+      const double min_abs = ((lo > 0.0 && hi > 0.0) || (lo < 0.0 && hi < 0.0))
+                                 ? (fabs(lo) < fabs(hi) ? fabs(lo) : fabs(hi))
+                                 : 0.0;
+      const double tolerance = 0 + tol * min_abs;
+      cont = !(fabs(hi - lo) < tolerance);
+    }
+    if (cont && iter == 40) status |= AIRICE_SOLVE_MAXITER;
+    if (frozen || !cont || iter == 40) phase = PH_DONE;
+  };
+  while (phase != PH_DONE) {
+    if (phase == PH_BISECT) {
+      // steps that need no evaluation: an exact zero at a bracket end (GSL returns that end),
+      // or a midpoint inside a guard region, whose sign is the region's: lo (left) or hi
+      // (right) moves to it, as gsl_root_fsolver_iterate would
+      if (f_lower == 0.0 || f_upper == 0.0) {
+        ++iter;
+        root = (f_lower == 0.0) ? lo : hi;
+        lo = root;
+        hi = root;
+        finish(false);
+        break;  // lo == hi: gsl_root_test_interval converges
+      }
+      if ((okL || okR) && lo > 0.0) {
+        // lean run (0 < lo < hi here): the root GSL reports after a step is 0.5 (lo + hi) of the
+        // new bracket either way; the interval test reduces to hi - lo < tol lo
+        const double gl = okL ? gL : -1.0, gr = okR ? gR : __builtin_inf();
+        const double lo0 = lo, hi0 = hi;
+        bool done = false;
+        for (;;) {
+          const double xm = (lo + hi) / 2.0;
+          if (xm <= gl) lo = xm;
+          else if (xm >= gr) hi = xm;
+          else break;
+          ++iter;
+          const bool cont = !(fabs(hi - lo) < 0 + tol * lo);
+          if (!cont || iter == 40) {
+            if (cont) status |= AIRICE_SOLVE_MAXITER;
+            done = true;
+            break;
+          }
+        }
+        if (lo != lo0) f_lower = fL;
+        if (hi != hi0) f_upper = fR;
+        if (lo != lo0 || hi != hi0) root = 0.5 * (lo + hi);
+        if (done) break;
+      }
+    }
+    double x;
+    if (phase == PH_FHI) {
+      x = hi;
+    } else if (phase == PH_BISECT) {
+      x = (lo + hi) / 2.0;
+    } else if (phase == PH_EST) {
+      x = (est == 0) ? x2 : x2 - f2 * ((x2 - x1) / (f2 - f1));
+      if (!(x > gL && x < gR)) x = 0.5 * (gL + gR);  // safeguard: the guards' midpoint
+    } else if (phase == PH_G1) {
+      x = xg - dlt;
+    } else if (phase == PH_G2) {
+      x = xg + dlt;
+    } else {
+      x = lo;
+    }
+    // the single evaluation site: MinimizeforLaunchAngle (.cc:873-917)
+    ++n_eval;
+    n_inside += (phase == PH_BISECT);
+    double L;
+    const double thd_air = air_thd(M, q, x, L);
+    double thd_ice = 0;
+    if (q.depth_pos != 0) {
+      const RayL RL = ray_L(M.A_ice * M.A_ice, L);
+      thd_ice += delta_D(slim(I.ice0), q.rx, RL);
+    }
+    const double f = (q.dist - (thd_ice + thd_air));
     if (phase == PH_PROBE) {
       if ((!isnan(thd_air) && thd_air > 0) || lo > hi - 0.1) {
         if (hi < 90.001 && hi > 90.00) hi = 90.05;
@@ -596,27 +706,64 @@ __device__ __forceinline__ SolveResult solve_root(const DevMedium& M, const IceC
         status |= AIRICE_SOLVE_NONFINITE_END;
         phase = PH_BISECT;
       } else {
-        f_lo_set = f;
+        fL = f;
         phase = PH_FHI;
       }
     } else if (phase == PH_FHI) {
+      phase = PH_BISECT;
       if (!isfinite(f)) {
         status |= AIRICE_SOLVE_NONFINITE_END;
       } else {
-        f_lower = f_lo_set;
+        f_lower = fL;
         f_upper = f;
+        if (!exact) {
+          gL = lo;
+          gR = hi;
+          fR = f;
+          okL = fabs(fL) >= tau;
+          okR = fabs(fR) >= tau;
+          if (okL && okR) {
+            if ((fL < 0.0) == (fR < 0.0)) {
+              gL = hi;  // no sign change: every midpoint has the ends' sign
+            } else {
+              const float ul = __tanf((float)((180 - lo) * M.d2r));
+              const float uh = __tanf((float)((180 - hi) * M.d2r));
+              const float un = uh - (float)fR * ((uh - ul) / (float)(fR - fL));
+              x1 = hi;
+              f1 = fR;
+              x2 = 180 - (double)atanf(un) * M.r2d;  // first guess, evaluated first
+              phase = PH_EST;
+            }
+          }
+        }
       }
-      phase = PH_BISECT;
-    } else {  // PH_BISECT: one gsl_root_fsolver_iterate + gsl_root_test_interval
+    } else if (phase == PH_EST) {
+      if (est > 0) {
+        x1 = x2;
+        f1 = f2;
+      }
+      x2 = x;
+      f2 = f;
+      ++est;
+      if (!isfinite(f)) {
+        phase = PH_BISECT;
+      } else if (fabs(f) < tau) {
+        // at the root: guards a few tau either side, scaled by the local secant slope
+        dlt = 4.0 * tau * fabs((x2 - x1) / (f2 - f1));
+        xg = x;
+        phase = (dlt > 0.0 && dlt < (gR - gL)) ? PH_G1 : PH_BISECT;
+      } else {
+        guard(x, f);
+        if (est >= 12) phase = PH_BISECT;
+      }
+    } else if (phase == PH_G1 || phase == PH_G2) {
+      if (isfinite(f)) guard(x, f);
+      phase = (phase == PH_G1) ? PH_G2 : PH_BISECT;
+    } else {  // PH_BISECT: gsl_root_fsolver_iterate at a midpoint between the guards
+      if (!exact && isfinite(f)) guard(x, f);
       ++iter;
       bool frozen = false;
-      if (f_lower == 0.0) {
-        root = lo;
-        hi = lo;
-      } else if (f_upper == 0.0) {
-        root = hi;
-        lo = hi;
-      } else if (!isfinite(f)) {
+      if (!isfinite(f)) {
         // EBADFUNC leaves the state unchanged: every later iterate repeats this one, so the
         // driver ends at max_iter with the same root.
         status |= AIRICE_SOLVE_STALE_MID | AIRICE_SOLVE_MAXITER;
@@ -634,21 +781,10 @@ __device__ __forceinline__ SolveResult solve_root(const DevMedium& M, const IceC
         lo = x;
         f_lower = f;
       }
-      bool cont;
-      if (lo > hi) {
-        cont = false;
-      } else {
-        const double min_abs = ((lo > 0.0 && hi > 0.0) || (lo < 0.0 && hi < 0.0))
-                                   ? (fabs(lo) < fabs(hi) ? fabs(lo) : fabs(hi))
-                                   : 0.0;
-        const double tolerance = 0 + tol * min_abs;
-        cont = !(fabs(hi - lo) < tolerance);
-      }
-      if (cont && iter == 40) status |= AIRICE_SOLVE_MAXITER;
-      if (frozen || !cont || iter == 40) phase = PH_DONE;
+      finish(frozen);
     }
   }
-  return SolveResult{root, status};
+  return SolveResult{root, status, n_eval, est, n_inside};
 }
 
 struct Solved {
@@ -767,19 +903,33 @@ struct Park {
   double* root;
   double* status;
   long long stride;
+  int exact;  // 1: evaluate every bisection midpoint (AIRICE_BISECT_EXACT, validation only)
+  int* stats; // debug (AIRICE_SOLVE_STATS): per query {evaluations, secant search, midpoints}
 };
 
+// Debug/validation switch: AIRICE_BISECT_EXACT=1 makes the root finder evaluate f at every
+// bisection midpoint instead of predicting the signs the guards determine (same roots).
+static inline int bisect_exact() {
+  const char* e = getenv("AIRICE_BISECT_EXACT");
+  return (e != nullptr && e[0] == '1') ? 1 : 0;
+}
+
 template <int IN>
-__global__ __launch_bounds__(kBlock, 4) void roots_kernel(DevMedium M, IceConsts I, QueryArgs Q,
+__global__ __launch_bounds__(kBlock, 3) void roots_kernel(DevMedium M, IceConsts I, QueryArgs Q,
                                                        Park park) {
   const long long k = (long long)blockIdx.x * kBlock + threadIdx.x;
   if (k >= Q.n) return;
   if (IN == IN_CM100 && !(Q.mask[k] & AIRICE_LOOKUP_FALLBACK)) return;
   double thR;
   const Geometry g = load_query<IN>(M, Q, k, thR);
-  const SolveResult r = solve_root(M, I, g, thR);
+  const SolveResult r = solve_root(M, I, g, thR, park.exact != 0);
   park.root[k * park.stride] = r.root;
   park.status[k * park.stride] = (double)r.status;
+  if (park.stats != nullptr) {
+    park.stats[3 * k] = r.n_eval;
+    park.stats[3 * k + 1] = r.n_est;
+    park.stats[3 * k + 2] = r.n_inside;
+  }
 }
 
 __device__ __forceinline__ bool check_solution(double thd, double D) {
@@ -999,9 +1149,23 @@ int launch_solve(const DevMedium& M, const IceConsts& I, int variant, const doub
                  double* out, size_t ld, uint8_t* status, hipStream_t st) {
   if (n == 0) return AIRICE_OK;
   const QueryArgs Q{txh, dist, depth, thr, I.ice_h, (long long)n};
-  const Park park{out + 10 * ld, out, 1};
+  Park park{out + 10 * ld, out, 1, bisect_exact(), nullptr};
+  static const char* stats_path = getenv("AIRICE_SOLVE_STATS");
+  if (stats_path != nullptr && hipMalloc(&park.stats, sizeof(int) * 3 * n) != hipSuccess)
+    return AIRICE_EHIP;
   const dim3 grid(grid_for((long long)n)), block(kBlock);
   hipLaunchKernelGGL(roots_kernel<IN_M>, grid, block, 0, st, M, I, Q, park);
+  if (park.stats != nullptr) {  // debug: append the per-query counts (synchronous)
+    std::vector<int> h(3 * n);
+    if (hipStreamSynchronize(st) != hipSuccess ||
+        hipMemcpy(h.data(), park.stats, sizeof(int) * 3 * n, hipMemcpyDeviceToHost) != hipSuccess)
+      return AIRICE_EHIP;
+    (void)hipFree(park.stats);
+    if (FILE* f = fopen(stats_path, "ab")) {
+      fwrite(h.data(), sizeof(int), 3 * n, f);
+      fclose(f);
+    }
+  }
   if (variant == AIRICE_VARIANT_MULTIRAY)
     hipLaunchKernelGGL(solve_out_kernel<AIRICE_VARIANT_MULTIRAY>, grid, block, 0, st, M, I, Q, out,
                        ld, status);
@@ -1016,7 +1180,7 @@ int launch_hdtip(const DevMedium& M, const IceConsts& I, const double* src, cons
                  uint8_t* ok, hipStream_t st) {
   if (n == 0) return AIRICE_OK;
   const QueryArgs Q{src, dist, depth, nullptr, ice_cm, (long long)n};
-  const Park park{out + 4 * ld, out, 1};
+  const Park park{out + 4 * ld, out, 1, bisect_exact(), nullptr};
   const dim3 grid(grid_for((long long)n)), block(kBlock);
   hipLaunchKernelGGL(roots_kernel<IN_CM>, grid, block, 0, st, M, I, Q, park);
   hipLaunchKernelGGL(hdtip_out_kernel, grid, block, 0, st, M, I, Q, out, ld, ok);
@@ -1031,7 +1195,7 @@ int launch_lookup_fallback(const DevMedium& M, const IceConsts& I, const double*
   // .cc:1309 turns IceLayerHeight into metres; .cc:1419 passes IceLayerHeight*100
   const double ice_arg = (ice_cm / 100) * 100;
   const QueryArgs Q{src, dist, depth, nullptr, ice_arg, (long long)n, flags};
-  const Park park{out + 4 * ld, out, 1};
+  const Park park{out + 4 * ld, out, 1, bisect_exact(), nullptr};
   const dim3 grid(grid_for((long long)n)), block(kBlock);
   hipLaunchKernelGGL(roots_kernel<IN_CM100>, grid, block, 0, st, M, I, Q, park);
   hipLaunchKernelGGL(lookup_fallback_out_kernel, grid, block, 0, st, M, I, Q, out, ld, ok);
@@ -1042,7 +1206,7 @@ int launch_trace(const DevMedium& M, const IceConsts& I, const double* depth, co
                  const double* txh, const double* dist, size_t n, double* out10, hipStream_t st) {
   if (n == 0) return AIRICE_OK;
   const QueryArgs Q{depth, ice, txh, dist, 0.0, (long long)n};
-  const Park park{out10 + 5, out10 + 9, 10};
+  const Park park{out10 + 5, out10 + 9, 10, bisect_exact(), nullptr};
   const dim3 grid(grid_for((long long)n)), block(kBlock);
   hipLaunchKernelGGL(roots_kernel<IN_TRACE>, grid, block, 0, st, M, I, Q, park);
   hipLaunchKernelGGL(trace_out_kernel, grid, block, 0, st, M, I, Q, out10);

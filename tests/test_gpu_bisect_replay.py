@@ -1,0 +1,90 @@
+"""The root finder's guarded bisection (evaluating f only at midpoints between the sign guards)
+must reproduce GSL bisection with f evaluated at every midpoint, bit for bit: same roots, same
+status bits, same outputs.  AIRICE_BISECT_EXACT=1 selects the every-midpoint form on the same
+device f, so the comparison isolates the sign prediction from the evaluation's rounding."""
+import os
+
+import numpy as np
+import pytest
+
+from tests import parity
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def solvers():
+    from airiceraytracing_amd import AirIceSolver, VARIANT_MULTIRAY, VARIANT_PYWRAPPER
+    return AirIceSolver(variant=VARIANT_MULTIRAY), AirIceSolver(variant=VARIANT_PYWRAPPER)
+
+
+def _both(fn):
+    old = os.environ.pop("AIRICE_BISECT_EXACT", None)
+    try:
+        fast = fn()
+        os.environ["AIRICE_BISECT_EXACT"] = "1"
+        exact = fn()
+    finally:
+        os.environ.pop("AIRICE_BISECT_EXACT", None)
+        if old is not None:
+            os.environ["AIRICE_BISECT_EXACT"] = old
+    return fast, exact
+
+
+def _same(a, b):
+    a = np.asarray(a)
+    b = np.asarray(b)
+    assert a.shape == b.shape
+    same = (a == b) | (np.isnan(a) & np.isnan(b))
+    bad = np.argwhere(~same)
+    assert bad.size == 0, f"{bad.shape[0]} differing entries, first {bad[:5].tolist()}"
+
+
+def test_replay_cfg3(solvers):
+    s, _ = solvers
+    txh, dist, depth = parity.cfg3_queries(200000, seed=99)
+    (out_f, st_f), (out_e, st_e) = _both(lambda: s.solve_host(txh, dist, depth, 3000.0))
+    _same(st_f, st_e)
+    _same(out_f, out_e)
+
+
+def test_replay_wide_ranges(solvers):
+    """Far distances (no straddle, root outside the bracket), Rx in air, tiny D, grazing Tx."""
+    s, _ = solvers
+    rng = np.random.default_rng(7)
+    n = 100000
+    txh = np.concatenate([rng.uniform(3001, 100000, n // 2), rng.uniform(3000.5, 3300, n // 2)])
+    dist = np.concatenate([rng.uniform(0, 300000, n // 2), rng.uniform(0, 5, n // 2)])
+    depth = np.concatenate([-rng.uniform(0, 300, n // 2), rng.uniform(-5, 500, n // 2)])
+    (out_f, st_f), (out_e, st_e) = _both(lambda: s.solve_host(txh, dist, depth, 3000.0))
+    _same(st_f, st_e)
+    _same(out_f, out_e)
+
+
+def test_replay_pywrapper_trace(solvers):
+    _, sp = solvers
+    depth, ice, txh, dist = parity.cfg5_queries(100000, seed=5)
+    fast, exact = _both(lambda: sp.trace_ice_to_air_host(depth, ice, txh, dist))
+    _same(fast, exact)
+
+
+def test_replay_hdtip_cm(solvers):
+    import torch
+    s, _ = solvers
+    rng = np.random.default_rng(11)
+    n = 50000
+    src = rng.uniform(300100, 1e7, n)
+    dist = rng.uniform(0, 5e6, n)
+    dep = -rng.uniform(0, 30000, n)
+    dev = torch.device("cuda:0")
+
+    def run():
+        t = [torch.from_numpy(a).to(dev) for a in (src, dist, dep)]
+        out = torch.empty((9, n), dtype=torch.float64, device=dev)
+        ok = torch.empty(n, dtype=torch.uint8, device=dev)
+        s.hdtip_device(t[0], t[1], t[2], 300000.0, out, ok, stream=torch.cuda.current_stream())
+        torch.cuda.synchronize()
+        return np.concatenate([out.cpu().numpy(), ok.cpu().numpy()[None].astype(np.float64)])
+
+    fast, exact = _both(run)
+    _same(fast, exact)

@@ -209,3 +209,21 @@ def test_pywrapper_constant_air_index(oracle_medium_py):
     rep = parity.compare_columns(out, ref, parity.PYSOLVE_FLOORS)
     _report("py-const-index", rep)
     assert rep["ok"], rep
+
+
+def test_solve_no_air_layer(solver, oracle_medium):
+    """Tx above the atmosphere (no air layer: the table lookup's x100 fallback lands here): the
+    probe loop's outcome is replayed without evaluations on the GPU; status bits and every
+    output must equal the oracle's evaluated probe (under its zeroed-state model)."""
+    rng = np.random.default_rng(21)
+    n = 3000
+    txh = rng.uniform(1.001e5, 1e7, n)
+    dist = np.concatenate([rng.uniform(0, 5e6, n // 2), rng.uniform(1e6, 5e7, n - n // 2)])
+    depth = np.concatenate([-rng.uniform(0, 300, n // 2), rng.uniform(0, 300, n - n // 2)])
+    out, st = solver.solve_host(txh, dist, depth, 3000.0)
+    ref, rst = oracle.solve_batch(oracle_medium, txh, dist, depth, 3000.0)
+    assert np.array_equal(st.astype(np.int64), rst)
+    assert np.any(rst & oracle.SOLVE_PROBED)
+    rep = parity.compare_columns(out, ref, parity.SOLVE_FLOORS)
+    _report("solve-no-air", rep)
+    assert rep["ok"], rep
