@@ -45,6 +45,7 @@ def parse():
     p.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     p.add_argument("--no-solve", action="store_true", help="skip the minimizer line item")
     p.add_argument("--no-lookup", action="store_true", help="skip the table-lookup line item")
+    p.add_argument("--no-pcie", action="store_true", help="skip the table-to-host line item")
     p.add_argument("--default-grid", action="store_true",
                    help="also time the reference default grid (8.7M rays; off by default so "
                         "every table_kernel launch of the run is the cfg2 workload)")
@@ -210,6 +211,31 @@ def main():
                       "queries on the cfg2 table, incl. the minimizer fallback pass)",
             "value": args.lookup_n / (lms * 1e-3), "unit": "lookups/s", "ms": lms,
             "ok_fraction": float(lok.cpu().numpy().mean())}
+    if not args.no_pcie:
+        # host-buffer callers (AllTableAllAntData is host memory): table build + D2H copy of the
+        # 11 float columns into pinned memory, in stream order; never the headline value
+        host = torch.empty((11, n), dtype=torch.float32, pin_memory=True)
+        e0, e1, e2 = (torch.cuda.Event(enable_timing=True) for _ in range(3))
+        reps = 10
+        step()
+        host.copy_(table, non_blocking=True)
+        torch.cuda.synchronize()
+        e0.record(stream)
+        for _ in range(reps):
+            step()
+            host.copy_(table, non_blocking=True)
+        e1.record(stream)
+        for _ in range(reps):
+            host.copy_(table, non_blocking=True)
+        e2.record(stream)
+        torch.cuda.synchronize()
+        pms = e0.elapsed_time(e1) / reps
+        cms = e1.elapsed_time(e2) / reps
+        extra["table_to_host"] = {
+            "metric": "cfg2 table build + D2H copy to pinned host memory (PCIe-inclusive rays/s)",
+            "value": n / (pms * 1e-3), "unit": "rays/s", "ms": pms, "d2h_ms": cms,
+            "d2h_GBps": 44 * n / (cms * 1e-3) / 1e9}
+        del host
     if args.default_grid:
         # the reference's default grid (10 m x 0.1 deg, 8,730,900 rays): throughput at a size
         # where launch ramp and tail are amortised
