@@ -51,6 +51,8 @@ def parse():
                         "every table_kernel launch of the run is the cfg2 workload)")
     p.add_argument("--lookup-n", type=int, default=1_000_000)
     p.add_argument("--cpu-threads", type=int, default=16)
+    p.add_argument("--cpu-seconds", type=float, default=10.0,
+                   help="wall time of the CPU-baseline sample (whole cfg2 grids)")
     return p.parse_args()
 
 
@@ -265,20 +267,32 @@ def main():
         og = oracle.grid_init(depth_cm, CFG2["ice_cm"], CFG2["height_step"], CFG2["start_angle"],
                               CFG2["stop_angle"], CFG2["angle_step"])
         nthr = max(1, min(args.cpu_threads, os.cpu_count() or 1))
+        # bounded sample: whole cfg2 grids, repeated until >= cpu_seconds of wall time
         c0 = time.perf_counter()
-        ot = oracle.table_rows(om, og, 0, og.height_steps, nthreads=nthr)
-        cdt = time.perf_counter() - c0
-        # 1-thread rate on a strided sample of rows
+        grids = 0
+        while True:
+            ot = oracle.table_rows(om, og, 0, og.height_steps, nthreads=nthr)
+            grids += 1
+            cdt = time.perf_counter() - c0
+            if cdt >= args.cpu_seconds or grids >= 2000:
+                break
+        # 1-thread rate on strided rows, repeated until >= cpu_seconds / 4
         rows1 = list(range(0, og.height_steps, 97))
         c1 = time.perf_counter()
-        for r in rows1:
-            oracle.table_rows(om, og, r, r + 1)
-        c1dt = time.perf_counter() - c1
-        cpu = {"value": og.height_steps * og.angle_steps / cdt, "unit": "rays/s", "cores": nthr,
-               "kind": "port",
-               "sample": f"full cfg2 grid ({og.height_steps * og.angle_steps} rays), oracle C "
-                         f"restatement, OpenMP {nthr} threads, gcc -O2; 1-thread "
-                         f"{len(rows1) * og.angle_steps / c1dt:.3e} rays/s on {len(rows1)} rows",
+        passes = 0
+        while True:
+            for r in rows1:
+                oracle.table_rows(om, og, r, r + 1)
+            passes += 1
+            c1dt = time.perf_counter() - c1
+            if c1dt >= args.cpu_seconds / 4:
+                break
+        cpu = {"value": grids * og.height_steps * og.angle_steps / cdt, "unit": "rays/s",
+               "cores": nthr, "kind": "port",
+               "sample": f"{grids} x the full cfg2 grid ({og.height_steps * og.angle_steps} rays "
+                         f"each) in {cdt:.1f} s, oracle C restatement, OpenMP {nthr} threads, "
+                         f"gcc -O2; 1-thread {passes * len(rows1) * og.angle_steps / c1dt:.3e} "
+                         f"rays/s ({passes} x {len(rows1)} strided rows in {c1dt:.1f} s)",
                "seconds": cdt}
         gt = table.cpu().numpy()
         ulps = parity.float_ulp_diff(gt, ot)
