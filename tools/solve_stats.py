@@ -73,6 +73,20 @@ def main():
         hist = np.bincount(ev, minlength=45)
         print("  evals histogram: " + " ".join(f"{i}:{c}" for i, c in enumerate(hist) if c),
               flush=True)
+        if mode == "fast":
+            eh = np.bincount(est)
+            print("  secant histogram: " + " ".join(f"{i}:{c}" for i, c in enumerate(eh) if c))
+            from tests import parity
+            txh, dist, depth = parity.cfg3_queries(n)
+            np.savez_compressed(os.path.join(ROOT, "gpurun_out", "solve_counts.npz"),
+                                ev=ev.astype(np.int8), est=est.astype(np.int8),
+                                ins=ins.astype(np.int8))
+            for lo_, hi_ in ((0, 7), (7, 10), (10, 13), (13, 99)):
+                m_ = (ev >= lo_) & (ev < hi_)
+                if m_.any():
+                    print(f"  evals [{lo_},{hi_}): n={m_.sum()} txh med {np.median(txh[m_]):.0f} "
+                          f"dist med {np.median(dist[m_]):.0f} D/(H-3000) med "
+                          f"{np.median(dist[m_] / (txh[m_] - 3000)):.3f}", flush=True)
 
 
 if __name__ == "__main__":
