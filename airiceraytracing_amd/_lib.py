@@ -115,13 +115,17 @@ LOOKUP_FALLBACK = 1  # AIRICE_LOOKUP_FALLBACK
 LOOKUP_UNPINNED = 2  # AIRICE_LOOKUP_UNPINNED
 
 # Every symbol include/airice.h declares (checked by tests/test_capi.py).
+# RayTracingFunctions:: scalar ops (include/airice.h AIRICE_RTF_*)
+RTF_HIT_POINT, RTF_OPTICAL_PATH, RTF_PROPAGATION_TIME, RTF_AIR_PROPAGATION = 0, 1, 2, 3
+RTF_ICE_PROPAGATION, RTF_FDNFR, RTF_FTIMED, RTF_MIN_LAUNCH = 4, 5, 6, 7
+
 EXPORTED_SYMBOLS = (
     "airice_last_error", "airice_version", "airice_atmosphere_load", "airice_atmosphere_parse",
     "airice_nz_air", "airice_nz_ice", "airice_grid_init", "airice_table_launch",
     "airice_table_host", "airice_rays_launch", "airice_solve_launch", "airice_solve_host",
     "airice_hdtip_launch", "airice_table_lookup_launch", "airice_single_ray_plan",
-    "airice_single_ray_launch", "airice_single_ray_host", "airice_trace_ice_to_air_launch", "airice_trace_ice_to_air_host",
-    "Py_TraceIceToAir", "airice_device_count", "airice_set_device", "airice_malloc",
+    "airice_single_ray_launch", "airice_single_ray_host", "airice_trace_ice_to_air_launch",
+    "airice_trace_ice_to_air_host", "airice_rtf_outputs", "airice_rtf_eval", "Py_TraceIceToAir", "airice_device_count", "airice_set_device", "airice_malloc",
     "airice_free", "airice_memcpy_h2d", "airice_memcpy_d2h", "airice_synchronize",
 )
 
@@ -179,6 +183,8 @@ def lib() -> ctypes.CDLL:
         "airice_single_ray_plan": ([M, D, D, D, D, ctypes.POINTER(SingleRayInfo)], I),
         "airice_single_ray_launch": ([M, D, D, D, D, P, P, P, S, P], I),
         "airice_single_ray_host": ([M, D, D, D, D, P, P, P, S], I),
+        "airice_rtf_outputs": ([I, I], I),
+        "airice_rtf_eval": ([M, I, P, S, P, S], I),
         "airice_trace_ice_to_air_launch": ([M, P, P, P, P, S, P, P], I),
         "airice_trace_ice_to_air_host": ([M, P, P, P, P, S, P], I),
         "Py_TraceIceToAir": ([D, D, D, D, ctypes.POINTER(D)], None),

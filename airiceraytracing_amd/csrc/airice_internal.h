@@ -41,6 +41,10 @@ int plan_single_ray(const airice_medium* m, double depth, double launch, double 
 int launch_single_ray(const DevMedium& M, const airice_medium* m, double depth, double launch,
                       double txh, double ice, double* d_work, double* d_x, double* d_z,
                       size_t cap, hipStream_t st);
+// RayTracingFunctions:: scalar layer (airice_rtf.hip): one call, one lane, d_out >= outputs
+int rtf_outputs(int op, int max_layers);
+int launch_rtf(const DevMedium& M, int op, const double* args, size_t n_args, double* d_out,
+               hipStream_t st);
 int launch_trace(const DevMedium& M, const IceConsts& I, const double* depth, const double* ice,
                  const double* txh, const double* dist, size_t n, double* out10, hipStream_t st);
 

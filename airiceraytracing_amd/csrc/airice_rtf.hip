@@ -1,0 +1,263 @@
+// airice_rtf.hip -- the RayTracingFunctions:: layer of the reference (RayTracingFunctions.cc, the
+// library behind the cfg1 CLI) on gfx950: GetLayerHitPointPar, GetRayOpticalPath,
+// GetRayPropagationTime, GetAirPropagationPar, GetIcePropagationPar, fDnfR, ftimeD and
+// MinimizeforLaunchAngle, evaluated on the device with the reference's own expressions (these
+// are the per-call scalar entry points of a drop-in, not a batch path: one lane per call;
+// batches go through the table / solve / single-ray kernels).
+//
+// Differences from MultiRayAirIceRefraction's forms: 4-wide outputs {THD, receive angle (deg), L,
+// time (s)} (no geometric path), GetAirPropagationPar's count at [4*MaxLayers]
+// (RayTracingFunctions.cc:529-659), and GetIcePropagationPar without the transition branch.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdint>
+
+#include "airice.h"
+#include "airice_internal.h"
+
+namespace airice {
+
+namespace {
+
+constexpr double kSpeedC = 299792458.0;  // RayTracingFunctions.h spedc
+
+// GetB_air / GetC_air layer scan (RayTracingFunctions.cc:172-213)
+__device__ int rtf_layer(const DevMedium& M, double z) {
+  const double zabs = fabs(z);
+  int which = 0;
+  for (int il = 0; il < M.ml - 1; il++) {
+    if (zabs < M.atm[il + 1] && zabs >= M.atm[il]) {
+      which = il;
+      break;
+    }
+  }
+  if (zabs >= M.atm[M.ml - 1]) which = M.ml - 1;
+  return which;
+}
+__device__ double rtf_B_air(const DevMedium& M, double z) { return M.B[rtf_layer(M, z)]; }
+__device__ double rtf_C_air(const DevMedium& M, double z) { return -M.negC[rtf_layer(M, z)]; }
+// Getnz_air (.cc:215-220), Getnz_ice (.cc:144-147)
+__device__ double rtf_nz_air(const DevMedium& M, double z) {
+  const double zabs = fabs(z);
+  return M.A_air + rtf_B_air(M, zabs) * exp(-rtf_C_air(M, zabs) * zabs);
+}
+__device__ double rtf_nz_ice(const DevMedium& M, double z) {
+  z = fabs(z);
+  return M.A_ice + M.B_ice * exp(M.negC_ice * z);
+}
+__device__ double rtf_B(const DevMedium& M, double z, int air) { return air ? rtf_B_air(M, z) : M.B_ice; }
+__device__ double rtf_C(const DevMedium& M, double z, int air) {
+  return air ? rtf_C_air(M, z) : -M.negC_ice;
+}
+__device__ double rtf_nz(const DevMedium& M, double z, int air) {
+  return air ? rtf_nz_air(M, z) : rtf_nz_ice(M, z);
+}
+
+// fDnfR (.cc:293-303)
+__device__ double rtf_fDnfR(double x, double A, double B, double C, double L) {
+  const double y = A + B * exp(C * x);
+  return (L / C) * (1.0 / sqrt(A * A - L * L)) *
+         (C * x - log(A * (A + B * exp(C * x)) - L * L + sqrt(A * A - L * L) * sqrt(y * y - L * L)));
+}
+
+// ftimeD (.cc:328-347); B is not used by the reference's formula
+__device__ double rtf_ftimeD(const DevMedium& M, double x, double A, double C, double Speedc,
+                             double L, int air) {
+  const double n = rtf_nz(M, x, air);
+  const double n2 = n * n;  // pow(Getnz(x), 2)
+  return (1.0 / (Speedc * C * sqrt(n2 - L * L))) *
+         (n2 - L * L +
+          (C * x - log(A * n - L * L + sqrt(A * A - L * L) * sqrt(n2 - L * L))) *
+              (A * A * sqrt(n2 - L * L)) / sqrt(A * A - L * L) +
+          A * sqrt(n2 - L * L) * log(n + sqrt(n2 - L * L)));
+}
+
+// GetRayOpticalPath (.cc:349-369): the horizontal distance between two heights
+__device__ double rtf_optical_path(const DevMedium& M, double A, double Rx, double Tx, double L,
+                                   int air) {
+  double x1 = +rtf_fDnfR(Rx, A, rtf_B(M, Rx, air), -rtf_C(M, Rx, air), L) -
+              rtf_fDnfR(Tx, A, rtf_B(M, Tx, air), -rtf_C(M, Tx, air), L);
+  if (air) x1 *= -1;
+  return x1;
+}
+
+// GetRayPropagationTime (.cc:371-397)
+__device__ double rtf_prop_time(const DevMedium& M, double A, double Rx, double Tx, double L,
+                                int air) {
+  double t = +rtf_ftimeD(M, Rx, A, -rtf_C(M, Rx, air), kSpeedC, L, air) -
+             rtf_ftimeD(M, Tx, A, -rtf_C(M, Tx, air), kSpeedC, L, air);
+  if (air) t *= -1;
+  return t;
+}
+
+// GetLayerHitPointPar (.cc:399-527): {x1, ReceiveAngle (deg), L, time}
+__device__ void rtf_hit_point(const DevMedium& M, double n_layer1, double Rx, double Tx,
+                              double IncidentAng, int air, double out[4]) {
+  const double SurfaceRayIncidentAngle = IncidentAng * M.d2r;
+  const double A = air ? M.A_air : M.A_ice;
+  const double nzRx = rtf_nz(M, Rx, air);
+  const double nzTx = rtf_nz(M, Tx, air);
+  const double Lang = asin((n_layer1 / nzTx) * sin(SurfaceRayIncidentAngle));
+  const double ReceiveAngle = asin((rtf_nz(M, Tx, air) * sin(Lang)) / rtf_nz(M, Rx, air));
+  const double Lvalue = nzRx * sin(ReceiveAngle);
+  out[0] = rtf_optical_path(M, A, Rx, Tx, Lvalue, air);
+  out[1] = ReceiveAngle * M.r2d;
+  out[2] = Lvalue;
+  out[3] = rtf_prop_time(M, A, Rx, Tx, Lvalue, air);
+}
+
+// Layer-skip scans of GetAirPropagationPar (.cc:531-559)
+__device__ int rtf_skip_above(const DevMedium& M, double txh) {
+  int skip = 0;
+  for (int il = M.ml; il > -1; il--) {
+    // ATMLAY[il-1] is read only when txh < ATMLAY[il]/100 (at il = 0 that is txh < 0)
+    if (txh < M.atm[il] && (il >= 1 ? txh >= M.atm[il - 1] : false)) il = -100;
+    if (il > -1) skip++;
+  }
+  return skip;
+}
+__device__ int rtf_skip_below(const DevMedium& M, double ice) {
+  int skip = 0;
+  for (int il = 0; il < M.ml; il++) {
+    if (ice >= M.atm[il] && ice < M.atm[il + 1]) il = 100;
+    if (il < M.ml) skip++;
+  }
+  return skip;
+}
+
+// GetAirPropagationPar (.cc:529-659): out[4*MaxLayers + 1], per layer {THD, Recv, L, t}, count
+// at [4*MaxLayers]
+__device__ int rtf_air_prop(const DevMedium& M, double LaunchAngleAir, double AirTxHeight,
+                            double IceLayerHeight, double* out) {
+  const int SkipLayersAbove = rtf_skip_above(M, AirTxHeight);
+  const int SkipLayersBelow = rtf_skip_below(M, IceLayerHeight);
+  const int top = M.ml - SkipLayersAbove - 1;
+  double StartAngle = 0, StartHeight = 0, Start_nh = 0, StopHeight = 0, L0 = 0;
+  int nf = 0;
+  for (int il = top; il > SkipLayersBelow - 1; il--) {
+    StartHeight = (il == top) ? AirTxHeight : M.atm[il + 1] - 0.00001;
+    Start_nh = rtf_nz_air(M, StartHeight);
+    StopHeight = (il == (SkipLayersBelow - 1) + 1) ? IceLayerHeight : M.atm[il];
+    if (il == top) {
+      StartAngle = 180 - LaunchAngleAir;
+      double hp[4];
+      rtf_hit_point(M, Start_nh, StopHeight, StartHeight, StartAngle, 1, hp);
+      for (int j = 0; j < 4; j++) out[4 * nf + j] = hp[j];
+      L0 = hp[2];
+      StartAngle = hp[1];
+    } else {
+      const double nzStopHeight = rtf_nz_air(M, StopHeight);
+      const double RecAng = asin(L0 / nzStopHeight) * M.r2d;
+      out[4 * nf + 0] = rtf_optical_path(M, M.A_air, StopHeight, StartHeight, L0, 1);
+      out[4 * nf + 1] = RecAng;
+      out[4 * nf + 2] = L0;
+      out[4 * nf + 3] = rtf_prop_time(M, M.A_air, StopHeight, StartHeight, L0, 1);
+      StartAngle = RecAng;
+    }
+    nf++;
+  }
+  out[4 * M.ml] = nf;
+  return nf;
+}
+
+// GetIcePropagationPar (.cc:661-681)
+__device__ void rtf_ice_prop(const DevMedium& M, double AntennaDepth, double Lvalue,
+                             double out[4]) {
+  const double nzStopDepth = rtf_nz_ice(M, AntennaDepth);
+  out[0] = rtf_optical_path(M, M.A_ice, AntennaDepth, 0.0, Lvalue, 0);
+  out[1] = asin(Lvalue / nzStopDepth) * M.r2d;
+  out[2] = Lvalue;
+  out[3] = rtf_prop_time(M, M.A_ice, AntennaDepth, 0.0, Lvalue, 0);
+}
+
+// MinimizeforLaunchAngle (.cc:683-731)
+__device__ double rtf_min_launch(const DevMedium& M, double x, double AirTxHeight,
+                                 double IceLayerHeight, double AntennaDepth, double D) {
+  double air[4 * kMaxLayers + 1];
+  const int nf = rtf_air_prop(M, x, AirTxHeight, IceLayerHeight, air);
+  double thd_air = 0;
+  for (int i = 0; i < nf; i++) thd_air += air[i * 4];
+  // no air layer (Tx above 150 km or below the ice): the reference reads an unset slot (UB),
+  // modelled as NaN like the oracle
+  const double Lvalue = nf > 0 ? air[2] : __builtin_nan("");
+  double thd_ice = 0;
+  if (AntennaDepth != 0) {
+    double ice[4];
+    rtf_ice_prop(M, AntennaDepth, Lvalue, ice);
+    thd_ice = ice[0];
+  }
+  return D - (thd_ice + thd_air);
+}
+
+struct RtfCall {
+  int op, n_out;
+  double a[8];
+};
+
+__global__ void rtf_kernel(DevMedium M, RtfCall c, double* __restrict__ out) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  double r[4 * kMaxLayers + 1];
+  for (int i = 0; i < 4 * kMaxLayers + 1; i++) r[i] = 0;
+  switch (c.op) {
+    case AIRICE_RTF_HIT_POINT:
+      rtf_hit_point(M, c.a[0], c.a[1], c.a[2], c.a[3], (int)c.a[4], r);
+      break;
+    case AIRICE_RTF_OPTICAL_PATH:
+      r[0] = rtf_optical_path(M, c.a[0], c.a[1], c.a[2], c.a[3], (int)c.a[4]);
+      break;
+    case AIRICE_RTF_PROPAGATION_TIME:
+      r[0] = rtf_prop_time(M, c.a[0], c.a[1], c.a[2], c.a[3], (int)c.a[4]);
+      break;
+    case AIRICE_RTF_AIR_PROPAGATION:
+      rtf_air_prop(M, c.a[0], c.a[1], c.a[2], r);
+      break;
+    case AIRICE_RTF_ICE_PROPAGATION:  // (IncidentAngleonIce, IceLayerHeight unused, .cc:664)
+      rtf_ice_prop(M, c.a[2], c.a[3], r);
+      break;
+    case AIRICE_RTF_FDNFR:
+      r[0] = rtf_fDnfR(c.a[0], c.a[1], c.a[2], c.a[3], c.a[4]);
+      break;
+    case AIRICE_RTF_FTIMED:
+      r[0] = rtf_ftimeD(M, c.a[0], c.a[1], c.a[3], c.a[4], c.a[5], (int)c.a[6]);
+      break;
+    case AIRICE_RTF_MIN_LAUNCH:
+      r[0] = rtf_min_launch(M, c.a[0], c.a[1], c.a[2], c.a[3], c.a[4]);
+      break;
+    default:
+      break;
+  }
+  for (int i = 0; i < c.n_out; i++) out[i] = r[i];
+}
+
+}  // namespace
+
+int rtf_outputs(int op, int max_layers) {
+  switch (op) {
+    case AIRICE_RTF_HIT_POINT:
+    case AIRICE_RTF_ICE_PROPAGATION:
+      return 4;
+    case AIRICE_RTF_AIR_PROPAGATION:
+      return 4 * max_layers + 1;
+    case AIRICE_RTF_OPTICAL_PATH:
+    case AIRICE_RTF_PROPAGATION_TIME:
+    case AIRICE_RTF_FDNFR:
+    case AIRICE_RTF_FTIMED:
+    case AIRICE_RTF_MIN_LAUNCH:
+      return 1;
+    default:
+      return -1;
+  }
+}
+
+int launch_rtf(const DevMedium& M, int op, const double* args, size_t n_args, double* d_out,
+               hipStream_t st) {
+  RtfCall c;
+  c.op = op;
+  c.n_out = rtf_outputs(op, M.ml);
+  for (int i = 0; i < 8; i++) c.a[i] = (size_t)i < n_args ? args[i] : 0.0;
+  hipLaunchKernelGGL(rtf_kernel, dim3(1), dim3(64), 0, st, M, c, d_out);
+  return hipGetLastError() == hipSuccess ? AIRICE_OK : AIRICE_EHIP;
+}
+
+}  // namespace airice

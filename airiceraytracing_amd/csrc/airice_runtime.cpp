@@ -554,6 +554,37 @@ int airice_single_ray_launch(const airice_medium* m, double antenna_depth_m, dou
   return rc;
 }
 
+int airice_rtf_outputs(int op, int max_layers) { return airice::rtf_outputs(op, max_layers); }
+
+int airice_rtf_eval(const airice_medium* m, int op, const double* args, size_t n_args, double* out,
+                    size_t n_out) {
+  if (m == nullptr || out == nullptr || (n_args > 0 && args == nullptr)) {
+    set_error("null argument");
+    return AIRICE_EINVAL;
+  }
+  DevMedium M;
+  int rc = build_dev_medium(m, AIRICE_VARIANT_MULTIRAY, &M);
+  if (rc) return rc;
+  const int need = airice::rtf_outputs(op, M.ml);
+  if (need < 0) {
+    set_error("unknown RayTracingFunctions op %d", op);
+    return AIRICE_EINVAL;
+  }
+  if (n_out < (size_t)need || n_args > 8) {
+    set_error("rtf op %d: %zu outputs (need %d), %zu args (max 8)", op, n_out, need, n_args);
+    return AIRICE_EINVAL;
+  }
+  thread_local double* d = nullptr;  // per-thread result slot, kept for the next call
+  if (d == nullptr) HIP_TRY(hipMalloc(&d, sizeof(double) * (4 * kMaxLayers + 1)));
+  rc = airice::launch_rtf(M, op, args, n_args, d, nullptr);
+  if (rc) {
+    set_error("rtf launch failed: %s", hipGetErrorString(hipGetLastError()));
+    return rc;
+  }
+  HIP_TRY(hipMemcpy(out, d, sizeof(double) * need, hipMemcpyDeviceToHost));
+  return AIRICE_OK;
+}
+
 int airice_single_ray_host(const airice_medium* m, double antenna_depth_m, double launch_deg,
                            double txh_m, double ice_m, double* summary, double* x, double* z,
                            size_t cap) {

@@ -172,6 +172,18 @@ class AirIceSolver:
                                                    _stream_handle(stream)),
               "airice_trace_ice_to_air_launch")
 
+    def rtf_eval(self, op: int, args) -> np.ndarray:
+        """One RayTracingFunctions:: scalar function on the GPU (AIRICE_RTF_*, include/airice.h),
+        in the reference's output layout."""
+        a = np.ascontiguousarray(args, dtype=np.float64)
+        n = lib().airice_rtf_outputs(op, int(self.medium.max_layers))
+        if n < 0:
+            raise ValueError(f"unknown RayTracingFunctions op {op}")
+        out = np.zeros(n, dtype=np.float64)
+        check(lib().airice_rtf_eval(ctypes.byref(self.medium), op, ptr(a), a.size, ptr(out), n),
+              "airice_rtf_eval")
+        return out
+
     def trace_ice_to_air_host(self, depth, ice, txh, dist):
         arrs = [np.ascontiguousarray(np.broadcast_to(a, np.shape(depth)), dtype=np.float64).ravel()
                 for a in (depth, ice, txh, dist)]

@@ -222,6 +222,31 @@ int airice_trace_ice_to_air_host(const airice_medium *m, const double *depth, co
 void Py_TraceIceToAir(double AntennaDepth, double IceLayerHeight, double AirTxHeight,
                       double HorizontalDistance, double ArrayParameters[10]);
 
+/* --- RayTracingFunctions:: scalar layer (RayTracingFunctions.cc, the cfg1 CLI's library) --- */
+/* One call evaluated on the device with the reference's expressions (pi 3.1415927); host
+ * arguments and outputs, synchronous.  For the RayTracingFunctions.h drop-in
+ * (include/RayTracingFunctions.h); batches belong on the table / solve / single-ray paths. */
+#define AIRICE_RTF_HIT_POINT 0        /* GetLayerHitPointPar (.cc:399-527)
+                                         args {n_layer1, RxDepth, TxDepth, IncidentAng, AirOrIce}
+                                         -> {THD, ReceiveAngle deg, L, time s} */
+#define AIRICE_RTF_OPTICAL_PATH 1     /* GetRayOpticalPath (.cc:349-369)
+                                         args {A, RxDepth, TxDepth, Lvalue, AirOrIce} -> {x} */
+#define AIRICE_RTF_PROPAGATION_TIME 2 /* GetRayPropagationTime (.cc:371-397), args as above */
+#define AIRICE_RTF_AIR_PROPAGATION 3  /* GetAirPropagationPar (.cc:529-659)
+                                         args {LaunchAngle, AirTxHeight, IceLayerHeight}
+                                         -> 4 x MaxLayers {THD, Recv, L, t} + count */
+#define AIRICE_RTF_ICE_PROPAGATION 4  /* GetIcePropagationPar (.cc:661-681) args {IncidentAngle,
+                                         IceLayerHeight, AntennaDepth, Lvalue} -> {THD, Recv, L, t} */
+#define AIRICE_RTF_FDNFR 5            /* fDnfR (.cc:293-303) args {x, a, b, c, l} -> {value} */
+#define AIRICE_RTF_FTIMED 6           /* ftimeD (.cc:328-347) args {x, a, b, c, speedc, l,
+                                         airorice} -> {value} */
+#define AIRICE_RTF_MIN_LAUNCH 7       /* MinimizeforLaunchAngle (.cc:683-731) args {x, airtxheight,
+                                         icelayerheight, antennadepth, horizontaldistance} */
+/* Outputs written for op (4 x max_layers + 1 for AIR_PROPAGATION), or -1 for an unknown op. */
+int airice_rtf_outputs(int op, int max_layers);
+int airice_rtf_eval(const airice_medium *m, int op, const double *args, size_t n_args,
+                    double *out, size_t n_out);
+
 /* Device bookkeeping (thin wrappers so ctypes callers need no HIP runtime binding). */
 int airice_device_count(int *count);
 int airice_set_device(int device);

@@ -316,3 +316,20 @@ def single_ray(m: Medium, depth, launch_deg, txh, ice):
     L.or_single_ray_trace(ctypes.byref(m), depth, launch_deg, txh, ice, ctypes.byref(r), _ptr(x),
                           _ptr(z), n)
     return r, x, z
+
+
+def rtf_eval(m: Medium, op: int, args) -> np.ndarray:
+    """RayTracingFunctions:: scalar function `op` (AIRICE_RTF_*) in the reference's layout."""
+    L = lib()
+    if not getattr(L, "_rtf_sig", False):
+        L.or_rtf_eval.argtypes = [ctypes.POINTER(Medium), ctypes.c_int, ctypes.c_void_p,
+                                  ctypes.c_void_p]
+        L.or_rtf_eval.restype = ctypes.c_int
+        L._rtf_sig = True
+    a = np.zeros(8)
+    a[:len(args)] = args
+    out = np.zeros(4 * 8 + 1)
+    n = L.or_rtf_eval(ctypes.byref(m), op, _ptr(a), _ptr(out))
+    if n < 0:
+        raise ValueError(f"unknown op {op}")
+    return out[:n].copy()

@@ -571,6 +571,54 @@ static double MinimizeforLaunchAngle(const or_medium *m, double x, const minp *p
   return (p->horizontaldistance - (thd_ice + thd_air));
 }
 
+/* RayTracingFunctions:: scalar layer (RayTracingFunctions.cc): the same formulas as the
+ * MultiRay restatements above in the RTF layouts -- GetLayerHitPointPar (.cc:399-527) and
+ * GetIcePropagationPar (.cc:661-681) 4-wide {THD, Recv deg, L, t}, GetAirPropagationPar
+ * (.cc:529-659) 4 x MaxLayers + count at [4*MaxLayers], GetRayOpticalPath (.cc:349-369),
+ * GetRayPropagationTime (.cc:371-397), fDnfR (.cc:293-303), ftimeD (.cc:328-347),
+ * MinimizeforLaunchAngle (.cc:683-731).  Op codes as AIRICE_RTF_* (include/airice.h). */
+int or_rtf_eval(const or_medium *m, int op, const double *a, double *out) {
+  double t[5 * 8 + 2];
+  switch (op) {
+    case 0: /* HIT_POINT */
+      or_layer_hit_point_par(m, a[0], a[1], a[2], a[3], (int)a[4], t);
+      for (int j = 0; j < 4; j++) out[j] = t[j];
+      return 4;
+    case 1: /* OPTICAL_PATH */
+      out[0] = GetRayHorizontalPath(m, a[0], a[1], a[2], a[3], (int)a[4]);
+      return 1;
+    case 2: /* PROPAGATION_TIME */
+      out[0] = GetRayPropagationTime(m, a[0], a[1], a[2], a[3], (int)a[4]);
+      return 1;
+    case 3: { /* AIR_PROPAGATION */
+      for (int j = 0; j < 5 * 8 + 2; j++) t[j] = 0;
+      int nf = air_propagation(m, a[0], a[1], a[2], t);
+      for (int j = 0; j < 4 * m->max_layers + 1; j++) out[j] = 0;
+      for (int i = 0; i < nf; i++)
+        for (int j = 0; j < 4; j++) out[4 * i + j] = t[5 * i + j];
+      out[4 * m->max_layers] = nf;
+      return 4 * m->max_layers + 1;
+    }
+    case 4: /* ICE_PROPAGATION (IncidentAngleonIce unused, .cc:664) */
+      ice_propagation(m, a[1], a[2], a[3], t);
+      for (int j = 0; j < 4; j++) out[j] = t[j];
+      return 4;
+    case 5: /* FDNFR */
+      out[0] = fDnfR(a[0], a[1], a[2], a[3], a[4]);
+      return 1;
+    case 6: /* FTIMED (b unused by the formula) */
+      out[0] = ftimeD(m, a[0], a[1], a[3], a[4], a[5], (int)a[6]);
+      return 1;
+    case 7: { /* MIN_LAUNCH */
+      minp p = {a[1], a[2], a[3], a[4]};
+      out[0] = MinimizeforLaunchAngle(m, a[0], &p);
+      return 1;
+    }
+    default:
+      return -1;
+  }
+}
+
 /* FindFunctionRoot (.cc:340-374) with GSL bisection semantics:
  * gsl_root_fsolver_set (fsolver.c) + bisection_init/bisection_iterate (bisection.c) +
  * gsl_root_test_interval(lo, hi, 0, tol) (convergence.c), loop while CONTINUE and

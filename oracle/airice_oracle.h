@@ -166,5 +166,8 @@ typedef struct or_single_ray {
   long n_air, n_ice;                    /* path samples in air / ice */
 } or_single_ray;
 /* x/z (nullable): capacity cap >= n_air + n_ice samples, in file order (ipoints). */
+/* RayTracingFunctions:: scalar layer in its own layouts; op as AIRICE_RTF_*; returns outputs. */
+int or_rtf_eval(const or_medium *m, int op, const double *args, double *out);
+
 int or_single_ray_trace(const or_medium *m, double depth, double launch_deg, double txh,
                         double ice, or_single_ray *out, double *x, double *z, long cap);
