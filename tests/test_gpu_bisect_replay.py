@@ -88,3 +88,19 @@ def test_replay_hdtip_cm(solvers):
 
     fast, exact = _both(run)
     _same(fast, exact)
+
+
+def test_replay_edge_grid(solvers):
+    """Tx exactly on layer bounds / at the atmosphere top, zero and tiny distances, antennas at
+    the surface, ice heights on layer bounds (per-query ice through the pythonwrapper trace)."""
+    import itertools
+    _, sp = solvers
+    txh = [3000.5, 3217.48275, 3217.4828, 8363.53902, 23141.7538, 50000.0, 99999.99, 100000.0]
+    dist = [0.0, 1e-9, 1e-3, 1.0, 1000.0, 5e4, 5e5]
+    depth = [-300.0, -1e-9, 0.0, 1e-9, 300.0]
+    ice = [0.0, 3000.0, 3217.48275, 8363.53902 - 1.0]
+    g = np.array(list(itertools.product(txh, dist, depth, ice)))
+    keep = g[:, 0] > g[:, 3] + np.maximum(g[:, 2], 0) + 0.1  # Tx above the Rx
+    g = g[keep]
+    fast, exact = _both(lambda: sp.trace_ice_to_air_host(g[:, 2], g[:, 3], g[:, 0], g[:, 1]))
+    _same(fast, exact)
