@@ -30,6 +30,25 @@
 
 #include "airice_tlog.hpp"
 
+#ifndef AIRICE_LEAN_LOG
+#define AIRICE_LEAN_LOG 1
+#endif
+#ifndef AIRICE_INT_RANGE
+#define AIRICE_INT_RANGE 1
+#endif
+#ifndef AIRICE_FAST_ASIN
+#define AIRICE_FAST_ASIN 1
+#endif
+#ifndef AIRICE_FAST_FRESNEL
+#define AIRICE_FAST_FRESNEL 1
+#endif
+#ifndef AIRICE_SQRT_FIX
+#define AIRICE_SQRT_FIX 1
+#endif
+#ifndef AIRICE_RCP_NEWTON
+#define AIRICE_RCP_NEWTON 1
+#endif
+
 namespace airice {
 
 constexpr int kMaxLayers = 4;  // ATMLAY has 5 bounds -> at most 4 air layers
@@ -101,6 +120,7 @@ struct IceConsts {
   TopEnd topend[kMaxLayers];   // layer l as the Tx layer: its stop end
   SegConst iceseg;             // ice surface -> antenna (table)
   double n_air_ice, n_ice0;    // Getnz_air(ice), Getnz_ice(0) (Snell into the ice, Fresnel)
+  double n_ratio;              // n_air_ice / n_ice0 (IEEE quotient, folded on the host)
 };
 
 __host__ __device__ inline SegConst make_segconst(const Endpoint& T, const Endpoint& R) {
@@ -189,6 +209,11 @@ struct RayL {
   double L, LL, sAL, rsAL;  // L, L^2, sqrt(A^2-L^2), 1/sqrt(A^2-L^2)
 };
 
+// High 32 bits (sign, exponent, top of the mantissa) of a double.
+__device__ __forceinline__ uint32_t hi_word(double x) {
+  return (uint32_t)(__builtin_bit_cast(uint64_t, x) >> 32);
+}
+
 // sqrt(q) and 1/sqrt(q) together from one v_rsq_f64 and Goldschmidt/Newton refinement (the
 // iteration ocml's sqrt uses, without its denormal rescaling: q here is a difference of squares of
 // O(1) refractive indices); both within ~1 ulp.  q = 0 gives (0, +inf) and q < 0 / NaN gives NaNs,
@@ -203,8 +228,10 @@ __device__ __forceinline__ void sqrt_rsqrt(double q, double& s, double& rs) {
   g = __builtin_fma(d, h, g);
   e = __builtin_fma(-h, g, 0.5);
   h = __builtin_fma(h, e, h);
-  d = __builtin_fma(-g, g, q);
-  g = __builtin_fma(d, h, g);
+  if (AIRICE_SQRT_FIX > 1) {
+    d = __builtin_fma(-g, g, q);
+    g = __builtin_fma(d, h, g);
+  }
   s = (q == 0.0) ? q : g;
   rs = (q == 0.0) ? __builtin_inf() : 2.0 * h;
 }
@@ -218,9 +245,56 @@ __device__ __forceinline__ double fast_sqrt(double q) {
   h = __builtin_fma(h, e, h);
   double d = __builtin_fma(-g, g, q);
   g = __builtin_fma(d, h, g);
-  d = __builtin_fma(-g, g, q);
-  g = __builtin_fma(d, h, g);
+  if (AIRICE_SQRT_FIX > 1) {
+    d = __builtin_fma(-g, g, q);
+    g = __builtin_fma(d, h, g);
+  }
   return (q == 0.0) ? q : g;
+}
+
+// a / b for b positive and normal (2^-1000 <= b < 2^1000): v_rcp_f64 (24 bits, measured by
+// tools/rcp_rsq_accuracy.hip), one Newton step (48 bits), quotient and one residual correction
+// (Markstein) -- the IEEE quotient but for rare last-bit cases.  Other b: the IEEE division.
+__device__ __forceinline__ double div_pos(double a, double b) {
+  if (!(hi_word(b) - 0x01700000u < 0x7D000000u)) return a / b;
+  double y = __builtin_amdgcn_rcp(b);
+  y = __builtin_fma(y, __builtin_fma(-b, y, 1.0), y);
+  const double q0 = a * y;
+  return __builtin_fma(__builtin_fma(-b, q0, a), y, q0);
+}
+
+// asin(x) (radians): t + t^3 P(t^2) on |x| < 1/2 (P: degree-12 fit, tools/gen_asin_poly.py, error
+// 1.2e-16 relative), pi/2 - 2 asin(sqrt((1 - |x|)/2)) above (1 - |x| exact there); NaN for
+// |x| > 1 or NaN, as asin().  ~25 FP64 ops against ~64 for ocml's asin (tools/opweights.json).
+__device__ __forceinline__ double asin_fast(double x) {
+  const double ax = fabs(x);
+  const bool big = ax >= 0.5;
+  const double s = big ? 0.5 * (1.0 - ax) : ax * ax;
+  const double t = big ? fast_sqrt(s) : ax;
+  double p = __builtin_fma(s, kc(0x1.d72b2bc8155f8p-6), kc(-0x1.e6aaa8a0a04ccp-7));
+  p = __builtin_fma(s, p, kc(0x1.1d189408314eep-6));
+  p = __builtin_fma(s, p, kc(0x1.65a9c4dfcf8b2p-8));
+  p = __builtin_fma(s, p, kc(0x1.52420b04b37bep-7));
+  p = __builtin_fma(s, p, kc(0x1.782651caa6547p-7));
+  p = __builtin_fma(s, p, kc(0x1.c9cf07674736ap-7));
+  p = __builtin_fma(s, p, kc(0x1.1c4d35cf95421p-6));
+  p = __builtin_fma(s, p, kc(0x1.6e8bb1c8209a2p-6));
+  p = __builtin_fma(s, p, kc(0x1.f1c71c1db0623p-6));
+  p = __builtin_fma(s, p, kc(0x1.6db6db6e31f13p-5));
+  p = __builtin_fma(s, p, kc(0x1.3333333332ecap-4));
+  p = __builtin_fma(s, p, kc(0x1.5555555555556p-3));
+  const double r = __builtin_fma(t * s, p, t);
+  const double y = big ? __builtin_fma(-2.0, r, 0x1.921fb54442d18p+0) : r;
+  return __builtin_copysign(y, x);
+}
+
+// asin for the kernels' angle outputs (fast form unless AIRICE_FAST_ASIN=0)
+__device__ __forceinline__ double k_asin(double x) {
+#if AIRICE_FAST_ASIN
+  return asin_fast(x);
+#else
+  return asin(x);
+#endif
 }
 
 __device__ __forceinline__ RayL ray_L(double A2, double L) {
@@ -251,13 +325,23 @@ __device__ __forceinline__ double fast_log(double x) { return tlog(x); }
 __device__ __forceinline__ double log_ratio_fast(double a, double b, const double* tab, bool& ok) {
   double y = __builtin_amdgcn_rcp(b);
   y = __builtin_fma(y, __builtin_fma(-b, y, 1.0), y);
-  y = __builtin_fma(y, __builtin_fma(-b, y, 1.0), y);
+  if (AIRICE_RCP_NEWTON > 1) y = __builtin_fma(y, __builtin_fma(-b, y, 1.0), y);
   const double q0 = a * y;
   const double q = __builtin_fma(__builtin_fma(-b, q0, a), y, q0);
   // a > 0 and q in range cover a (a tiny / huge / inf / NaN shows in q or in a > 0); b in range
   // keeps v_rcp_f64 and the Newton steps clear of overflow and denormals
+#if AIRICE_INT_RANGE
+  // the same test on the high words: 2^-1000 <= b, q < 2^1000 as unsigned exponent ranges
+  // (a negative, zero, NaN or infinite value falls outside; a <= 0 or NaN makes q so)
+  ok = (hi_word(b) - 0x01700000u < 0x7D000000u) && (hi_word(q) - 0x01700000u < 0x7D000000u);
+#else
   ok = a > 0.0 && b > 0x1p-1000 && b < 0x1p1000 && q > 0x1p-1000 && q < 0x1p1000;
-  return tlog_pos(q, tab);  // garbage, and unused, when !ok
+#endif
+#if AIRICE_LEAN_LOG
+  return tlog_lean(q, tab);  // garbage, and unused, when !ok
+#else
+  return tlog_pos(q, tab);
+#endif
 }
 
 __device__ __forceinline__ double log_ratio_ieee(double a, double b) {

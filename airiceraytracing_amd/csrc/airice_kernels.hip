@@ -38,7 +38,20 @@ constexpr int kBlock = 256;
 #ifndef AIRICE_TABLE_WAVES
 #define AIRICE_TABLE_WAVES 8
 #endif
+#ifndef AIRICE_TABLE_WAVES2
+#define AIRICE_TABLE_WAVES2 7
+#endif
 constexpr int kTableBlock = AIRICE_TABLE_BS;
+// R = 2 window (rays per launch): above one round of resident R = 1 waves (256 CUs x 4 SIMDs x
+// AIRICE_TABLE_WAVES waves x 64 lanes), up to one round of R = 2 waves
+#ifndef AIRICE_TWO_RAY_MIN
+#define AIRICE_TWO_RAY_MIN (256 * 4 * AIRICE_TABLE_WAVES * 64)
+#endif
+#ifndef AIRICE_TWO_RAY_MAX
+#define AIRICE_TWO_RAY_MAX (2 * 256 * 4 * AIRICE_TABLE_WAVES2 * 64)
+#endif
+constexpr int kTwoRayMin = AIRICE_TWO_RAY_MIN;
+constexpr int kTwoRayMax = AIRICE_TWO_RAY_MAX;
 
 // ---------------------------------------------------------------------------
 // Forward ray: GetRayTracingSolutions (.cc:1796-2017).  d[] = dummy[0..17].
@@ -55,18 +68,28 @@ __device__ __forceinline__ Endpoint stop_of(const DevMedium& M, int l) {
 
 // Fresnel T_S, T_P (.cc:285-337) at the incidence whose sine is v (identity (2):
 // sin(asin(v) r2d d2r) = v, cos = sqrt(1 - v^2) on [0, 90] degrees).
-__device__ __forceinline__ void fresnel_from_sine(double n1, double n2, double v, double& tS,
-                                                  double& tP) {
+// ratio = n1 / n2 (folded on the host, IceConsts::n_ratio).  The two quotients have positive
+// denominators (n1, n2 > 0 and ct, sqterm >= 0, never both 0): div_pos.
+__device__ __forceinline__ void fresnel_from_sine(double n1, double n2, double ratio, double v,
+                                                  double& tS, double& tP) {
   const double st = v, ct = fast_sqrt(1 - v * v);
-  const double a = (n1 / n2) * st;
+  const double a = ratio * st;
   const double sqterm = fast_sqrt(1 - a * a);
   double num = n1 * ct - n2 * sqterm;
   double den = n1 * ct + n2 * sqterm;
+#if AIRICE_FAST_FRESNEL
+  tS = 1 + div_pos(num, den);
+#else
   tS = 1 + (num / den);
+#endif
   if (isnan(tS)) tS = 0;
   num = n1 * sqterm - n2 * ct;
   den = n1 * sqterm + n2 * ct;
-  tP = (1 - (num / den)) * (n1 / n2);
+#if AIRICE_FAST_FRESNEL
+  tP = (1 - div_pos(num, den)) * ratio;
+#else
+  tP = (1 - (num / den)) * ratio;
+#endif
   if (isnan(tP)) tP = 0;
 }
 
@@ -141,6 +164,26 @@ __device__ __forceinline__ double sin_start(double x) {
   return __builtin_fma(x * x2, p, x);
 }
 
+// Wave priority = segments still to trace (capped at 3), lowered at each segment boundary of the
+// table kernel: the arbiter issues from the highest-priority ready wave (oldest first among
+// equals), so waves that are behind catch up and the SIMD keeps many waves until the end instead
+// of running its youngest waves alone (latency-bound) at the tail.  rem must be wave-uniform.
+#ifndef AIRICE_TABLE_PRIO
+#define AIRICE_TABLE_PRIO 0
+#endif
+__device__ __forceinline__ void prio_remaining(bool on, int rem) {
+  if (!on) return;
+  rem = __builtin_amdgcn_readfirstlane(rem);
+  if (rem >= 3)
+    __builtin_amdgcn_s_setprio(3);
+  else if (rem == 2)
+    __builtin_amdgcn_s_setprio(2);
+  else if (rem == 1)
+    __builtin_amdgcn_s_setprio(1);
+  else
+    __builtin_amdgcn_s_setprio(0);
+}
+
 // want_inc: dummy[12] (the incidence angle on the ice, one asin) is not a table column
 // (.cc:2101-2111), so table launches without the double output skip it.
 // top_hi >= 0: a wave-uniform upper bound of the lanes' Tx layers (the table block's first row);
@@ -151,7 +194,9 @@ __device__ __forceinline__ void ray_solution_row(const DevMedium& M, const IceCo
                                                  const RowConst& rc, double theta, bool in_ice,
                                                  double* d, bool want_inc,
                                                  const double* tab = &kLogTable[0][0],
-                                                 int top_hi = -1) {
+                                                 int top_hi = -1, int prio_after = -1) {
+  // prio_after >= 0: table launch; segments of later rays of this lane still to come
+  const bool prio = AIRICE_TABLE_PRIO && prio_after >= 0;
   const double H = rc.H;
   const int top = rc.top;
   const int bot = I.bot;
@@ -168,6 +213,7 @@ __device__ __forceinline__ void ray_solution_row(const DevMedium& M, const IceCo
   }
   // lower layers: both ends folded on the host (I.lower, scalar reads)
   if (top_hi >= 0) {
+    prio_remaining(prio, prio_after + (top_hi - bot) + (in_ice ? 1 : 0));
 #pragma clang loop unroll(disable)
     for (int il = top_hi - 1; il >= bot; --il) {
       if (il < top) {
@@ -176,6 +222,7 @@ __device__ __forceinline__ void ray_solution_row(const DevMedium& M, const IceCo
         t_air += s.t;
         geo_air += s.geo;
       }
+      prio_remaining(prio, prio_after + (il - bot) + (in_ice ? 1 : 0));
     }
   } else {
 #pragma unroll
@@ -189,22 +236,23 @@ __device__ __forceinline__ void ray_solution_row(const DevMedium& M, const IceCo
   }
   // IncidentAngleonIce = last layer's receive angle; 0 when no air layer (.cc:1832, 1881)
   double inc = 0.0;
-  if (want_inc) inc = any ? asin(v) * M.r2d : 0.0;
+  if (want_inc) inc = any ? k_asin(v) * M.r2d : 0.0;
   const double vinc = any ? v : 0.0;
   double thd_ice = 0.0, t_ice = 0.0, geo_ice = 0.0, recv_ice = 0.0;
   if (in_ice) {
     // .cc:1897-1922: n_layer1 = Getnz_air(IceLayerHeight), Rx = -AntennaDepth, Tx = 0
     const double A2i = M.A_ice * M.A_ice;
-    const double u = sin_asin((I.n_air_ice / I.n_ice0) * vinc);
+    const double u = sin_asin(I.n_ratio * vinc);
     double v2;
     const Segment s = segment_const(I.iceseg, M.A_ice, A2i, u, false, v2, tab);
     thd_ice += s.thd;
     t_ice += s.t;
     geo_ice += s.geo;
-    recv_ice = asin(v2) * M.r2d;
+    recv_ice = k_asin(v2) * M.r2d;
+    prio_remaining(prio, prio_after);
   }
   double tS, tP;
-  fresnel_from_sine(I.n_air_ice, I.n_ice0, vinc, tS, tP);
+  fresnel_from_sine(I.n_air_ice, I.n_ice0, I.n_ratio, vinc, tS, tP);
   d[0] = 0;
   d[1] = H;
   d[2] = thd_air + thd_ice;
@@ -240,7 +288,8 @@ struct TableArgs {
   int hsteps, asteps;
   int row0, in_ice;
   int n;              // rays of this launch (< 2^31; launch_table splits larger grids)
-  int rows_per_block; // LDS rows a block may span
+  int rows_per_block; // LDS rows a block's set of rays may span
+  int half;           // rays per set (R = 2: ceil(n / 2); R = 1: n)
   size_t ld;
 };
 
@@ -271,13 +320,13 @@ __device__ __forceinline__ int ray_row(const TableArgs& G, int k) {
 __device__ __forceinline__ void table_ray(const DevMedium& M, const IceConsts& I,
                                           const TableArgs& G, const RowConst& rc, int r, int k,
                                           float* __restrict__ table, double* __restrict__ full,
-                                          const double* tab, int top_hi) {
+                                          const double* tab, int top_hi, int prio_after) {
   const int iang = k - r * G.asteps;
   // .cc:2085, 2092-2094
   double th = G.start_a + G.step_a * iang;
   if (iang == G.asteps - 1) th = G.stop_a;
   double d[18];
-  ray_solution_row(M, I, rc, th, G.in_ice != 0, d, full != nullptr, tab, top_hi);
+  ray_solution_row(M, I, rc, th, G.in_ice != 0, d, full != nullptr, tab, top_hi, prio_after);
   const size_t ld = G.ld;
   // AllTableAllAntData columns (.cc:2101-2111)
   table[0 * ld + k] = (float)d[1];
@@ -297,16 +346,20 @@ __device__ __forceinline__ void table_ray(const DevMedium& M, const IceConsts& I
   }
 }
 
-// Table launch: one ray per lane.  The block first evaluates the Tx-height-only constants of the
-// (few) rows it spans into LDS -- one lane per row, so the exp / layer scans / top-layer folding
-// run once per row instead of once per wave -- then every lane traces its ray.  (Persistent
-// grid-stride and atomic-chunk schedules were measured and rejected: the loop around the inlined
-// ray body raises register pressure to 160 VGPRs, or 330 B/lane of scratch when capped at 64,
-// and runs 2.7x / 7x slower.)
-template <int BS, bool TRACE = false>
-// waves_per_eu(8): 64 VGPRs (12 B/lane spilled) at 8 waves/SIMD measured on par or slightly
-// ahead of 67 VGPRs at 7 (bench 42.0 vs 42.9 us for cfg2).
-__global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(AIRICE_TABLE_WAVES, AIRICE_TABLE_WAVES))) void table_kernel(
+// Table launch: R rays per lane, ray k of set j = k0 + j * G.half + threadIdx.x (each set a
+// contiguous range, so every column store of a wave stays one 256 B segment).  The block first
+// evaluates the Tx-height-only constants of the (few) rows each set spans into LDS -- one lane per
+// row, so the exp / layer scans / top-layer folding run once per row instead of once per wave --
+// then every lane traces its rays one after the other.  R = 2 exists for grids that would need
+// about 1.6 rounds of resident waves at R = 1 (BASELINE cfg2): with half as many waves the whole
+// grid is resident at once, so no wave starts late and finishes after the others.
+// (Persistent grid-stride and atomic-chunk schedules were measured and rejected: the loop around
+// the inlined ray body raises register pressure to 160 VGPRs, or 330 B/lane of scratch when capped
+// at 64, and runs 2.7x / 7x slower; the R copies here are straight-line code.)
+template <int BS, int R, bool TRACE = false>
+// waves_per_eu(8) at R = 1: 64 VGPRs (12 B/lane spilled) at 8 waves/SIMD measured on par or
+// slightly ahead of 67 VGPRs at 7 (bench 42.0 vs 42.9 us for cfg2).  R = 2 needs <= 7 waves/SIMD.
+__global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(R == 1 ? AIRICE_TABLE_WAVES : AIRICE_TABLE_WAVES2, R == 1 ? AIRICE_TABLE_WAVES : AIRICE_TABLE_WAVES2))) void table_kernel(
                                                    DevMedium M, IceConsts I, TableArgs G,
                                                    float* __restrict__ table,
                                                    double* __restrict__ full,
@@ -324,19 +377,33 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(AIRICE_TABLE
   const int lane = threadIdx.x & 63;
   if (TRACE && lane == 0) trace[wave].t0 = __builtin_amdgcn_s_memrealtime();
   const int k0 = (int)blockIdx.x * BS;
-  const int r0 = ray_row(G, k0);
-  const int nrows = ray_row(G, min(k0 + BS, G.n) - 1) - r0 + 1;
-  for (int t = threadIdx.x; t < nrows; t += BS)
-    rows[t] = row_const(M, I, row_height(G, G.row0 + r0 + t));
+  int r0[R];
+#pragma unroll
+  for (int j = 0; j < R; ++j) {
+    const int kb = k0 + j * G.half;                        // first ray of set j
+    const int ke = min(kb + BS, j + 1 < R ? G.half + j * G.half : G.n);  // end of set j
+    r0[j] = kb < ke ? ray_row(G, kb) : 0;
+    const int nrows = kb < ke ? ray_row(G, ke - 1) - r0[j] + 1 : 0;
+    for (int t = threadIdx.x; t < nrows; t += BS)
+      rows[j * G.rows_per_block + t] = row_const(M, I, row_height(G, G.row0 + r0[j] + t));
+  }
   __syncthreads();
-  // the block's first row has the highest Tx, so its Tx layer bounds every lane's (top_layer is
-  // monotone in the height)
-  const int top_hi = __builtin_amdgcn_readfirstlane(rows[0].top);
-  __builtin_assume(top_hi >= 0);
-  const int k = k0 + (int)threadIdx.x;
-  if (k < G.n) {
-    const int r = ray_row(G, k);
-    table_ray(M, I, G, rows[r - r0], r, k, table, full, &s_logtab[0][0], top_hi);
+  prio_remaining(AIRICE_TABLE_PRIO, 3);
+#pragma unroll
+  for (int j = 0; j < R; ++j) {
+    const int k = k0 + j * G.half + (int)threadIdx.x;
+    const int ke = j + 1 < R ? G.half + j * G.half : G.n;
+    if (k0 + j * G.half >= ke) break;  // block-uniform: set j of this block is empty
+    // the set's first row has the highest Tx, so its Tx layer bounds every lane's (top_layer is
+    // monotone in the height)
+    const int top_hi = __builtin_amdgcn_readfirstlane(rows[j * G.rows_per_block].top);
+    __builtin_assume(top_hi >= 0);
+    if (k < ke) {
+      const int r = ray_row(G, k);
+      // later rays of the lane: ~4 segments each
+      table_ray(M, I, G, rows[j * G.rows_per_block + (r - r0[j])], r, k, table, full,
+                &s_logtab[0][0], top_hi, 4 * (R - 1 - j));
+    }
   }
   if (TRACE && lane == 0) {
     trace[wave].t1 = __builtin_amdgcn_s_memrealtime();
@@ -1143,12 +1210,12 @@ int launch_table(const DevMedium& M, const IceConsts& I, const airice_grid* g, i
   A.in_ice = g->in_ice;
   A.ld = ld;
   A.inv_asteps = 1.0 / (double)g->angle_steps;
-  // rows a 256-ray block can touch, for the LDS row constants
+  // rows a 256-ray set can touch, for the LDS row constants
   A.rows_per_block = std::min(kTableBlock, (kTableBlock - 1) / g->angle_steps + 2);
-  const size_t lds = sizeof(RowConst) * (size_t)A.rows_per_block;
   static const char* trace_path = getenv("AIRICE_TABLE_TRACE");
+  static const int force_r = getenv("AIRICE_TABLE_RPL") ? atoi(getenv("AIRICE_TABLE_RPL")) : 0;
   // ray indices are 32-bit inside a launch: grids of 2^31 rays or more go in row slabs
-  const int max_rows = (int)std::max<long long>(1, ((1LL << 31) - kTableBlock) / g->angle_steps);
+  const int max_rows = (int)std::max<long long>(1, ((1LL << 31) - 2 * kTableBlock) / g->angle_steps);
   for (int done = 0; done < row_count;) {
     const int rows = std::min(max_rows, row_count - done);
     const size_t off = (size_t)done * (size_t)g->angle_steps;
@@ -1156,11 +1223,21 @@ int launch_table(const DevMedium& M, const IceConsts& I, const airice_grid* g, i
     A.n = rows * g->angle_steps;
     float* tab = d_table + off;
     double* full = d_full ? d_full + off : nullptr;
-    const unsigned blocks = (unsigned)((A.n + kTableBlock - 1) / kTableBlock);
     done += rows;
+    // two rays per lane when one ray per lane would take more than one round of resident waves
+    // but two fit in one (kTwoRayMin..kTwoRayMax rays; the double-output parity launches keep one)
+    const int R = force_r ? force_r
+                          : (full == nullptr && A.n > kTwoRayMin && A.n <= kTwoRayMax ? 2 : 1);
+    A.half = R == 2 ? (A.n + 1) / 2 : A.n;
+    const size_t lds = sizeof(RowConst) * (size_t)A.rows_per_block * R;
+    const unsigned blocks = (unsigned)((A.half + kTableBlock - 1) / kTableBlock);
     if (trace_path == nullptr) {
-      hipLaunchKernelGGL((table_kernel<kTableBlock, false>), dim3(blocks), dim3(kTableBlock), lds, st, M, I,
-                         A, tab, full, nullptr);
+      if (R == 2)
+        hipLaunchKernelGGL((table_kernel<kTableBlock, 2, false>), dim3(blocks), dim3(kTableBlock),
+                           lds, st, M, I, A, tab, full, nullptr);
+      else
+        hipLaunchKernelGGL((table_kernel<kTableBlock, 1, false>), dim3(blocks), dim3(kTableBlock),
+                           lds, st, M, I, A, tab, full, nullptr);
       if (hipGetLastError() != hipSuccess) return AIRICE_EHIP;
       continue;
     }
@@ -1168,8 +1245,12 @@ int launch_table(const DevMedium& M, const IceConsts& I, const airice_grid* g, i
     const long long nw = (long long)blocks * (kTableBlock / 64);
     WaveTrace* dtr = nullptr;
     if (hipMalloc(&dtr, sizeof(WaveTrace) * nw) != hipSuccess) return AIRICE_EHIP;
-    hipLaunchKernelGGL((table_kernel<kTableBlock, true>), dim3(blocks), dim3(kTableBlock), lds, st, M, I, A,
-                       tab, full, dtr);
+    if (R == 2)
+      hipLaunchKernelGGL((table_kernel<kTableBlock, 2, true>), dim3(blocks), dim3(kTableBlock), lds,
+                         st, M, I, A, tab, full, dtr);
+    else
+      hipLaunchKernelGGL((table_kernel<kTableBlock, 1, true>), dim3(blocks), dim3(kTableBlock), lds,
+                         st, M, I, A, tab, full, dtr);
     std::vector<WaveTrace> h(nw);
     if (hipStreamSynchronize(st) != hipSuccess ||
         hipMemcpy(h.data(), dtr, sizeof(WaveTrace) * nw, hipMemcpyDeviceToHost) != hipSuccess)

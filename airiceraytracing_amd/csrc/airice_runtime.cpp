@@ -230,6 +230,7 @@ void build_ice_consts(const DevMedium& M, double ice_h, double rx_depth, IceCons
   out->ice_rx = host_ice_endpoint(M, rx_depth);
   out->n_air_ice = out->ice_air.n;
   out->n_ice0 = out->ice0.n;
+  out->n_ratio = out->n_air_ice / out->n_ice0;
   // lowest air layer: SkipLayersBelow scan (.cc:1815-1825)
   int bot = 0;
   for (int il = 0; il < M.ml; ++il) {

@@ -1,10 +1,11 @@
 // CPU twin of the device logarithm (airice_tlog.hpp compiled by g++): writes tlog() of the
 // deterministic inputs for the bit comparison with the GPU, and reports the error against
 // long double logl over the finite, positive inputs.
-//   tlog_check N seed out.bin
+//   tlog_check N seed out.bin [lean]   (lean: tlog_lean on the finite positive normal inputs)
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
+#include <string>
 #include <vector>
 
 #include "../../airiceraytracing_amd/csrc/airice_tlog.hpp"
@@ -13,11 +14,13 @@
 int main(int argc, char** argv) {
   if (argc < 4) return 2;
   const uint64_t n = std::strtoull(argv[1], nullptr, 10), seed = std::strtoull(argv[2], nullptr, 10);
+  const bool lean = argc > 4 && std::string(argv[4]) == "lean";
   std::vector<double> y(n);
   double max_ulp = 0, worst_x = 0;
   for (uint64_t i = 0; i < n; ++i) {
     const double x = tlog_input(i, seed);
-    y[i] = airice::tlog(x);
+    const bool normal = x >= 0x1p-1022 && x < __builtin_inf();
+    y[i] = (lean && normal) ? airice::tlog_lean(x) : airice::tlog(x);
     if (x > 0 && std::isfinite(x)) {
       const long double ref = logl((long double)x);
       const double rd = (double)ref;

@@ -19,11 +19,11 @@ GPU = os.path.join(ROOT, "tests", "cpp", "tlog_gpu")
 N = 4_000_000
 
 
-def _cpu(tmp_path, n=N, seed=12345):
+def _cpu(tmp_path, n=N, seed=12345, lean=False):
     assert os.path.exists(CPU), "build with __graft_entry__.build()"
     out = tmp_path / "cpu.bin"
-    r = subprocess.run([CPU, str(n), str(seed), str(out)], capture_output=True, text=True,
-                       timeout=300)
+    r = subprocess.run([CPU, str(n), str(seed), str(out)] + (["lean"] if lean else []),
+                       capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stdout + r.stderr
     return json.loads(r.stdout), np.fromfile(out, dtype=np.float64)
 
@@ -67,13 +67,20 @@ def test_twin_against_mpmath(tmp_path):
     assert worst < 1.0, worst
 
 
+def test_lean_twin_within_two_ulps(tmp_path):
+    """tlog_lean (the log-ratio logarithm of the ray kernels): no hi + lo bookkeeping."""
+    rep, _ = _cpu(tmp_path, lean=True)
+    assert rep["max_ulp"] < 2.5, rep  # 1.91 measured
+
+
 @pytest.mark.gpu
-def test_device_matches_twin_bitwise(tmp_path):
+@pytest.mark.parametrize("lean", [False, True])
+def test_device_matches_twin_bitwise(tmp_path, lean):
     assert os.path.exists(GPU), "build with __graft_entry__.build()"
-    _, y_cpu = _cpu(tmp_path)
+    _, y_cpu = _cpu(tmp_path, lean=lean)
     out = tmp_path / "gpu.bin"
-    r = subprocess.run([GPU, str(N), "12345", str(out)], capture_output=True, text=True,
-                       timeout=300)
+    r = subprocess.run([GPU, str(N), "12345", str(out)] + (["lean"] if lean else []),
+                       capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stdout + r.stderr
     y_gpu = np.fromfile(out, dtype=np.float64)
     same = (y_gpu.view(np.uint64) == y_cpu.view(np.uint64)) | (np.isnan(y_gpu) & np.isnan(y_cpu))

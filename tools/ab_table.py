@@ -11,6 +11,8 @@ import os
 import subprocess
 import sys
 
+import numpy as np
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
@@ -34,8 +36,37 @@ def one(lib_path, reps, grid):
         e1.record(st)
     torch.cuda.synchronize()
     ms = e0.elapsed_time(e1) / reps
-    h = hashlib.sha1(table.cpu().numpy().tobytes()).hexdigest()
-    print(json.dumps({"lib": lib_path, "ms": ms, "rays_per_s": g.n_rays / ms * 1e3, "sha1": h}))
+    tnp = table.cpu().numpy()
+    h = hashlib.sha1(tnp.tobytes()).hexdigest()
+    rec = {"lib": lib_path, "ms": ms, "rays_per_s": g.n_rays / ms * 1e3, "sha1": h}
+    if os.environ.get("AB_PARITY"):
+        # float table vs the oracle (max ulps, differing entries) and the double outputs of a
+        # row sample vs the oracle (max relative difference, SURVEY.md §8(d) floors)
+        import oracle
+        from tests import parity
+        om = oracle.load_atmosphere(os.path.join(ROOT, "airiceraytracing_amd", "data",
+                                                 "Atmosphere.dat.gz"))
+        og = oracle.grid_init(*grid)
+        ot = oracle.table_rows(om, og, 0, og.height_steps, nthreads=16)
+        rec["max_ulps"] = int(parity.float_ulp_diff(tnp, ot))
+        rec["n_diff"] = int(np.count_nonzero(tnp.view(np.int32) != ot.view(np.int32)))
+        worst = 0.0
+        fh = hashlib.sha1()
+        for r0 in range(0, g.height_steps, g.height_steps // 7):
+            rr = min(200, g.height_steps - r0)
+            full = torch.empty((18, rr * g.angle_steps), dtype=torch.float64, device="cuda:0")
+            tt = torch.empty((11, rr * g.angle_steps), dtype=torch.float32, device="cuda:0")
+            s.table_device(g, tt, full, row_begin=r0, row_count=rr)
+            torch.cuda.synchronize()
+            _, of = oracle.table_rows(om, og, r0, r0 + rr, full=True, nthreads=16)
+            fnp = full.cpu().numpy()
+            fh.update(fnp.tobytes())
+            rep = parity.compare_columns(fnp, of, parity.RAY_FLOORS)
+            assert rep["ok"], rep
+            worst = max(worst, rep["max_rel"])
+        rec["full_max_rel"] = worst
+        rec["full_sha1"] = fh.hexdigest()[:12]
+    print(json.dumps(rec))
 
 
 def main():

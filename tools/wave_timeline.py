@@ -44,6 +44,9 @@ def main():
     key = (((xcc * 8 + se) * 2 + sh) * 16 + cu) * 4 + simd
     nsimd = len(np.unique(key))
     dur = end - start
+    out = os.environ.get("AIRICE_TRACE_NPZ")
+    if out:
+        np.savez_compressed(out, start=start, end=end, key=key)
     print(f"waves={len(w)} simds={nsimd} waves/simd={len(w) / nsimd:.2f} "
           f"kernel span={end.max():.2f}us first-start spread={np.percentile(start, 99):.2f}us")
     print(f"wave duration us: min {dur.min():.2f} p10 {np.percentile(dur, 10):.2f} "
