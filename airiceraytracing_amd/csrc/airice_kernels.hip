@@ -42,13 +42,16 @@ constexpr int kBlock = 256;
 #define AIRICE_TABLE_WAVES2 7
 #endif
 constexpr int kTableBlock = AIRICE_TABLE_BS;
-// R = 2 window (rays per launch): above one round of resident R = 1 waves (256 CUs x 4 SIMDs x
-// AIRICE_TABLE_WAVES waves x 64 lanes), up to one round of R = 2 waves
+// R = 2 window (rays per launch).  Measured on cfg2 (858,627 rays: 1.64 rounds of R = 1 waves,
+// one round at R = 2): 42.4 us at R = 2 against 40.1 us at R = 1 -- the single round's waves run
+// oldest-first, so the SIMDs still drain one wave at a time (tools/wave_timeline.py) -- hence the
+// window is empty by default and R = 2 is reachable only through AIRICE_TABLE_RPL=2 or building
+// with e.g. -DAIRICE_TWO_RAY_MIN=524288 -DAIRICE_TWO_RAY_MAX=917504.
 #ifndef AIRICE_TWO_RAY_MIN
-#define AIRICE_TWO_RAY_MIN (256 * 4 * AIRICE_TABLE_WAVES * 64)
+#define AIRICE_TWO_RAY_MIN 0
 #endif
 #ifndef AIRICE_TWO_RAY_MAX
-#define AIRICE_TWO_RAY_MAX (2 * 256 * 4 * AIRICE_TABLE_WAVES2 * 64)
+#define AIRICE_TWO_RAY_MAX 0
 #endif
 constexpr int kTwoRayMin = AIRICE_TWO_RAY_MIN;
 constexpr int kTwoRayMax = AIRICE_TWO_RAY_MAX;
@@ -350,9 +353,9 @@ __device__ __forceinline__ void table_ray(const DevMedium& M, const IceConsts& I
 // contiguous range, so every column store of a wave stays one 256 B segment).  The block first
 // evaluates the Tx-height-only constants of the (few) rows each set spans into LDS -- one lane per
 // row, so the exp / layer scans / top-layer folding run once per row instead of once per wave --
-// then every lane traces its rays one after the other.  R = 2 exists for grids that would need
-// about 1.6 rounds of resident waves at R = 1 (BASELINE cfg2): with half as many waves the whole
-// grid is resident at once, so no wave starts late and finishes after the others.
+// then every lane traces its rays one after the other.  R = 2 was built for grids that need about
+// 1.6 rounds of resident waves at R = 1 (BASELINE cfg2), so that the whole grid is resident at
+// once; it measured slower (kTwoRayMin/kTwoRayMax above) and is off by default.
 // (Persistent grid-stride and atomic-chunk schedules were measured and rejected: the loop around
 // the inlined ray body raises register pressure to 160 VGPRs, or 330 B/lane of scratch when capped
 // at 64, and runs 2.7x / 7x slower; the R copies here are straight-line code.)
