@@ -254,13 +254,17 @@ __device__ __forceinline__ double fast_sqrt(double q) {
 
 // a / b for b positive and normal (2^-1000 <= b < 2^1000): v_rcp_f64 (24 bits, measured by
 // tools/rcp_rsq_accuracy.hip), one Newton step (48 bits), quotient and one residual correction
-// (Markstein) -- the IEEE quotient but for rare last-bit cases.  Other b: the IEEE division.
+// (Markstein) -- the IEEE quotient but for rare last-bit cases.  Other b, and a non-finite
+// result (an infinite or NaN a, an overflowing quotient: the residual is then NaN), take the IEEE
+// division (tests/test_device_prims.py forces each case).
 __device__ __forceinline__ double div_pos(double a, double b) {
   if (!(hi_word(b) - 0x01700000u < 0x7D000000u)) return a / b;
   double y = __builtin_amdgcn_rcp(b);
   y = __builtin_fma(y, __builtin_fma(-b, y, 1.0), y);
   const double q0 = a * y;
-  return __builtin_fma(__builtin_fma(-b, q0, a), y, q0);
+  const double q = __builtin_fma(__builtin_fma(-b, q0, a), y, q0);
+  if (__builtin_expect(!__builtin_isfinite(q), 0)) return a / b;
+  return q;
 }
 
 // asin(x) (radians): t + t^3 P(t^2) on |x| < 1/2 (P: degree-12 fit, tools/gen_asin_poly.py, error

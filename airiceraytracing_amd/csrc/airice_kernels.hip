@@ -509,6 +509,7 @@ __device__ __forceinline__ double delta_D(const Slim& T, const Slim& R, const Ra
 struct Query {
   Slim tx, rtop, iceair, rx;
   double n_tx, n_rtop;
+  double ratio;  // n_tx / n_rtop: the first layer's Snell step (as the table's SegConst::ratio)
   int top, bot;
   double dist;
   double depth_pos;  // MinforLAng_params.antennadepth (> 0 in ice, 0 in air)
@@ -522,7 +523,10 @@ __device__ __forceinline__ double air_thd(const DevMedium& M, const Query& q, do
     L0 = __builtin_nan("");
     return 0.0;
   }
-  const double L = q.n_rtop * first_layer_v2(M, q.n_tx, q.n_rtop, theta);
+  // first_layer_v2 with the per-query ratio and the start-angle polynomial (theta in [90, 180]
+  // here; other angles go through ocml's sin inside sin_start)
+  const double v1 = sin_start((180 - theta) * M.d2r);
+  const double L = q.n_rtop * sin_asin(q.ratio * sin_asin(v1));
   L0 = L;
   const RayL RL = ray_L(M.A_air * M.A_air, L);
   double thd = 0.0;
@@ -601,6 +605,7 @@ __device__ __forceinline__ SolveResult solve_root(const DevMedium& M, const IceC
     q.rtop = q.tx;
     q.n_rtop = q.n_tx;
   }
+  q.ratio = q.n_tx / q.n_rtop;
   {
     const double e = exp(M.negC_ice * g.depth_pos);
     const double y = M.A_ice + M.B_ice * e;

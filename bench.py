@@ -84,7 +84,13 @@ def pmc_traffic(kernel: str):
 
 def main():
     args = parse()
-    os.environ.setdefault("NCCL_DEBUG", "WARN")  # keep RCCL's banner off stdout
+    os.environ.setdefault("NCCL_DEBUG", "WARN")
+    # stdout carries exactly one JSON line (rank 0): RCCL prints its version banner to fd 1 at
+    # communicator init, so fd 1 points at stderr for the whole run and the JSON line goes to the
+    # saved descriptor
+    sys.stdout.flush()
+    json_fd = os.dup(1)
+    os.dup2(2, 1)
     import torch
     import torch.distributed as dist
 
@@ -209,6 +215,30 @@ def main():
             "value": args.trace_n / (tms * 1e-3), "unit": "queries/s", "ms": tms,
             "solved_fraction": float((tout[:, 0] != -1000).double().mean().item())}
         del q, tout
+        # the scalar ctypes symbol itself (one query per call, host arrays, as the reference's
+        # TraceIceToAir.py calls it) on a subsample of the same queries
+        import ctypes
+        from airiceraytracing_amd import lib
+        d5 = cfg5_queries(2000, seed=777 + rank)
+        arr = (ctypes.c_double * 10)()
+        # Py_TraceIceToAir reads ./Atmosphere.dat, else $AIRICE_ATMOSPHERE (plain text)
+        import gzip
+        import tempfile
+        atm = os.path.join(tempfile.gettempdir(), f"airice_bench_atm_{os.getpid()}.dat")
+        with gzip.open(os.path.join(ROOT, "airiceraytracing_amd", "data",
+                                    "Atmosphere.dat.gz")) as fz, open(atm, "wb") as fo:
+            fo.write(fz.read())
+        os.environ.setdefault("AIRICE_ATMOSPHERE", atm)
+        lib().Py_TraceIceToAir(float(d5[0][0]), float(d5[1][0]), float(d5[2][0]),
+                               float(d5[3][0]), arr)  # first call parses the atmosphere
+        c0 = time.perf_counter()
+        for i in range(2000):
+            lib().Py_TraceIceToAir(float(d5[0][i]), float(d5[1][i]), float(d5[2][i]),
+                                   float(d5[3][i]), arr)
+        cus = (time.perf_counter() - c0) / 2000 * 1e6
+        os.remove(atm)
+        extra["pywrapper_trace"]["scalar_call_us"] = cus
+        extra["pywrapper_trace"]["scalar_sample"] = "2000 Py_TraceIceToAir ctypes calls"
     if not args.no_lookup:
         # batched GetHorizontalDistanceToIntersectionPoint_Table on this step's table (HBM
         # resident), cfg3-distributed queries (cm) for the table's own antenna
@@ -366,7 +396,8 @@ def main():
             **extra,
             "work_model": work,
         }
-        print(json.dumps(line))
+        sys.stdout.flush()
+        os.write(json_fd, (json.dumps(line) + "\n").encode())
     if distributed:
         dist.destroy_process_group()
 

@@ -35,6 +35,12 @@ def _inputs(n, seed=2024):
     q[:4] = [0.0, 1.0, 4.0, 0.25]
     a = rng.uniform(-2, 2, n)
     b = np.exp2(rng.uniform(-12, 12, n))
+    # rare branches of div_pos / log_ratio: b or a/b outside 2^+-1000, zeros, infinities, NaN
+    # (quotients stay finite: log_ratio takes log of the IEEE quotient)
+    a[4:16] = [1.0, 1.0, 0.0, 1.0, 2.0**-1050, 2.0**1020, 1.0, -1.0, np.inf, np.nan, 1.0,
+               2.0**-60]
+    b[4:16] = [2.0**-1010, 2.0**1010, 1.0, 0.0, 1.0, 2.0**10, np.inf, 0.0, 1.0, 1.0, np.nan,
+               2.0**-1074]
     x = np.concatenate([rng.uniform(-1, 1, n - 16),
                         [0.5, -0.5, np.nextafter(0.5, 0), np.nextafter(0.5, 1), 1.0, -1.0, 0.0,
                          -0.0, 1.0 + 2**-52, -1.5, np.nan, 0.74, 1e-300, 0.25, 0.999999, 0.7]])
@@ -59,18 +65,25 @@ def test_device_primitives(tmp_path):
     rs = (np.longdouble(1) / np.sqrt(q[nz].astype(np.longdouble))).astype(np.float64)
     ur = _ulps(o[nz, 2], rs)
     assert ur.max() <= 16.0, (ur.max(), q[nz][np.argmax(ur)])
-    assert _ulps(o[:, 3], a / b).max() <= 1.0
+    with np.errstate(all="ignore"):
+        q_ref = a / b
+    fq = np.isfinite(q_ref) & (q_ref != 0)
+    assert _ulps(o[fq, 3], q_ref[fq]).max() <= 1.0
+    assert np.array_equal(o[~fq, 3], q_ref[~fq], equal_nan=True)
     ref_asin = np.arcsin(x)
     fin = np.isfinite(ref_asin)
     assert np.array_equal(np.isnan(o[:, 4]), np.isnan(ref_asin))
     z = fin & (ref_asin != 0)
     assert _ulps(o[z, 4], ref_asin[z]).max() <= 3.0
     assert np.array_equal(o[fin & (ref_asin == 0), 4], ref_asin[fin & (ref_asin == 0)])
-    # log(a / b) for positive a: absolute error against long double
-    pos = a > 0
-    lr = np.log(a[pos].astype(np.longdouble) / b[pos].astype(np.longdouble)).astype(np.float64)
-    err = np.abs(o[pos, 5] - lr) / np.maximum(np.spacing(np.abs(lr)), 2.0**-53)
+    # log(a / b): log(a) - log(b) in long double (special values: -inf, +inf, NaN as the
+    # IEEE log of the quotient)
+    with np.errstate(all="ignore"):
+        lr = (np.log(a.astype(np.longdouble)) - np.log(b.astype(np.longdouble))).astype(np.float64)
+    fin = np.isfinite(lr)
+    err = np.abs(o[fin, 5] - lr[fin]) / np.maximum(np.spacing(np.abs(lr[fin])), 2.0**-53)
     assert err.max() <= 4.0, err.max()
+    assert np.array_equal(o[~fin, 5], lr[~fin], equal_nan=True), (a[~fin], b[~fin], o[~fin, 5])
     # mpmath sample for asin
     mpmath = pytest.importorskip("mpmath")
     mpmath.mp.prec = 100
