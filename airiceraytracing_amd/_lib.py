@@ -97,7 +97,11 @@ class LookupTable(ctypes.Structure):
         ("height_step", ctypes.c_double),
         ("total_height_steps", ctypes.c_int32),
         ("total_angle_steps", ctypes.c_int32),
+        ("entries", ctypes.c_void_p),
     ]
+
+
+LOOKUP_ENTRY_FLOATS = 12  # AIRICE_LOOKUP_ENTRY_FLOATS
 
 
 class SingleRayInfo(ctypes.Structure):
@@ -123,7 +127,7 @@ EXPORTED_SYMBOLS = (
     "airice_last_error", "airice_version", "airice_atmosphere_load", "airice_atmosphere_parse",
     "airice_nz_air", "airice_nz_ice", "airice_grid_init", "airice_table_launch",
     "airice_table_host", "airice_rays_launch", "airice_solve_launch", "airice_solve_host",
-    "airice_hdtip_launch", "airice_table_lookup_launch", "airice_single_ray_plan",
+    "airice_hdtip_launch", "airice_table_lookup_launch", "airice_lookup_pack", "airice_single_ray_plan",
     "airice_single_ray_launch", "airice_single_ray_host", "airice_trace_ice_to_air_launch",
     "airice_trace_ice_to_air_host", "airice_rtf_outputs", "airice_rtf_eval", "Py_TraceIceToAir", "airice_device_count", "airice_set_device", "airice_malloc",
     "airice_free", "airice_memcpy_h2d", "airice_memcpy_d2h", "airice_synchronize",
@@ -180,6 +184,7 @@ def lib() -> ctypes.CDLL:
         "airice_hdtip_launch": ([M, P, P, P, D, S, P, S, P, P], I),
         "airice_table_lookup_launch": ([M, ctypes.POINTER(LookupTable), P, P, P, D, S, P, S, P,
                                         P, P], I),
+        "airice_lookup_pack": ([ctypes.POINTER(LookupTable), P, P], I),
         "airice_single_ray_plan": ([M, D, D, D, D, ctypes.POINTER(SingleRayInfo)], I),
         "airice_single_ray_launch": ([M, D, D, D, D, P, P, P, S, P], I),
         "airice_single_ray_host": ([M, D, D, D, D, P, P, P, S], I),

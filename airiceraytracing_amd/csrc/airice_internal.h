@@ -31,6 +31,7 @@ int launch_hdtip(const DevMedium& M, const IceConsts& I, const double* src, cons
 int launch_lookup(const DevMedium& M, const IceConsts& I, const airice_lookup_table* t,
                   const double* src, const double* dist, const double* depth, double ice_cm,
                   size_t n, double* out, size_t ld, uint8_t* ok, uint8_t* flags, hipStream_t st);
+int launch_lookup_pack(const airice_lookup_table* t, float* entries, hipStream_t st);
 int launch_lookup_fallback(const DevMedium& M, const IceConsts& I, const double* src,
                            const double* dist, const double* depth, double ice_cm, size_t n,
                            double* out, size_t ld, uint8_t* ok, const uint8_t* flags,

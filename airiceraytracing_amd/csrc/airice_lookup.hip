@@ -6,7 +6,9 @@
 //                    FindClosestAirTxHeight (.cc:1033-1126)  row of the Tx height and the
 //                                                            valid-THD span of that row,
 //                    FindClosestTHD         (.cc:1128-1169)  8 bisection steps + linear scan,
-//                    GetParValues           (.cc:1172-1302)  10 columns at 2 heights,
+//                    GetParValues           (.cc:1172-1302)  10 columns at 2 heights
+//                                                            (one 48-byte packed record per
+//                                                            entry when the table is packed),
 //                    _Table                 (.cc:1305-1462)  interpolation in height, checks.
 //                  Lanes that hit the one-sided extrapolation case (.cc:1418) are flagged and
 //                  finished by the masked minimizer pass (launch_lookup_fallback,
@@ -32,10 +34,39 @@ constexpr int kLkBlock = 256;
 
 struct LkTable {
   const float* t;
+  const float* e;  // packed entries (airice_lookup_pack) or nullptr
   long long ld, n;
   double stop_h, step_h;
   int hsteps, asteps;
 };
+
+// One table entry's 11 columns, from the packed copy when there is one (three 16-byte loads of
+// one 48-byte record) or else column by column.  Out-of-range entries: NaN, flagged, as lk_at.
+struct LkRec {
+  float c[AIRICE_LOOKUP_ENTRY_FLOATS];
+};
+
+__device__ __forceinline__ LkRec lk_rec(const LkTable& T, long long i, int& fl) {
+  LkRec r;
+  if (i < 0 || i >= T.n) {
+    fl |= AIRICE_LOOKUP_UNPINNED;
+#pragma unroll
+    for (int c = 0; c < AIRICE_LOOKUP_ENTRY_FLOATS; ++c) r.c[c] = __builtin_nanf("");
+    return r;
+  }
+  if (T.e != nullptr) {
+    const float4* p = reinterpret_cast<const float4*>(T.e + (long long)AIRICE_LOOKUP_ENTRY_FLOATS * i);
+    const float4 a = p[0], b = p[1], d = p[2];
+    r.c[0] = a.x, r.c[1] = a.y, r.c[2] = a.z, r.c[3] = a.w;
+    r.c[4] = b.x, r.c[5] = b.y, r.c[6] = b.z, r.c[7] = b.w;
+    r.c[8] = d.x, r.c[9] = d.y, r.c[10] = d.z, r.c[11] = d.w;
+    return r;
+  }
+#pragma unroll
+  for (int c = 0; c < 11; ++c) r.c[c] = T.t[(long long)c * T.ld + i];
+  r.c[11] = 0.0f;
+  return r;
+}
 
 __device__ __forceinline__ double lk_at(const LkTable& T, int c, long long i, int& fl) {
   if (i < 0 || i >= T.n) {
@@ -146,13 +177,14 @@ __device__ __forceinline__ void row_params(const LkTable& T, double D, long long
     *closest = b.c;
     if (b.c != 0) {
       const double x1 = lk_at(T, 1, b.s, fl), x2 = lk_at(T, 1, b.e, fl);
+      const LkRec rs = lk_rec(T, b.s, fl), re = lk_rec(T, b.e, fl);
 #pragma unroll
       for (int ip = 0; ip < 10; ++ip)
-        par[ip] = lk_interp(D, x1, lk_at(T, 1 + ip, b.s, fl), x2, lk_at(T, 1 + ip, b.e, fl));
+        par[ip] = lk_interp(D, x1, (double)rs.c[1 + ip], x2, (double)re.c[1 + ip]);
     } else {
-      const long long i = b.s + 1;
+      const LkRec r = lk_rec(T, b.s + 1, fl);
 #pragma unroll
-      for (int ip = 0; ip < 10; ++ip) par[ip] = lk_at(T, 1 + ip, i, fl);
+      for (int ip = 0; ip < 10; ++ip) par[ip] = (double)r.c[1 + ip];
     }
   } else {
 #pragma unroll
@@ -255,7 +287,32 @@ __global__ __launch_bounds__(kLkBlock) void lookup_kernel(LkTable T, const doubl
   flags[k] = (uint8_t)fl;
 }
 
+// airice_lookup_pack: one lane per entry; each column read is coalesced across the wave and each
+// wave writes one contiguous 3 KB run of records.
+__global__ __launch_bounds__(kLkBlock) void lookup_pack_kernel(const float* __restrict__ t,
+                                                               long long ld, long long n,
+                                                               float* __restrict__ e) {
+  const long long i = (long long)blockIdx.x * kLkBlock + threadIdx.x;
+  if (i >= n) return;
+  float c[AIRICE_LOOKUP_ENTRY_FLOATS];
+#pragma unroll
+  for (int k = 0; k < 11; ++k) c[k] = t[(long long)k * ld + i];
+  c[11] = 0.0f;
+  float4* p = reinterpret_cast<float4*>(e + (long long)AIRICE_LOOKUP_ENTRY_FLOATS * i);
+  p[0] = make_float4(c[0], c[1], c[2], c[3]);
+  p[1] = make_float4(c[4], c[5], c[6], c[7]);
+  p[2] = make_float4(c[8], c[9], c[10], c[11]);
+}
+
 }  // namespace
+
+int launch_lookup_pack(const airice_lookup_table* t, float* e, hipStream_t st) {
+  const long long n = (long long)t->n_entries;
+  if (n == 0) return AIRICE_OK;
+  hipLaunchKernelGGL(lookup_pack_kernel, dim3((unsigned)((n + kLkBlock - 1) / kLkBlock)),
+                     dim3(kLkBlock), 0, st, t->table, (long long)t->ld, n, e);
+  return hipGetLastError() == hipSuccess ? AIRICE_OK : AIRICE_EHIP;
+}
 
 int launch_lookup(const DevMedium& M, const IceConsts& I, const airice_lookup_table* t,
                   const double* src, const double* dist, const double* depth, double ice_cm,
@@ -263,6 +320,7 @@ int launch_lookup(const DevMedium& M, const IceConsts& I, const airice_lookup_ta
   if (n == 0) return AIRICE_OK;
   LkTable T;
   T.t = t->table;
+  T.e = t->entries;
   T.ld = (long long)t->ld;
   T.n = (long long)t->n_entries;
   T.stop_h = t->loop_stop_height;

@@ -515,7 +515,8 @@ int airice_table_lookup_launch(const airice_medium* m, const airice_lookup_table
     return AIRICE_EINVAL;
   }
   if (t->n_entries == 0 || t->ld < t->n_entries || t->total_angle_steps < 1 ||
-      t->total_height_steps < 1 || !(t->height_step > 0)) {
+      t->total_height_steps < 1 || !(t->height_step > 0) ||
+      (reinterpret_cast<uintptr_t>(t->entries) & 15) != 0) {
     set_error("invalid lookup table description");
     return AIRICE_EINVAL;
   }
@@ -527,6 +528,20 @@ int airice_table_lookup_launch(const airice_medium* m, const airice_lookup_table
   rc = launch_lookup(M, I, t, d_src_cm, d_dist_cm, d_depth_cm, ice_cm, n, d_out, ld, d_ok,
                      d_flags, (hipStream_t)stream);
   if (rc) set_error("lookup launch failed: %s", hipGetErrorString(hipGetLastError()));
+  return rc;
+}
+
+int airice_lookup_pack(const airice_lookup_table* t, float* d_entries, void* stream) {
+  if (t == nullptr || t->table == nullptr || d_entries == nullptr) {
+    set_error("null argument");
+    return AIRICE_EINVAL;
+  }
+  if (t->ld < t->n_entries || (reinterpret_cast<uintptr_t>(d_entries) & 15) != 0) {
+    set_error("ld < n_entries or entries not 16-byte aligned");
+    return AIRICE_EINVAL;
+  }
+  const int rc = launch_lookup_pack(t, d_entries, (hipStream_t)stream);
+  if (rc) set_error("lookup pack failed: %s", hipGetErrorString(hipGetLastError()));
   return rc;
 }
 

@@ -55,6 +55,7 @@ struct DevTable {
   const float* host0 = nullptr;  // AllTableAllAntData[i][0].data() when mirrored
   size_t n = 0;
   float* dev = nullptr;
+  float* packed = nullptr;  // airice_lookup_pack copy, made at the first lookup
 };
 std::vector<DevTable> g_tables;
 
@@ -72,7 +73,9 @@ const float* device_table(int index, size_t* n_out) {
   *n_out = n;
   if (t.dev != nullptr && t.host0 == cols[0].data() && t.n == n) return t.dev;
   if (t.dev != nullptr) (void)hipFree(t.dev);
+  if (t.packed != nullptr) (void)hipFree(t.packed);
   t.dev = nullptr;
+  t.packed = nullptr;
   if (hipMalloc(&t.dev, sizeof(float) * AIRICE_TABLE_COLUMNS * n) != hipSuccess) die("hipMalloc");
   for (int c = 0; c < AIRICE_TABLE_COLUMNS; ++c) {
     if (cols[c].size() != n) die("table lookup (ragged table)");
@@ -87,6 +90,7 @@ const float* device_table(int index, size_t* n_out) {
 
 airice_lookup_table lookup_desc(const float* dev, size_t n) {
   airice_lookup_table t;
+  t.entries = nullptr;
   t.table = dev;
   t.ld = n;
   t.n_entries = n;
@@ -243,6 +247,8 @@ int MakeRayTracingTable(double AntennaDepth, double IceLayerHeight, int AntennaN
   const size_t index = AllTableAllAntData.size() - 1;
   if (g_tables.size() <= index) g_tables.resize(index + 1);
   if (g_tables[index].dev != nullptr) (void)hipFree(g_tables[index].dev);
+  if (g_tables[index].packed != nullptr) (void)hipFree(g_tables[index].packed);
+  g_tables[index].packed = nullptr;
   g_tables[index].dev = dt;
   g_tables[index].host0 = AllTableAllAntData[index][0].data();
   g_tables[index].n = n;
@@ -297,7 +303,14 @@ void TableLookupBatch(const double* SrcHeightASL, const double* HorizontalDistan
     die("hipMemcpy");
   uint8_t* dok = reinterpret_cast<uint8_t*>(d + 12 * n);
   uint8_t* dfl = dok + n;
-  const airice_lookup_table t = lookup_desc(dev, entries);
+  airice_lookup_table t = lookup_desc(dev, entries);
+  DevTable& dt = g_tables[TableIndex];
+  if (dt.packed == nullptr) {
+    if (hipMalloc(&dt.packed, sizeof(float) * AIRICE_LOOKUP_ENTRY_FLOATS * entries) != hipSuccess ||
+        airice_lookup_pack(&t, dt.packed, nullptr) != AIRICE_OK)
+      die("airice_lookup_pack");
+  }
+  t.entries = dt.packed;
   if (airice_table_lookup_launch(&m, &t, d, d + n, d + 2 * n, IceLayerHeight, n, d + 3 * n, n,
                                  dok, dfl, nullptr) != AIRICE_OK)
     die("GetHorizontalDistanceToIntersectionPoint_Table");

@@ -132,6 +132,19 @@ class AirIceSolver:
         t.total_angle_steps = grid.angle_steps
         return t
 
+    @staticmethod
+    def lookup_pack(lt: LookupTable, stream=None):
+        """airice_lookup_pack: a packed copy of the table (12 floats per entry, torch tensor on
+        the table's device) that ``lt`` then reads; the tensor is kept on ``lt``."""
+        import torch
+        packed = torch.empty(int(lt.n_entries) * _lib.LOOKUP_ENTRY_FLOATS, dtype=torch.float32,
+                             device=torch.device("cuda", torch.cuda.current_device()))
+        check(lib().airice_lookup_pack(ctypes.byref(lt), ptr(packed), _stream_handle(stream)),
+              "airice_lookup_pack")
+        lt.entries = ptr(packed).value
+        lt._packed = packed
+        return packed
+
     def table_lookup_device(self, lt: LookupTable, src_cm, dist_cm, depth_cm, ice_cm: float,
                             out, ok, flags, ld: int | None = None, stream=None) -> None:
         """Batched GetHorizontalDistanceToIntersectionPoint_Table (.cc:1305-1462): out is the

@@ -251,6 +251,16 @@ def main():
         lok = torch.empty(args.lookup_n, dtype=torch.uint8, device=dev)
         lfl = torch.empty(args.lookup_n, dtype=torch.uint8, device=dev)
         lt = solver.lookup_table(table, grid)
+        # packed copy for the lookup (airice_lookup_pack, once per table; timed separately)
+        solver.lookup_pack(lt, stream=stream)
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        for _ in range(10):
+            solver.lookup_pack(lt, stream=stream)
+        e1.record(stream)
+        torch.cuda.synchronize()
+        pack_ms = e0.elapsed_time(e1) / 10
 
         def lookup():
             solver.table_lookup_device(lt, src, dcm, dep, CFG2["ice_cm"], lout, lok, lfl,
@@ -270,7 +280,8 @@ def main():
             "metric": "GetHorizontalDistanceToIntersectionPoint_Table lookups/s (1e6 cfg3 "
                       "queries on the cfg2 table, incl. the minimizer fallback pass)",
             "value": args.lookup_n / (lms * 1e-3), "unit": "lookups/s", "ms": lms,
-            "ok_fraction": float(lok.cpu().numpy().mean())}
+            "ok_fraction": float(lok.cpu().numpy().mean()),
+            "pack_ms": pack_ms, "packed": True}
     if not args.no_pcie:
         # host-buffer callers (AllTableAllAntData is host memory): table build + D2H copy of the
         # 11 float columns into pinned memory, in stream order; never the headline value

@@ -163,7 +163,18 @@ typedef struct airice_lookup_table {
   double height_step;         /* m */
   int32_t total_height_steps;
   int32_t total_angle_steps;
+  const float *entries;       /* optional device copy from airice_lookup_pack (NULL: the lookup
+                                 reads the columns only); same values, fewer cache lines */
 } airice_lookup_table;
+
+/* Floats per packed entry: the 11 columns of one table entry, then one 0 (48 B, 16 B aligned). */
+#define AIRICE_LOOKUP_ENTRY_FLOATS 12
+
+/* Pack one antenna's table for the lookup: d_entries[12*i + c] = column c of entry i (c < 11),
+ * n_entries * 12 floats, 16-byte aligned.  The lookup reads the 10 interpolated parameters of a
+ * table entry from 48 contiguous bytes instead of 10 columns ld floats apart; results are
+ * identical.  Stream-ordered; run once per table, then set t->entries = d_entries. */
+int airice_lookup_pack(const airice_lookup_table *t, float *d_entries, void *stream);
 
 #define AIRICE_LOOKUP_FALLBACK 1 /* the minimizer fallback ran (.cc:1418-1420) */
 #define AIRICE_LOOKUP_UNPINNED 2 /* the reference reads uninitialised/out-of-range memory here:

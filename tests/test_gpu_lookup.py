@@ -55,6 +55,19 @@ def _run_case(solver, oracle_medium, depth_cm, hstep, a0, a1, astep, nq, seed):
                                stream=torch.cuda.current_stream())
     torch.cuda.synchronize()
     out, ok, fl = out.cpu().numpy(), ok.cpu().numpy(), fl.cpu().numpy()
+    # the packed table (airice_lookup_pack): the same floats from 48-byte records -> identical
+    lp = solver.lookup_table(table, g)
+    solver.lookup_pack(lp, stream=torch.cuda.current_stream())
+    out_p = torch.empty_like(torch.from_numpy(out)).to(dev)
+    ok_p = torch.empty(n, dtype=torch.uint8, device=dev)
+    fl_p = torch.empty(n, dtype=torch.uint8, device=dev)
+    solver.table_lookup_device(lp, ts, td, tp, ICE_CM, out_p, ok_p, fl_p,
+                               stream=torch.cuda.current_stream())
+    torch.cuda.synchronize()
+    assert np.array_equal(out_p.cpu().numpy(), out, equal_nan=True)
+    assert np.array_equal(ok_p.cpu().numpy(), ok) and np.array_equal(fl_p.cpu().numpy(), fl)
+    packed = lp._packed.cpu().numpy().reshape(-1, 12)
+    assert np.array_equal(packed[:, :11].T, host, equal_nan=True) and not packed[:, 11].any()
     rout, rok, rfl = oracle.table_lookup_batch(oracle_medium, oracle.lookup_table(host, og),
                                                src, dist, dep, ICE_CM, nthreads=NTHREADS)
     assert np.array_equal(fl, rfl), np.flatnonzero(fl != rfl)[:10]
