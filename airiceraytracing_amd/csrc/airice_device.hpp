@@ -355,9 +355,10 @@ __device__ __forceinline__ double log_ratio_ieee(double a, double b) {
   return (a > 0.0 && b > 0.0) ? tlog(a / b) : special;
 }
 
-__device__ __forceinline__ double log_ratio(double a, double b) {
+__device__ __forceinline__ double log_ratio(double a, double b,
+                                            const double* tab = &kLogTable[0][0]) {
   bool ok;
-  const double r = log_ratio_fast(a, b, &kLogTable[0][0], ok);
+  const double r = log_ratio_fast(a, b, tab, ok);
   if (ok) return r;
   return log_ratio_ieee(a, b);
 }

@@ -499,9 +499,11 @@ __device__ __forceinline__ double stop_n(const DevMedium& M, int l) {
 
 
 // fDnfR(R) - fDnfR(T) with one logarithm when both ends share C (identity (5)).
-__device__ __forceinline__ double delta_D(const Slim& T, const Slim& R, const RayL& RL) {
+// tab: the log table (the roots kernel's LDS copy, else the global one).
+__device__ __forceinline__ double delta_D(const Slim& T, const Slim& R, const RayL& RL,
+                                          const double* tab = &kLogTable[0][0]) {
   const double syR = fast_sqrt(R.y2 - RL.LL), syT = fast_sqrt(T.y2 - RL.LL);
-  const double d1 = log_ratio(R.Ay - RL.LL + RL.sAL * syR, T.Ay - RL.LL + RL.sAL * syT);
+  const double d1 = log_ratio(R.Ay - RL.LL + RL.sAL * syR, T.Ay - RL.LL + RL.sAL * syT, tab);
   return (RL.L * R.invC) * RL.rsAL * ((R.Cx - T.Cx) - d1);
 }
 
@@ -518,7 +520,7 @@ struct Query {
 // Sum of per-layer horizontal distances in air for launch angle theta (THD only: the time
 // and geometric-path terms do not enter f).  Returns L0 through the reference.
 __device__ __forceinline__ double air_thd(const DevMedium& M, const Query& q, double theta,
-                                          double& L0) {
+                                          double& L0, const double* tab) {
   if (q.top < q.bot) {  // no layer: the reference reads unset output slots (UB)
     L0 = __builtin_nan("");
     return 0.0;
@@ -535,7 +537,7 @@ __device__ __forceinline__ double air_thd(const DevMedium& M, const Query& q, do
     if (il > q.top || il < q.bot) continue;
     const Slim T = pick(il == q.top, q.tx, slim(M.start[il]));
     const Slim R = pick(il == q.top, q.rtop, pick(il == q.bot, q.iceair, slim(M.stop[il])));
-    double x1 = delta_D(T, R, RL);
+    double x1 = delta_D(T, R, RL, tab);
     x1 *= -1;
     thd += x1;
   }
@@ -586,7 +588,8 @@ enum { PH_PROBE = 0, PH_FLO = 1, PH_FHI = 2, PH_EST = 3, PH_G1 = 4, PH_G2 = 5, P
        PH_DONE = 7 };
 
 __device__ __forceinline__ SolveResult solve_root(const DevMedium& M, const IceConsts& I,
-                                                  const Geometry& g, double thR, bool exact) {
+                                                  const Geometry& g, double thR, bool exact,
+                                                  const double* tab) {
   int status = 0;
   Query q;
   q.depth_pos = g.depth_pos;
@@ -755,11 +758,11 @@ __device__ __forceinline__ SolveResult solve_root(const DevMedium& M, const IceC
     ++n_eval;
     n_inside += (phase == PH_BISECT);
     double L;
-    const double thd_air = air_thd(M, q, x, L);
+    const double thd_air = air_thd(M, q, x, L, tab);
     double thd_ice = 0;
     if (q.depth_pos != 0) {
       const RayL RL = ray_L(M.A_ice * M.A_ice, L);
-      thd_ice += delta_D(slim(I.ice0), q.rx, RL);
+      thd_ice += delta_D(slim(I.ice0), q.rx, RL, tab);
     }
     const double f = (q.dist - (thd_ice + thd_air));
     if (phase == PH_PROBE) {
@@ -1011,6 +1014,14 @@ __global__ __launch_bounds__(kRootsBlock, AIRICE_ROOTS_WAVES) void roots_kernel(
                                                        Park park) {
   __shared__ int s_count[kSortBuckets + 1];
   __shared__ int s_slot[kRootsBlock];
+  // the log table in LDS (one 16-byte entry per thread), as in table_kernel: every evaluation's
+  // log ratios read it instead of global memory
+  __shared__ __align__(16) double s_logtab[1 << kLogTableBits][2];
+  static_assert(kRootsBlock >= (1 << kLogTableBits), "one table entry per thread");
+  if (threadIdx.x < (1u << kLogTableBits)) {
+    s_logtab[threadIdx.x][0] = kLogTable[threadIdx.x][0];
+    s_logtab[threadIdx.x][1] = kLogTable[threadIdx.x][1];
+  }
   const long long k0 = (long long)blockIdx.x * kRootsBlock;
   const long long kt = k0 + threadIdx.x;
   if (threadIdx.x <= kSortBuckets) s_count[threadIdx.x] = 0;
@@ -1041,7 +1052,7 @@ __global__ __launch_bounds__(kRootsBlock, AIRICE_ROOTS_WAVES) void roots_kernel(
   if (IN == IN_CM100 && !(Q.mask[k] & AIRICE_LOOKUP_FALLBACK)) return;
   double thR;
   const Geometry g = load_query<IN>(M, Q, k, thR);
-  const SolveResult r = solve_root(M, I, g, thR, park.exact != 0);
+  const SolveResult r = solve_root(M, I, g, thR, park.exact != 0, &s_logtab[0][0]);
   park.root[k * park.stride] = r.root;
   park.status[k * park.stride] = (double)r.status;
   if (park.stats != nullptr) {
