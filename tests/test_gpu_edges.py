@@ -1,0 +1,66 @@
+"""Boundary cases of the C-ABI entry points on the GPU: empty batches (n = 0 launches nothing and
+returns AIRICE_OK), degenerate grids (one launch angle, one Tx row, a single ray), and a grid whose
+row count is not a multiple of anything the kernel tiles by -- each compared with the oracle."""
+import numpy as np
+import pytest
+
+import oracle
+from tests import parity
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def solver():
+    from airiceraytracing_amd import AirIceSolver
+    return AirIceSolver()
+
+
+@pytest.fixture(scope="module")
+def solver_py():
+    from airiceraytracing_amd import AirIceSolver, VARIANT_PYWRAPPER
+    return AirIceSolver(variant=VARIANT_PYWRAPPER)
+
+
+def test_empty_batches(solver, solver_py):
+    import torch
+    dev = torch.device("cuda:0")
+    e = np.zeros(0)
+    out, st = solver.solve_host(e, e, e, 3000.0)
+    assert out.shape[-1] == 0 and st.size == 0
+    rows = solver_py.trace_ice_to_air_host(e, e, e, e)
+    assert rows.shape == (0, 10)
+    z = torch.zeros(0, dtype=torch.float64, device=dev)
+    o = torch.zeros((18, 0), dtype=torch.float64, device=dev)
+    solver.rays_device(z, z, 3000.0, -200.0, True, o)
+    torch.cuda.synchronize()
+
+
+@pytest.mark.parametrize("depth_cm,hstep,a0,a1,astep", [
+    (-20000.0, 20.0, 180.0, 180.0, 0.5),    # one launch angle (the forced last column, 180 deg)
+    (-20000.0, 97000.0, 92.0, 180.0, 0.5),  # two Tx rows: 100 km and the forced 3 km stop row
+    (-20000.0, 97000.0, 180.0, 180.0, 0.5),  # two rays
+    (-1234.0, 37.0, 90.1, 180.0, 0.37),     # ragged: 2,622 rows x 243 angles
+])
+def test_degenerate_and_ragged_grids(solver, oracle_medium, depth_cm, hstep, a0, a1, astep):
+    from airiceraytracing_amd import make_grid
+    g = make_grid(depth_cm, 300000.0, hstep, a0, a1, astep)
+    og = oracle.grid_init(depth_cm, 300000.0, hstep, a0, a1, astep)
+    assert (g.height_steps, g.angle_steps) == (og.height_steps, og.angle_steps)
+    table, full = solver.table_host(g, full=True)
+    ot, of = oracle.table_rows(oracle_medium, og, 0, og.height_steps, full=True, nthreads=16)
+    rep = parity.compare_columns(full, of, parity.RAY_FLOORS)
+    assert rep["ok"], rep
+    assert parity.float_ulp_diff(table, ot) <= 1
+
+
+def test_single_query_batches(solver, oracle_medium):
+    """n = 1 through the batched minimizer (one lane in a 1024-query sort block)."""
+    for txh, dist, depth in ((5000.0, 1000.0, -200.0), (99999.0, 49999.0, -300.0),
+                             (3001.0, 0.0, -0.5), (20000.0, 5000.0, 10.0)):
+        out, st = solver.solve_host(np.array([txh]), np.array([dist]), np.array([depth]), 3000.0)
+        ref, rst = oracle.solve_batch(oracle_medium, np.array([txh]), np.array([dist]),
+                                      np.array([depth]), 3000.0)
+        mask = (rst & oracle.SOLVE_UNPINNED) == 0
+        rep = parity.compare_columns(out, ref, parity.SOLVE_FLOORS, mask=mask)
+        assert rep["ok"], (txh, dist, depth, rep)
