@@ -47,6 +47,14 @@ constexpr int kTableBlock = AIRICE_TABLE_BS;
 // oldest-first, so the SIMDs still drain one wave at a time (tools/wave_timeline.py) -- hence the
 // window is empty by default and R = 2 is reachable only through AIRICE_TABLE_RPL=2 or building
 // with e.g. -DAIRICE_TWO_RAY_MIN=524288 -DAIRICE_TWO_RAY_MAX=917504.
+// AIRICE_TABLE_R2=0 leaves the R = 2 kernel out of the build (co-compiled template variants can
+// perturb each other's register allocation)
+#ifndef AIRICE_ROWCONST_ALIGN16
+#define AIRICE_ROWCONST_ALIGN16 0
+#endif
+#ifndef AIRICE_TABLE_R2
+#define AIRICE_TABLE_R2 1
+#endif
 #ifndef AIRICE_TWO_RAY_MIN
 #define AIRICE_TWO_RAY_MIN 0
 #endif
@@ -116,7 +124,11 @@ __device__ __forceinline__ TopEnd topend_of(const IceConsts& I, int top) {
 // Everything of a ray that depends on its Tx height only: the Tx layer and the Tx layer's
 // segment folded like the lower layers' (Tx endpoint -> the layer's stop end, or the ice).  The
 // table computes it once per row into LDS (a block spans few rows); other launches per lane.
-struct RowConst {
+struct
+#if AIRICE_ROWCONST_ALIGN16
+__attribute__((aligned(16)))
+#endif
+RowConst {
   SegConst seg;  // Tx endpoint -> stop end of the Tx layer (zero-length case resolved)
   double H;
   int top;       // MaxLayers - SkipLayersAbove - 1
@@ -1245,15 +1257,16 @@ int launch_table(const DevMedium& M, const IceConsts& I, const airice_grid* g, i
     done += rows;
     // two rays per lane when one ray per lane would take more than one round of resident waves
     // but two fit in one (kTwoRayMin..kTwoRayMax rays; the double-output parity launches keep one)
-    const int R = force_r ? force_r
-                          : (full == nullptr && A.n > kTwoRayMin && A.n <= kTwoRayMax ? 2 : 1);
+    const int R = !AIRICE_TABLE_R2 ? 1
+                  : force_r ? force_r
+                            : (full == nullptr && A.n > kTwoRayMin && A.n <= kTwoRayMax ? 2 : 1);
     A.half = R == 2 ? (A.n + 1) / 2 : A.n;
     const size_t lds = sizeof(RowConst) * (size_t)A.rows_per_block * R;
     const unsigned blocks = (unsigned)((A.half + kTableBlock - 1) / kTableBlock);
     if (trace_path == nullptr) {
-      if (R == 2)
-        hipLaunchKernelGGL((table_kernel<kTableBlock, 2, false>), dim3(blocks), dim3(kTableBlock),
-                           lds, st, M, I, A, tab, full, nullptr);
+      if (AIRICE_TABLE_R2 && R == 2)
+        hipLaunchKernelGGL((table_kernel<kTableBlock, 1 + AIRICE_TABLE_R2, false>), dim3(blocks),
+                           dim3(kTableBlock), lds, st, M, I, A, tab, full, nullptr);
       else
         hipLaunchKernelGGL((table_kernel<kTableBlock, 1, false>), dim3(blocks), dim3(kTableBlock),
                            lds, st, M, I, A, tab, full, nullptr);
@@ -1264,9 +1277,9 @@ int launch_table(const DevMedium& M, const IceConsts& I, const airice_grid* g, i
     const long long nw = (long long)blocks * (kTableBlock / 64);
     WaveTrace* dtr = nullptr;
     if (hipMalloc(&dtr, sizeof(WaveTrace) * nw) != hipSuccess) return AIRICE_EHIP;
-    if (R == 2)
-      hipLaunchKernelGGL((table_kernel<kTableBlock, 2, true>), dim3(blocks), dim3(kTableBlock), lds,
-                         st, M, I, A, tab, full, dtr);
+    if (AIRICE_TABLE_R2 && R == 2)
+      hipLaunchKernelGGL((table_kernel<kTableBlock, 1 + AIRICE_TABLE_R2, true>), dim3(blocks),
+                         dim3(kTableBlock), lds, st, M, I, A, tab, full, dtr);
     else
       hipLaunchKernelGGL((table_kernel<kTableBlock, 1, true>), dim3(blocks), dim3(kTableBlock), lds,
                          st, M, I, A, tab, full, dtr);
