@@ -190,6 +190,215 @@ __device__ double rtf_min_launch(const DevMedium& M, double x, double AirTxHeigh
   return D - (thd_ice + thd_air);
 }
 
+// gsl_root_fsolver_brent (GNU GSL 2.x roots/brent.c: brent_init / brent_iterate) driven by
+// RayTracingFunctions::FindFunctionRoot (RayTracingFunctions.cc:256-290: set, then
+// {iterate; root; x_lower; x_upper; gsl_root_test_interval(lo, hi, 0, tol)} while CONTINUE and
+// iter < max_iter, the last root returned).  As for the bisection: a
+// non-finite f at a bracket end makes brent_init return before the state is stored (the
+// reference then iterates on uninitialised malloc memory) -- modelled as a zero state and flagged
+// AIRICE_SOLVE_NONFINITE_END; a non-finite f at an iterate returns EBADFUNC with nothing stored
+// (AIRICE_SOLVE_STALE_MID); lower > upper makes gsl_root_fsolver_set fail (AIRICE_SOLVE_BAD_BRACKET,
+// root 0).  The same restatement is oracle/airice_oracle.c or_brent.
+struct RtfBrent {
+  double root;
+  int status, iters;
+};
+
+template <class F>
+__device__ RtfBrent gsl_brent(F f, double x_lo, double x_hi, double tolerance, int max_iter) {
+  const double kEps = 2.2204460492503131e-16;  // GSL_DBL_EPSILON
+  RtfBrent R{0.0, 0, 0};
+  if (x_lo > x_hi) {
+    R.status |= AIRICE_SOLVE_BAD_BRACKET;
+    return R;
+  }
+  double root = 0.5 * (x_lo + x_hi);
+  double lo = x_lo, hi = x_hi;
+  double a = 0, b = 0, c = 0, d = 0, e = 0, fa = 0, fb = 0, fc = 0;
+  const double f_lower = f(x_lo);
+  double f_upper = 0;
+  bool ok = isfinite(f_lower);
+  if (ok) {
+    f_upper = f(x_hi);
+    ok = isfinite(f_upper);
+  }
+  if (!ok) {
+    R.status |= AIRICE_SOLVE_NONFINITE_END;
+  } else {
+    a = x_lo, fa = f_lower;
+    b = x_hi, fb = f_upper;
+    c = x_hi, fc = f_upper;
+    d = x_hi - x_lo;
+    e = x_hi - x_lo;
+  }
+  int iter = 0;
+  bool cont = true;
+  do {
+    iter++;
+    // brent_iterate on local copies; the state is stored only when the new point is finite
+    double la = a, lb = b, lc = c, ld = d, le = e, lfa = fa, lfb = fb, lfc = fc;
+    bool ac_equal = false;
+    if ((lfb < 0 && lfc < 0) || (lfb > 0 && lfc > 0)) {
+      ac_equal = true;
+      lc = la;
+      lfc = lfa;
+      ld = lb - la;
+      le = lb - la;
+    }
+    if (fabs(lfc) < fabs(lfb)) {
+      ac_equal = true;
+      la = lb;
+      lb = lc;
+      lc = la;
+      lfa = lfb;
+      lfb = lfc;
+      lfc = lfa;
+    }
+    const double tol = 0.5 * kEps * fabs(lb);
+    const double m = 0.5 * (lc - lb);
+    if (lfb == 0) {
+      root = lb;
+      lo = lb;
+      hi = lb;
+    } else if (fabs(m) <= tol) {
+      root = lb;
+      if (lb < lc) {
+        lo = lb;
+        hi = lc;
+      } else {
+        lo = lc;
+        hi = lb;
+      }
+    } else {
+      if (fabs(le) < tol || fabs(lfa) <= fabs(lfb)) {
+        ld = m;  // bisection
+        le = m;
+      } else {
+        double p, q, r;  // inverse cubic interpolation
+        const double sr = lfb / lfa;
+        if (ac_equal) {
+          p = 2 * m * sr;
+          q = 1 - sr;
+        } else {
+          q = lfa / lfc;
+          r = lfb / lfc;
+          p = sr * (2 * m * q * (q - r) - (lb - la) * (r - 1));
+          q = (q - 1) * (r - 1) * (sr - 1);
+        }
+        if (p > 0)
+          q = -q;
+        else
+          p = -p;
+        const double t1 = 3 * m * q - fabs(tol * q), t2 = fabs(le * q);
+        if (2 * p < (t1 < t2 ? t1 : t2)) {  // GSL_MIN
+          le = ld;
+          ld = p / q;
+        } else {
+          ld = m;
+          le = m;
+        }
+      }
+      la = lb;
+      lfa = lfb;
+      if (fabs(ld) > tol)
+        lb += ld;
+      else
+        lb += (m > 0 ? +tol : -tol);
+      const double fnew = f(lb);
+      if (!isfinite(fnew)) {
+        R.status |= AIRICE_SOLVE_STALE_MID;
+      } else {
+        lfb = fnew;
+        a = la, b = lb, c = lc, d = ld, e = le, fa = lfa, fb = lfb, fc = lfc;
+        root = lb;
+        double cc = lc;
+        if ((lfb < 0 && lfc < 0) || (lfb > 0 && lfc > 0)) cc = la;
+        if (lb < cc) {
+          lo = lb;
+          hi = cc;
+        } else {
+          lo = cc;
+          hi = lb;
+        }
+      }
+    }
+    // gsl_root_test_interval(lo, hi, 0, tolerance)
+    if (lo > hi) {
+      cont = false;
+    } else {
+      const double min_abs = ((lo > 0.0 && hi > 0.0) || (lo < 0.0 && hi < 0.0))
+                                 ? (fabs(lo) < fabs(hi) ? fabs(lo) : fabs(hi))
+                                 : 0.0;
+      cont = !(fabs(hi - lo) < 0 + tolerance * min_abs);
+    }
+  } while (cont && iter < max_iter);
+  if (cont) R.status |= AIRICE_SOLVE_MAXITER;
+  R.root = root;
+  R.iters = iter;
+  return R;
+}
+
+// Air2IceRayTracing CLI solve (Air2IceRayTracing.C:56-185; StoreRayPath is false there).
+__device__ void rtf_air2ice(const DevMedium& M, double AirTxHeight, double HorizontalDistance,
+                            double IceLayerHeight, double AntennaDepth, double* o) {
+  const double StraightAngle =
+      180 - (atan(HorizontalDistance / (AirTxHeight - IceLayerHeight + AntennaDepth)) * M.r2d);
+  double startanglelim = StraightAngle - 16;
+  double endanglelim = StraightAngle;
+  int probes = 0;
+  double air[4 * kMaxLayers + 1];
+  if (startanglelim < 90.00) {
+    startanglelim = 90.05;
+    bool checknan = false;
+    while (!checknan && startanglelim > 89.9) {
+      const int nf = rtf_air_prop(M, startanglelim, AirTxHeight, IceLayerHeight, air);
+      double thd = 0;
+      for (int i = 0; i < nf; i++) thd += air[i * 4];
+      if ((!isnan(thd) && thd > 0) || startanglelim > endanglelim - 1) {
+        checknan = true;
+      } else {
+        startanglelim = startanglelim + 0.05;
+        ++probes;
+      }
+    }
+  }
+  if (endanglelim < 90.001 && endanglelim > 90.00) endanglelim = 90.05;
+  const RtfBrent br = gsl_brent(
+      [&](double x) {
+        return rtf_min_launch(M, x, AirTxHeight, IceLayerHeight, AntennaDepth, HorizontalDistance);
+      },
+      startanglelim, endanglelim, 0.000000001, 20);
+  const double LaunchAngleAir = br.root;
+  const int nf = rtf_air_prop(M, LaunchAngleAir, AirTxHeight, IceLayerHeight, air);
+  double thd_air = 0, t_air = 0;
+  for (int i = 0; i < nf; i++) {
+    thd_air += air[i * 4];
+    t_air += air[3 + i * 4] * 1e9;  // pow(10, 9)
+  }
+  // nf == 0: the reference reads unset slots (UB); NaN here, as the oracle
+  const double Lvalue = nf > 0 ? air[2] : __builtin_nan("");
+  const double inc = nf > 0 ? air[1 + (nf - 1) * 4] : __builtin_nan("");
+  double ice[4];
+  rtf_ice_prop(M, AntennaDepth, Lvalue, ice);
+  const double t_ice = ice[3] * 1e9;
+  o[0] = startanglelim;
+  o[1] = endanglelim;
+  o[2] = LaunchAngleAir;
+  o[3] = thd_air;
+  o[4] = inc;
+  o[5] = Lvalue;
+  o[6] = t_air;
+  o[7] = ice[0];
+  o[8] = ice[1];
+  o[9] = t_ice;
+  o[10] = ice[0] + thd_air;
+  o[11] = t_ice + t_air;
+  o[12] = br.status | (nf == 0 ? AIRICE_SOLVE_NO_AIR_LAYER : 0);
+  o[13] = br.iters;
+  o[14] = probes;
+  o[15] = nf;
+}
+
 struct RtfCall {
   int op, n_out;
   double a[8];
@@ -197,8 +406,9 @@ struct RtfCall {
 
 __global__ void rtf_kernel(DevMedium M, RtfCall c, double* __restrict__ out) {
   if (threadIdx.x != 0 || blockIdx.x != 0) return;
-  double r[4 * kMaxLayers + 1];
-  for (int i = 0; i < 4 * kMaxLayers + 1; i++) r[i] = 0;
+  double r[AIRICE_RTF_AIR2ICE_FIELDS > 4 * kMaxLayers + 1 ? AIRICE_RTF_AIR2ICE_FIELDS
+                                                         : 4 * kMaxLayers + 1];
+  for (int i = 0; i < (int)(sizeof(r) / sizeof(r[0])); i++) r[i] = 0;
   switch (c.op) {
     case AIRICE_RTF_HIT_POINT:
       rtf_hit_point(M, c.a[0], c.a[1], c.a[2], c.a[3], (int)c.a[4], r);
@@ -224,6 +434,9 @@ __global__ void rtf_kernel(DevMedium M, RtfCall c, double* __restrict__ out) {
     case AIRICE_RTF_MIN_LAUNCH:
       r[0] = rtf_min_launch(M, c.a[0], c.a[1], c.a[2], c.a[3], c.a[4]);
       break;
+    case AIRICE_RTF_AIR2ICE:
+      rtf_air2ice(M, c.a[0], c.a[1], c.a[2], c.a[3], r);
+      break;
     default:
       break;
   }
@@ -245,6 +458,8 @@ int rtf_outputs(int op, int max_layers) {
     case AIRICE_RTF_FTIMED:
     case AIRICE_RTF_MIN_LAUNCH:
       return 1;
+    case AIRICE_RTF_AIR2ICE:
+      return AIRICE_RTF_AIR2ICE_FIELDS;
     default:
       return -1;
   }

@@ -4,6 +4,7 @@
 
 #include <cmath>
 #include <cstdarg>
+#include <algorithm>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -591,7 +592,8 @@ int airice_rtf_eval(const airice_medium* m, int op, const double* args, size_t n
     return AIRICE_EINVAL;
   }
   thread_local double* d = nullptr;  // per-thread result slot, kept for the next call
-  if (d == nullptr) HIP_TRY(hipMalloc(&d, sizeof(double) * (4 * kMaxLayers + 1)));
+  if (d == nullptr)
+    HIP_TRY(hipMalloc(&d, sizeof(double) * std::max(4 * kMaxLayers + 1, AIRICE_RTF_AIR2ICE_FIELDS)));
   rc = airice::launch_rtf(M, op, args, n_args, d, nullptr);
   if (rc) {
     set_error("rtf launch failed: %s", hipGetErrorString(hipGetLastError()));

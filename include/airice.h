@@ -253,6 +253,17 @@ void Py_TraceIceToAir(double AntennaDepth, double IceLayerHeight, double AirTxHe
                                          airorice} -> {value} */
 #define AIRICE_RTF_MIN_LAUNCH 7       /* MinimizeforLaunchAngle (.cc:683-731) args {x, airtxheight,
                                          icelayerheight, antennadepth, horizontaldistance} */
+#define AIRICE_RTF_AIR2ICE 8          /* the Air2IceRayTracing CLI's solve (Air2IceRayTracing.C:56-185):
+                                         args {AirTxHeight, HorizontalDistance, IceLayerHeight,
+                                         AntennaDepth (> 0 in ice)} -> AIRICE_RTF_AIR2ICE_FIELDS:
+                                         launch-angle bracket and its probe, GSL-Brent root of
+                                         MinimizeforLaunchAngle (FindFunctionRoot, .cc:256-290,
+                                         max_iter 20, tolerance 1e-9), air and ice results */
+#define AIRICE_RTF_AIR2ICE_FIELDS 16  /* {startangle, endangle, LaunchAngleAir, THD_air,
+                                         IncidentAngleonIce, Lvalue, t_air ns, THD_ice,
+                                         IncidentAngleonAntenna, t_ice ns, THD, t ns,
+                                         status (AIRICE_SOLVE_* bits), Brent iterations,
+                                         probe steps, filled air layers} */
 /* Outputs written for op (4 x max_layers + 1 for AIR_PROPAGATION), or -1 for an unknown op. */
 int airice_rtf_outputs(int op, int max_layers);
 int airice_rtf_eval(const airice_medium *m, int op, const double *args, size_t n_args,

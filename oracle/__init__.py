@@ -200,6 +200,31 @@ def bisect(fn, lo: float, hi: float, tol: float = 1e-9, max_iter: int = 40):
     return r, st.value, calls
 
 
+def brent(fn, lo: float, hi: float, tol: float = 1e-9, max_iter: int = 20):
+    """GSL-Brent emulation (RayTracingFunctions FindFunctionRoot, .cc:256-290) on a Python
+    callable.  Returns (root, status bits, f evaluation points, iterations)."""
+    calls = []
+
+    def cb(x, _ctx):
+        calls.append(x)
+        return float(fn(x))
+
+    L = lib()
+    if not getattr(L, "_brent_sig", False):
+        L.or_brent.argtypes = [_FN, ctypes.c_void_p, ctypes.c_double, ctypes.c_double,
+                               ctypes.c_double, ctypes.c_int, ctypes.POINTER(ctypes.c_int),
+                               ctypes.POINTER(ctypes.c_int)]
+        L.or_brent.restype = ctypes.c_double
+        L._brent_sig = True
+    cfn = _FN(cb)
+    st, it = ctypes.c_int(0), ctypes.c_int(0)
+    r = L.or_brent(cfn, None, lo, hi, tol, max_iter, ctypes.byref(st), ctypes.byref(it))
+    return r, st.value, calls, it.value
+
+
+RTF_AIR2ICE = 8  # AIRICE_RTF_AIR2ICE
+
+
 def straight_angle_of(m: Medium, txh, dist, ice_h, depth) -> float:
     return lib().or_straight_angle(ctypes.byref(m), txh, dist, ice_h, depth)
 

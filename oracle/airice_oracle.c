@@ -614,6 +614,9 @@ int or_rtf_eval(const or_medium *m, int op, const double *a, double *out) {
       out[0] = MinimizeforLaunchAngle(m, a[0], &p);
       return 1;
     }
+    case 8: /* AIR2ICE: the Air2IceRayTracing CLI solve */
+      or_rtf_air2ice(m, a[0], a[1], a[2], a[3], out);
+      return 16;
     default:
       return -1;
   }
@@ -682,6 +685,125 @@ static double bisection_root(const or_medium *m, const minp *p, double x_lo, dou
                              double tol, int max_iter, int *status) {
   minctx c = {m, p};
   return or_bisect(min_cb, &c, x_lo, x_hi, tol, max_iter, status);
+}
+
+/* gsl_root_fsolver_brent (GNU GSL 2.x roots/brent.c, brent_init / brent_iterate; GSL is absent
+ * from this image: restated from its published algorithm, parity unpinned by reference output)
+ * under RayTracingFunctions::FindFunctionRoot (RayTracingFunctions.cc:256-290: max_iter 20,
+ * gsl_root_test_interval(lo, hi, 0, tol)).  Uninitialised-state cases as in or_bisect: a
+ * non-finite f at a bracket end leaves a zero state (flag NONFINITE_END); a non-finite f at an
+ * iterate stores nothing (STALE_MID); lower > upper fails set (BAD_BRACKET, root 0). */
+double or_brent(or_fn f, void *ctx, double x_lo, double x_hi, double tol_rel, int max_iter,
+                int *status, int *iters) {
+  const double EPS = 2.2204460492503131e-16; /* GSL_DBL_EPSILON */
+  if (x_lo > x_hi) { *status |= OR_SOLVE_BAD_BRACKET; *iters = 0; return 0.0; }
+  double root = 0.5 * (x_lo + x_hi), lo = x_lo, hi = x_hi;
+  double a = 0, b = 0, c = 0, d = 0, e = 0, fa = 0, fb = 0, fc = 0;
+  double fl = f(x_lo, ctx), fu = 0;
+  int ok = isfinite(fl);
+  if (ok) { fu = f(x_hi, ctx); ok = isfinite(fu); }
+  if (!ok) *status |= OR_SOLVE_NONFINITE_END;
+  else {
+    a = x_lo; fa = fl; b = x_hi; fb = fu; c = x_hi; fc = fu;
+    d = x_hi - x_lo; e = x_hi - x_lo;
+  }
+  int iter = 0, cont;
+  do {
+    iter++;
+    double la = a, lb = b, lc = c, ld = d, le = e, lfa = fa, lfb = fb, lfc = fc;
+    int ac_equal = 0;
+    if ((lfb < 0 && lfc < 0) || (lfb > 0 && lfc > 0)) {
+      ac_equal = 1; lc = la; lfc = lfa; ld = lb - la; le = lb - la;
+    }
+    if (fabs(lfc) < fabs(lfb)) {
+      ac_equal = 1; la = lb; lb = lc; lc = la; lfa = lfb; lfb = lfc; lfc = lfa;
+    }
+    double tol = 0.5 * EPS * fabs(lb);
+    double mm = 0.5 * (lc - lb);
+    if (lfb == 0) { root = lb; lo = lb; hi = lb; }
+    else if (fabs(mm) <= tol) {
+      root = lb;
+      if (lb < lc) { lo = lb; hi = lc; } else { lo = lc; hi = lb; }
+    } else {
+      if (fabs(le) < tol || fabs(lfa) <= fabs(lfb)) { ld = mm; le = mm; }
+      else {
+        double p, q, r, sr = lfb / lfa;
+        if (ac_equal) { p = 2 * mm * sr; q = 1 - sr; }
+        else {
+          q = lfa / lfc; r = lfb / lfc;
+          p = sr * (2 * mm * q * (q - r) - (lb - la) * (r - 1));
+          q = (q - 1) * (r - 1) * (sr - 1);
+        }
+        if (p > 0) q = -q; else p = -p;
+        double t1 = 3 * mm * q - fabs(tol * q), t2 = fabs(le * q);
+        if (2 * p < (t1 < t2 ? t1 : t2)) { le = ld; ld = p / q; }
+        else { ld = mm; le = mm; }
+      }
+      la = lb; lfa = lfb;
+      if (fabs(ld) > tol) lb += ld; else lb += (mm > 0 ? +tol : -tol);
+      double fnew = f(lb, ctx);
+      if (!isfinite(fnew)) *status |= OR_SOLVE_STALE_MID;
+      else {
+        lfb = fnew;
+        a = la; b = lb; c = lc; d = ld; e = le; fa = lfa; fb = lfb; fc = lfc;
+        root = lb;
+        double cc = lc;
+        if ((lfb < 0 && lfc < 0) || (lfb > 0 && lfc > 0)) cc = la;
+        if (lb < cc) { lo = lb; hi = cc; } else { lo = cc; hi = lb; }
+      }
+    }
+    if (lo > hi) cont = 0;
+    else {
+      double min_abs = ((lo > 0.0 && hi > 0.0) || (lo < 0.0 && hi < 0.0))
+                           ? (fabs(lo) < fabs(hi) ? fabs(lo) : fabs(hi)) : 0;
+      cont = !(fabs(hi - lo) < 0 + tol_rel * min_abs);
+    }
+  } while (cont && iter < max_iter);
+  if (cont) *status |= OR_SOLVE_MAXITER;
+  *iters = iter;
+  return root;
+}
+
+/* Air2IceRayTracing CLI solve (Air2IceRayTracing.C:56-185) on the RayTracingFunctions layer:
+ * straight-line angle, bracket [thR-16, thR] with the 0.05-degree probe (90.00 threshold), Brent,
+ * then GetAirPropagationPar / GetIcePropagationPar at the root.  out[16]: include/airice.h
+ * AIRICE_RTF_AIR2ICE_FIELDS. */
+void or_rtf_air2ice(const or_medium *m, double AirTxHeight, double HorizontalDistance,
+                    double IceLayerHeight, double AntennaDepth, double *o) {
+  const double pi = m->pi;
+  double StraightAngle = 180 - (atan(HorizontalDistance / (AirTxHeight - IceLayerHeight + AntennaDepth)) * (180.0 / pi));
+  double startanglelim = StraightAngle - 16, endanglelim = StraightAngle;
+  int probes = 0;
+  double out[5 * 8 + 2];
+  if (startanglelim < 90.00) {
+    startanglelim = 90.05;
+    int checknan = 0;
+    while (checknan == 0 && startanglelim > 89.9) {
+      int nf = air_propagation(m, startanglelim, AirTxHeight, IceLayerHeight, out);
+      double t = 0;
+      for (int i = 0; i < nf; i++) t += out[i * 5];
+      if ((isnan(t) == 0 && t > 0) || startanglelim > endanglelim - 1) checknan = 1;
+      else { startanglelim = startanglelim + 0.05; probes++; }
+    }
+  }
+  if (endanglelim < 90.001 && endanglelim > 90.00) endanglelim = 90.05;
+  minp p = {AirTxHeight, IceLayerHeight, AntennaDepth, HorizontalDistance};
+  minctx c = {m, &p};
+  int status = 0, iters = 0;
+  double LaunchAngleAir = or_brent(min_cb, &c, startanglelim, endanglelim, 0.000000001, 20,
+                                   &status, &iters);
+  int nf = air_propagation(m, LaunchAngleAir, AirTxHeight, IceLayerHeight, out);
+  double thd_air = 0, t_air = 0;
+  for (int i = 0; i < nf; i++) { thd_air += out[i * 5]; t_air += out[3 + i * 5] * pow(10, 9); }
+  double L = nf > 0 ? out[2] : NAN;
+  double inc = nf > 0 ? out[1 + (nf - 1) * 5] : NAN;
+  double ic[5];
+  ice_propagation(m, IceLayerHeight, AntennaDepth, L, ic);
+  double t_ice = ic[3] * pow(10, 9);
+  o[0] = startanglelim; o[1] = endanglelim; o[2] = LaunchAngleAir; o[3] = thd_air;
+  o[4] = inc; o[5] = L; o[6] = t_air; o[7] = ic[0]; o[8] = ic[1]; o[9] = t_ice;
+  o[10] = ic[0] + thd_air; o[11] = t_ice + t_air;
+  o[12] = status | (nf == 0 ? OR_SOLVE_NO_AIR_LAYER : 0); o[13] = iters; o[14] = probes; o[15] = nf;
 }
 
 double or_straight_angle(const or_medium *m, double H, double D, double ice, double depth) {

@@ -99,6 +99,12 @@ int or_air2ice(const or_medium *m, double txh, double dist, double ice_h, double
                double straight_angle, double dummy[17]);
 /* Generic GSL-bisection driver (FindFunctionRoot .cc:340-374), exposed for unit tests. */
 typedef double (*or_fn)(double x, void *ctx);
+/* GSL 2.x Brent under RayTracingFunctions::FindFunctionRoot; *iters = iterations run. */
+double or_brent(or_fn f, void *ctx, double x_lo, double x_hi, double tol_rel, int max_iter,
+                int *status, int *iters);
+/* Air2IceRayTracing CLI solve (Air2IceRayTracing.C:56-185); out[16] as AIRICE_RTF_AIR2ICE. */
+void or_rtf_air2ice(const or_medium *m, double AirTxHeight, double HorizontalDistance,
+                    double IceLayerHeight, double AntennaDepth, double *out);
 double or_bisect(or_fn f, void *ctx, double x_lo, double x_hi, double tol, int max_iter,
                  int *status);
 /* thR of GetHorizontalDistanceToIntersectionPoint (.cc:952-958), metres. */
