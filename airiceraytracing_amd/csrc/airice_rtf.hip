@@ -198,7 +198,7 @@ __device__ double rtf_min_launch(const DevMedium& M, double x, double AirTxHeigh
 // reference then iterates on uninitialised malloc memory) -- modelled as a zero state and flagged
 // AIRICE_SOLVE_NONFINITE_END; a non-finite f at an iterate returns EBADFUNC with nothing stored
 // (AIRICE_SOLVE_STALE_MID); lower > upper makes gsl_root_fsolver_set fail (AIRICE_SOLVE_BAD_BRACKET,
-// root 0).  The same restatement is oracle/airice_oracle.c or_brent.
+// root 0).  The test oracle restates it the same way (or_brent).
 struct RtfBrent {
   double root;
   int status, iters;
