@@ -375,7 +375,11 @@ def main():
     weights = load_opweights()
     W, work = table_work_per_ray(grid, weights)
     achieved = n * W / (kern_ms * 1e-3) / 1e12
-    roof = {"bound": "valu", "kernel": "table_kernel", "achieved": achieved,
+    roof = {"bound": "valu",
+            "bound_note": "FP64 VALU: neither HBM (the 44 B/ray store is ~14 % of 8 TB/s) nor MFMA "
+                          "applies -- per-lane transcendental chains, no contraction; peak = the "
+                          "MI355X FP64 vector rate (78.6 TFLOP/s with FMA as 2 = 39.3 T lane-ops/s)",
+            "kernel": "table_kernel", "achieved": achieved,
             "peak": PEAK_FP64_VALU_TOPS, "unit": "TFLOP/s (FP64 VALU lane-ops/s x 1e-12)",
             "frac": achieved / PEAK_FP64_VALU_TOPS, "traffic": pmc_traffic("table_kernel"),
             "algorithmic_ops_per_ray": W, "rays_per_launch": n, "kernel_ms": kern_ms,
