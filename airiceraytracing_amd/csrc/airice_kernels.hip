@@ -49,6 +49,12 @@ constexpr int kTableBlock = AIRICE_TABLE_BS;
 // with e.g. -DAIRICE_TWO_RAY_MIN=524288 -DAIRICE_TWO_RAY_MAX=917504.
 // AIRICE_TABLE_R2=0 leaves the R = 2 kernel out of the build (co-compiled template variants can
 // perturb each other's register allocation)
+#ifndef AIRICE_OVERSHOOT
+#define AIRICE_OVERSHOOT 0
+#endif
+#ifndef AIRICE_GUARD_SKIP
+#define AIRICE_GUARD_SKIP 0
+#endif
 #ifndef AIRICE_ROWCONST_ALIGN16
 #define AIRICE_ROWCONST_ALIGN16 0
 #endif
@@ -466,7 +472,7 @@ __device__ __forceinline__ AirPath make_air_path(const DevMedium& M, double H, d
 // sin of the receive angle of the first layer (GetLayerHitPointPar .cc:562-589).
 __device__ __forceinline__ double first_layer_v2(const DevMedium& M, double n_tx, double n_rtop,
                                                  double theta) {
-  const double v1 = sin((180 - theta) * M.d2r);
+  const double v1 = sin_start((180 - theta) * M.d2r);
   return sin_asin((n_tx * sin_asin(v1)) / n_rtop);
 }
 
@@ -758,6 +764,15 @@ __device__ __forceinline__ SolveResult solve_root(const DevMedium& M, const IceC
       x = (lo + hi) / 2.0;
     } else if (phase == PH_EST) {
       x = (est == 0) ? x2 : x2 - f2 * ((x2 - x1) / (f2 - f1));
+#if AIRICE_OVERSHOOT
+      // near convergence (the step is under a quarter of GSL's final bracket width W and x2 is
+      // a guard), aim W/8 past the predicted root: the new point and x2 then straddle the root
+      // within W/2, which ends the search without the two guard evaluations below
+      if (est > 0 && fabs(f2) >= tau) {
+        const double W = 1e-9 * gL, step = x - x2;
+        if (fabs(step) < 0.25 * W) x += __builtin_copysign(0.125 * W, step);
+      }
+#endif
       if (!(x > gL && x < gR)) x = 0.5 * (gL + gR);  // safeguard: the guards' midpoint
     } else if (phase == PH_G1) {
       x = xg - dlt;
@@ -838,17 +853,26 @@ __device__ __forceinline__ SolveResult solve_root(const DevMedium& M, const IceC
       if (!isfinite(f)) {
         phase = PH_BISECT;
       } else if (fabs(f) < tau) {
-        // at the root: guards a few tau either side, scaled by the local secant slope
+        // at the root: guards a few tau either side, scaled by the local secant slope; a side
+        // whose guard already lies within W/4 of the root needs none
         dlt = 4.0 * tau * fabs((x2 - x1) / (f2 - f1));
         xg = x;
-        phase = (dlt > 0.0 && dlt < (gR - gL)) ? PH_G1 : PH_BISECT;
+        const double Wq = AIRICE_GUARD_SKIP ? 0.25e-9 * gL : 0.0;
+        const bool needL = !(xg - gL <= Wq), needR = !(gR - xg <= Wq);
+        phase = (dlt > 0.0 && dlt < (gR - gL)) ? (needL ? PH_G1 : (needR ? PH_G2 : PH_BISECT))
+                                               : PH_BISECT;
       } else {
         guard(x, f);
         if (est >= 12) phase = PH_BISECT;
+#if AIRICE_GUARD_SKIP
+        // guards on both sides within W/2: the bisection evaluates at most ~1 midpoint
+        if (gR - gL <= 0.5e-9 * gL) phase = PH_BISECT;
+#endif
       }
     } else if (phase == PH_G1 || phase == PH_G2) {
       if (isfinite(f)) guard(x, f);
-      phase = (phase == PH_G1) ? PH_G2 : PH_BISECT;
+      phase = (phase == PH_G1 && !(AIRICE_GUARD_SKIP && gR - xg <= 0.25e-9 * gL)) ? PH_G2
+                                                                               : PH_BISECT;
     } else {  // PH_BISECT: gsl_root_fsolver_iterate at a midpoint between the guards
       if (!exact && isfinite(f)) guard(x, f);
       ++iter;
@@ -912,7 +936,7 @@ __device__ __forceinline__ Solved evaluate_root(const DevMedium& M, const IceCon
       S.geo_air += sg.geo;
     }
     // receive angle of the last layer: asin(v2) for the first layer, asin(L0/n(Stop)) below
-    S.inc = asin(P.top == P.bot ? v2 : L0 / P.iceair.n) * M.r2d;
+    S.inc = k_asin(P.top == P.bot ? v2 : L0 / P.iceair.n) * M.r2d;
   }
   S.thd_ice = 0.0;
   S.t_ice = 0.0;
@@ -924,7 +948,7 @@ __device__ __forceinline__ Solved evaluate_root(const DevMedium& M, const IceCon
     const RayL RL = ray_L(A2i, L0);
     const Segment sg = segment(I.ice0, rx, M.A_ice, A2i, RL, false);
     S.thd_ice = sg.thd;
-    S.ant = asin(L0 / rx.n) * M.r2d;
+    S.ant = k_asin(L0 / rx.n) * M.r2d;
     S.t_ice = sg.t;
     S.geo_ice = sg.geo;
   }
@@ -1110,7 +1134,7 @@ __global__ __launch_bounds__(kBlock) void solve_out_kernel(DevMedium M, IceConst
   out[10 * ld + k] = S.launch;
   if (VARIANT == AIRICE_VARIANT_MULTIRAY) {
     double tS, tP;
-    fresnel_trans(S.ice_n, I.ice0.n, S.inc * M.d2r, tS, tP);
+    fresnel_from_sine(S.ice_n, I.ice0.n, S.ice_n / I.ice0.n, sin_start(S.inc * M.d2r), tS, tP);
     out[11 * ld + k] = S.ant;
     out[12 * ld + k] = tS;
     out[13 * ld + k] = tP;
@@ -1118,7 +1142,7 @@ __global__ __launch_bounds__(kBlock) void solve_out_kernel(DevMedium M, IceConst
     out[15 * ld + k] = S.geo_ice;
     out[16 * ld + k] = S.inc;
   } else {
-    out[11 * ld + k] = asin((S.ice_n / I.ice0.n) * sin(S.inc * M.d2r)) * M.r2d;
+    out[11 * ld + k] = k_asin((S.ice_n / I.ice0.n) * sin_start(S.inc * M.d2r)) * M.r2d;
     out[12 * ld + k] = S.ant;
     out[13 * ld + k] = S.geo_air;
     out[14 * ld + k] = S.geo_ice;
@@ -1139,7 +1163,7 @@ __global__ __launch_bounds__(kBlock) void hdtip_out_kernel(DevMedium M, IceConst
   const Solved S = evaluate_root(M, I, g, x, st);
   const double thd = S.thd_ice + S.thd_air;
   double tS, tP;
-  fresnel_trans(S.ice_n, I.ice0.n, S.inc * M.d2r, tS, tP);
+  fresnel_from_sine(S.ice_n, I.ice0.n, S.ice_n / I.ice0.n, sin_start(S.inc * M.d2r), tS, tP);
   out[0 * ld + k] = (S.t_ice * kSpeedC) * 100;
   out[1 * ld + k] = (S.t_air * kSpeedC) * 100;
   out[2 * ld + k] = S.geo_ice * 100;
@@ -1170,7 +1194,7 @@ __global__ __launch_bounds__(kBlock) void lookup_fallback_out_kernel(
   const Solved S = evaluate_root(M, I, g, x, st);
   const double thd = S.thd_ice + S.thd_air;
   double tS, tP;
-  fresnel_trans(S.ice_n, I.ice0.n, S.inc * M.d2r, tS, tP);
+  fresnel_from_sine(S.ice_n, I.ice0.n, S.ice_n / I.ice0.n, sin_start(S.inc * M.d2r), tS, tP);
   const double launch = S.launch * M.d2r;
   const bool good = ok[k] != 0 && check_solution(thd, g.D) && !(launch < 0);
   out[0 * ld + k] = good ? S.geo_ice * 100 : 0.0;
@@ -1197,7 +1221,7 @@ __global__ __launch_bounds__(kBlock) void trace_out_kernel(DevMedium M, IceConst
   const int st = (int)o[9];
   const Solved S = evaluate_root(M, I, g, x, st);
   const double thd = S.thd_ice + S.thd_air;
-  const double aoi = asin((S.ice_n / I.ice0.n) * sin(S.inc * M.d2r)) * M.r2d;
+  const double aoi = k_asin((S.ice_n / I.ice0.n) * sin_start(S.inc * M.d2r)) * M.r2d;
   if (check_solution(thd, g.D)) {
     // swap(launch, received); received = 180 - received (TraceIceToAir.C:33-34)
     o[0] = g.H;
