@@ -21,6 +21,7 @@
 #include <cstdio>
 #include <algorithm>
 #include <cstdlib>
+#include <mutex>
 #include <vector>
 
 #include "airice.h"
@@ -1044,6 +1045,23 @@ constexpr int kRootsBlock = AIRICE_ROOTS_BS;
 #ifndef AIRICE_ROOTS_WAVES
 #define AIRICE_ROOTS_WAVES 4
 #endif
+// batch-wide grouping: batches of at least AIRICE_GROUP_MIN queries (0: never) are sorted across
+// the whole batch and solved in AIRICE_SORTED_BS-thread blocks (roots_sorted_kernel)
+#ifndef AIRICE_GROUP_MIN
+#define AIRICE_GROUP_MIN 65536
+#endif
+#ifndef AIRICE_SORTED_BS
+#define AIRICE_SORTED_BS 256
+#endif
+#ifndef AIRICE_GROUP_BUCKETS
+#define AIRICE_GROUP_BUCKETS 8
+#endif
+#ifndef AIRICE_GROUP_ITEMS
+#define AIRICE_GROUP_ITEMS 8
+#endif
+#ifndef AIRICE_SORTED_WAVES
+#define AIRICE_SORTED_WAVES AIRICE_ROOTS_WAVES
+#endif
 
 template <int IN>
 __global__ __launch_bounds__(kRootsBlock, AIRICE_ROOTS_WAVES) void roots_kernel(DevMedium M, IceConsts I, QueryArgs Q,
@@ -1096,6 +1114,139 @@ __global__ __launch_bounds__(kRootsBlock, AIRICE_ROOTS_WAVES) void roots_kernel(
     park.stats[3 * k + 1] = r.n_est;
     park.stats[3 * k + 2] = r.n_inside;
   }
+}
+
+// ---------------------------------------------------------------------------
+// Batch-wide grouping (large batches).  roots_kernel above sorts inside each 1024-query block, so
+// a CU -- which holds one such block at 128 VGPRs -- waits for the block's slowest wave before
+// the next block can start.  Here the whole batch is first grouped by the same straight-line
+// angle key (counting sort: keys + histogram, then a scatter), and roots_sorted_kernel solves the
+// queries in that order in small blocks that the CU replaces independently.  Each query is still
+// solved on its own and written by its index: results are identical either way.
+// ---------------------------------------------------------------------------
+constexpr int kGroupBuckets = AIRICE_GROUP_BUCKETS;
+constexpr int kGroupItems = AIRICE_GROUP_ITEMS;  // queries per thread in the sort passes
+constexpr int kGroupChunk = kBlock * kGroupItems;     // queries per block and round
+constexpr int kGroupBlocks = 512;                     // blocks of the sort passes (at most)
+constexpr int kSortedBlock = AIRICE_SORTED_BS;
+
+// The sort key is roots_kernel's straight-line-angle bucket, b = floor((thR - 90) * B / 90) with
+// thR = 180 - atan(x) deg, x = D / (H - ice - depth), evaluated without the atan: b >= j exactly
+// when x <= tan(90 deg * (1 - j / B)), so b counts the host-computed thresholds x lies below.
+// (The key only orders the work; results do not depend on it.)
+struct GroupKey {
+  double t[kGroupBuckets];  // t[j - 1] = tan(90 deg * (1 - j / B)), j = 1 .. B-1
+};
+
+template <int IN>
+__device__ __forceinline__ int query_bucket(const DevMedium& M, const QueryArgs& Q, long long k,
+                                            const GroupKey& K) {
+  if (IN == IN_CM100 && !(Q.mask[k] & AIRICE_LOOKUP_FALLBACK)) return -1;  // not a fallback lane
+  double thR_unused;
+  const Geometry g = load_query<IN>(M, Q, k, thR_unused);
+  const double den = g.H - g.ice - g.depth;
+  if (!(den > 0)) return den < 0 ? kGroupBuckets - 1 : 0;  // thR > 180 (clamped) / 90 or NaN
+  int b = 0;
+#pragma unroll
+  for (int j = 0; j < kGroupBuckets - 1; ++j) b += (g.D <= K.t[j] * den) ? 1 : 0;
+  return b;
+}
+
+// Pass 1: the key of every query and each block's bucket counts, bucket-major:
+// cnt[b * nblocks + block] (no global atomics: thousands of blocks adding into a few counters
+// serialise on them).
+template <int IN>
+__global__ __launch_bounds__(kBlock) void group_count_kernel(DevMedium M, QueryArgs Q, GroupKey K,
+                                                             int rounds, int8_t* __restrict__ key,
+                                                             int* __restrict__ cnt) {
+  __shared__ int s_c[kGroupBuckets];
+  if (threadIdx.x < kGroupBuckets) s_c[threadIdx.x] = 0;
+  __syncthreads();
+  for (int rr = 0; rr < rounds; ++rr) {
+    const long long k0 = ((long long)blockIdx.x * rounds + rr) * kGroupChunk + threadIdx.x;
+#pragma unroll
+    for (int i = 0; i < kGroupItems; ++i) {
+      const long long k = k0 + i * kBlock;
+      if (k < Q.n) {
+        const int b = query_bucket<IN>(M, Q, k, K);
+        key[k] = (int8_t)b;
+        if (b >= 0) atomicAdd(&s_c[b], 1);
+      }
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x < kGroupBuckets) cnt[threadIdx.x * gridDim.x + blockIdx.x] = s_c[threadIdx.x];
+}
+
+// Pass 2: perm[position] = query index, positions grouped by bucket.  Each block first derives
+// its own first position per bucket from all blocks' counts (bucket b's earlier buckets in full,
+// plus bucket b of the blocks before it): 16 lanes per bucket sum strided slices of cnt[], so no
+// separate scan pass is needed.  A block's queries of one bucket take consecutive positions.
+static_assert(kBlock % kGroupBuckets == 0, "lanes per bucket");
+constexpr int kLanesPerBucket = kBlock / kGroupBuckets;
+__global__ __launch_bounds__(kBlock) void group_scatter_kernel(const int8_t* __restrict__ key,
+                                                               long long n, int rounds,
+                                                               const int* __restrict__ cnt,
+                                                               int* __restrict__ grouped,
+                                                               int* __restrict__ perm) {
+  __shared__ int s_tot[kGroupBuckets][kLanesPerBucket], s_pre[kGroupBuckets][kLanesPerBucket];
+  __shared__ int s_base[kGroupBuckets];
+  const int nb = gridDim.x, blk = blockIdx.x;
+  {
+    const int bb = threadIdx.x / kLanesPerBucket, l = threadIdx.x % kLanesPerBucket;
+    const int* c = cnt + (long long)bb * nb;
+    int tot = 0, pre = 0;
+#pragma unroll 8
+    for (int j = l; j < nb; j += kLanesPerBucket) {
+      const int v = c[j];
+      tot += v;
+      pre += j < blk ? v : 0;
+    }
+    s_tot[bb][l] = tot;
+    s_pre[bb][l] = pre;
+  }
+  __syncthreads();
+  if (threadIdx.x < kGroupBuckets) {
+    int base = 0;
+    for (int b = 0; b < (int)threadIdx.x; ++b)
+      for (int l = 0; l < kLanesPerBucket; ++l) base += s_tot[b][l];
+    for (int l = 0; l < kLanesPerBucket; ++l) base += s_pre[threadIdx.x][l];
+    s_base[threadIdx.x] = base;
+    if (blk == 0 && threadIdx.x == kGroupBuckets - 1) {  // number of queries with a bucket
+      for (int l = 0; l < kLanesPerBucket; ++l) base += s_tot[kGroupBuckets - 1][l];
+      *grouped = base;
+    }
+  }
+  __syncthreads();
+  for (int rr = 0; rr < rounds; ++rr) {
+    const long long k0 = ((long long)blk * rounds + rr) * kGroupChunk + threadIdx.x;
+#pragma unroll
+    for (int i = 0; i < kGroupItems; ++i) {
+      const long long k = k0 + i * kBlock;
+      const int b = k < n ? (int)key[k] : -1;
+      if (b >= 0) perm[atomicAdd(&s_base[b], 1)] = (int)k;
+    }
+  }
+}
+
+template <int IN>
+__global__ __launch_bounds__(kSortedBlock, AIRICE_SORTED_WAVES) void roots_sorted_kernel(
+    DevMedium M, IceConsts I, QueryArgs Q, Park park, const int* __restrict__ perm,
+    const int* __restrict__ grouped) {
+  __shared__ __align__(16) double s_logtab[1 << kLogTableBits][2];
+  for (int t = threadIdx.x; t < (1 << kLogTableBits); t += kSortedBlock) {
+    s_logtab[t][0] = kLogTable[t][0];
+    s_logtab[t][1] = kLogTable[t][1];
+  }
+  __syncthreads();
+  const long long ks = (long long)blockIdx.x * kSortedBlock + threadIdx.x;
+  if (ks >= *grouped) return;  // past the queries with a bucket (the lookup's fallback lanes)
+  const long long k = perm[ks];
+  double thR;
+  const Geometry g = load_query<IN>(M, Q, k, thR);
+  const SolveResult r = solve_root(M, I, g, thR, park.exact != 0, &s_logtab[0][0]);
+  park.root[k * park.stride] = r.root;
+  park.status[k * park.stride] = (double)r.status;
 }
 
 __device__ __forceinline__ bool check_solution(double thd, double D) {
@@ -1244,11 +1395,78 @@ __global__ __launch_bounds__(kBlock) void trace_out_kernel(DevMedium M, IceConst
 // Host launchers
 // ---------------------------------------------------------------------------
 static inline unsigned grid_for(long long n) { return (unsigned)((n + kBlock - 1) / kBlock); }
+static inline int launch_ok() { return hipGetLastError() == hipSuccess ? AIRICE_OK : AIRICE_EHIP; }
+
 static inline dim3 roots_grid(size_t n) {
   return dim3((unsigned)((n + kRootsBlock - 1) / kRootsBlock));
 }
 
-static inline int launch_ok() { return hipGetLastError() == hipSuccess ? AIRICE_OK : AIRICE_EHIP; }
+// Stream-ordered scratch for the grouping passes: a library-owned pool per device whose release
+// threshold keeps freed blocks for reuse (the default pool returns them at every synchronisation,
+// and re-growing it made each launch wait on the host).
+static hipError_t scratch_alloc(void** p, size_t bytes, hipStream_t st) {
+  static std::mutex mu;
+  static std::vector<hipMemPool_t> pools;
+  int dev = 0;
+  if (hipError_t e = hipGetDevice(&dev)) return e;
+  hipMemPool_t pool = nullptr;
+  {
+    std::lock_guard<std::mutex> lock(mu);
+    if ((int)pools.size() <= dev) pools.resize(dev + 1, nullptr);
+    if (pools[dev] == nullptr) {
+      hipMemPoolProps props{};
+      props.allocType = hipMemAllocationTypePinned;
+      props.location.type = hipMemLocationTypeDevice;
+      props.location.id = dev;
+      if (hipError_t e = hipMemPoolCreate(&pools[dev], &props)) return e;
+      uint64_t keep = UINT64_MAX;
+      (void)hipMemPoolSetAttribute(pools[dev], hipMemPoolAttrReleaseThreshold, &keep);
+    }
+    pool = pools[dev];
+  }
+  return hipMallocFromPoolAsync(p, bytes, pool, st);
+}
+
+// Stage 1 of every minimizer launch: roots_kernel (block-local grouping) for small batches and
+// debug statistics, the batch-wide grouping otherwise (stream-ordered scratch from the HIP pool).
+template <int IN>
+static int launch_roots(const DevMedium& M, const IceConsts& I, const QueryArgs& Q,
+                        const Park& park, size_t n, hipStream_t st) {
+  static const int group_min = getenv("AIRICE_GROUP_MIN") ? atoi(getenv("AIRICE_GROUP_MIN"))
+                                                           : AIRICE_GROUP_MIN;
+  if (group_min <= 0 || n < (size_t)group_min || park.stats != nullptr || n >= (1ull << 31)) {
+    hipLaunchKernelGGL(roots_kernel<IN>, roots_grid(n), dim3(kRootsBlock), 0, st, M, I, Q, park);
+    return launch_ok();
+  }
+  static const GroupKey key_t = [] {
+    GroupKey K{};
+    for (int j = 1; j < kGroupBuckets; ++j) K.t[j - 1] = tan(M_PI / 2 * (1.0 - (double)j / kGroupBuckets));
+    return K;
+  }();
+  // at most kGroupBlocks blocks in the two passes (each scatter block reads every block's
+  // counts); larger batches give each block several chunks
+  const size_t chunks = (n + kGroupChunk - 1) / kGroupChunk;
+  const int rounds = (int)((chunks + kGroupBlocks - 1) / kGroupBlocks);
+  const unsigned nb = (unsigned)((chunks + rounds - 1) / rounds);
+  const size_t m = (size_t)kGroupBuckets * nb;
+  const size_t ws_bytes = sizeof(int) * (m + 1 + n) + n;  // cnt, grouped count, perm, keys
+  void* ws = nullptr;
+  if (scratch_alloc(&ws, ws_bytes, st) != hipSuccess) return AIRICE_EHIP;
+  int* cnt = static_cast<int*>(ws);
+  int* grouped = cnt + m;
+  int* perm = grouped + 1;
+  int8_t* key = reinterpret_cast<int8_t*>(perm + n);
+  hipLaunchKernelGGL(group_count_kernel<IN>, dim3(nb), dim3(kBlock), 0, st, M, Q, key_t, rounds,
+                     key, cnt);
+  hipLaunchKernelGGL(group_scatter_kernel, dim3(nb), dim3(kBlock), 0, st, key, (long long)n,
+                     rounds, cnt, grouped, perm);
+  hipLaunchKernelGGL(roots_sorted_kernel<IN>, dim3((unsigned)((n + kSortedBlock - 1) / kSortedBlock)),
+                     dim3(kSortedBlock), 0, st, M, I, Q, park, perm, grouped);
+  const int rc = launch_ok();
+  if (hipFreeAsync(ws, st) != hipSuccess) return AIRICE_EHIP;
+  return rc;
+}
+
 
 int launch_table(const DevMedium& M, const IceConsts& I, const airice_grid* g, int row_begin,
                  int row_count, float* d_table, double* d_full, size_t ld, hipStream_t st) {
@@ -1338,7 +1556,7 @@ int launch_solve(const DevMedium& M, const IceConsts& I, int variant, const doub
   if (stats_path != nullptr && hipMalloc(&park.stats, sizeof(int) * 3 * n) != hipSuccess)
     return AIRICE_EHIP;
   const dim3 grid(grid_for((long long)n)), block(kBlock);
-  hipLaunchKernelGGL(roots_kernel<IN_M>, roots_grid(n), dim3(kRootsBlock), 0, st, M, I, Q, park);
+  if (int rc = launch_roots<IN_M>(M, I, Q, park, n, st)) return rc;
   if (park.stats != nullptr) {  // debug: append the per-query counts (synchronous)
     std::vector<int> h(3 * n);
     if (hipStreamSynchronize(st) != hipSuccess ||
@@ -1366,7 +1584,7 @@ int launch_hdtip(const DevMedium& M, const IceConsts& I, const double* src, cons
   const QueryArgs Q{src, dist, depth, nullptr, ice_cm, (long long)n};
   const Park park{out + 4 * ld, out, 1, bisect_exact(), nullptr};
   const dim3 grid(grid_for((long long)n)), block(kBlock);
-  hipLaunchKernelGGL(roots_kernel<IN_CM>, roots_grid(n), dim3(kRootsBlock), 0, st, M, I, Q, park);
+  if (int rc = launch_roots<IN_CM>(M, I, Q, park, n, st)) return rc;
   hipLaunchKernelGGL(hdtip_out_kernel, grid, block, 0, st, M, I, Q, out, ld, ok);
   return launch_ok();
 }
@@ -1381,7 +1599,7 @@ int launch_lookup_fallback(const DevMedium& M, const IceConsts& I, const double*
   const QueryArgs Q{src, dist, depth, nullptr, ice_arg, (long long)n, flags};
   const Park park{out + 4 * ld, out, 1, bisect_exact(), nullptr};
   const dim3 grid(grid_for((long long)n)), block(kBlock);
-  hipLaunchKernelGGL(roots_kernel<IN_CM100>, roots_grid(n), dim3(kRootsBlock), 0, st, M, I, Q, park);
+  if (int rc = launch_roots<IN_CM100>(M, I, Q, park, n, st)) return rc;
   hipLaunchKernelGGL(lookup_fallback_out_kernel, grid, block, 0, st, M, I, Q, out, ld, ok);
   return launch_ok();
 }
@@ -1392,7 +1610,7 @@ int launch_trace(const DevMedium& M, const IceConsts& I, const double* depth, co
   const QueryArgs Q{depth, ice, txh, dist, 0.0, (long long)n};
   const Park park{out10 + 5, out10 + 9, 10, bisect_exact(), nullptr};
   const dim3 grid(grid_for((long long)n)), block(kBlock);
-  hipLaunchKernelGGL(roots_kernel<IN_TRACE>, roots_grid(n), dim3(kRootsBlock), 0, st, M, I, Q, park);
+  if (int rc = launch_roots<IN_TRACE>(M, I, Q, park, n, st)) return rc;
   hipLaunchKernelGGL(trace_out_kernel, grid, block, 0, st, M, I, Q, out10);
   return launch_ok();
 }
