@@ -910,7 +910,8 @@ struct Solved {
 
 // Outputs at the root (GetAirPropagationPar + GetIcePropagationPar, .cc:1524-1566).
 __device__ __forceinline__ Solved evaluate_root(const DevMedium& M, const IceConsts& I,
-                                                const Geometry& g, double x, int status) {
+                                                const Geometry& g, double x, int status,
+                                                const double* tab) {
   Solved S;
   S.status = status;
   S.launch = x;
@@ -931,7 +932,7 @@ __device__ __forceinline__ Solved evaluate_root(const DevMedium& M, const IceCon
     for (int il = P.top; il > P.bot - 1; --il) {
       const Endpoint T = (il == P.top) ? P.tx : M.start[il];
       const Endpoint R = (il == P.top) ? P.rtop : ((il == P.bot) ? P.iceair : M.stop[il]);
-      const Segment sg = segment(T, R, M.A_air, A2, RL, true);
+      const Segment sg = segment(T, R, M.A_air, A2, RL, true, tab);
       S.thd_air += sg.thd;
       S.t_air += sg.t;
       S.geo_air += sg.geo;
@@ -947,7 +948,7 @@ __device__ __forceinline__ Solved evaluate_root(const DevMedium& M, const IceCon
     const Endpoint rx = ice_endpoint(M, g.depth_pos);
     const double A2i = M.A_ice * M.A_ice;
     const RayL RL = ray_L(A2i, L0);
-    const Segment sg = segment(I.ice0, rx, M.A_ice, A2i, RL, false);
+    const Segment sg = segment(I.ice0, rx, M.A_ice, A2i, RL, false, tab);
     S.thd_ice = sg.thd;
     S.ant = k_asin(L0 / rx.n) * M.r2d;
     S.t_ice = sg.t;
@@ -1257,6 +1258,14 @@ __device__ __forceinline__ bool check_solution(double thd, double D) {
   return good;
 }
 
+// The stage-2 kernels read the log table from LDS like the solve (one entry per thread).
+static_assert(kBlock == (1 << kLogTableBits), "one log-table entry per thread");
+__device__ __forceinline__ void stage_log_table(double (*s)[2]) {
+  s[threadIdx.x][0] = kLogTable[threadIdx.x][0];
+  s[threadIdx.x][1] = kLogTable[threadIdx.x][1];
+  __syncthreads();
+}
+
 // Stage 2 of Air2IceRayTracing: dummy[0..16] (MultiRay, .cc:1597-1614) or dummy[0..14]
 // (pythonwrapper, AirIceRayTracing.cc:1070-1084), SoA with stride ld.
 template <int VARIANT>
@@ -1264,12 +1273,14 @@ __global__ __launch_bounds__(kBlock) void solve_out_kernel(DevMedium M, IceConst
                                                            double* __restrict__ out, size_t ld,
                                                            uint8_t* __restrict__ status) {
   const long long k = (long long)blockIdx.x * kBlock + threadIdx.x;
+  __shared__ __align__(16) double s_logtab[1 << kLogTableBits][2];
+  stage_log_table(s_logtab);
   if (k >= Q.n) return;
   double thR;
   const Geometry g = load_query<IN_M>(M, Q, k, thR);
   const double x = out[10 * ld + k];
   const int st = (int)out[0 * ld + k];
-  const Solved S = evaluate_root(M, I, g, x, st);
+  const Solved S = evaluate_root(M, I, g, x, st, &s_logtab[0][0]);
   const double thd = S.thd_ice + S.thd_air;
   const double tt = S.t_ice + S.t_air;
   out[0 * ld + k] = g.H;
@@ -1306,12 +1317,14 @@ __global__ __launch_bounds__(kBlock) void hdtip_out_kernel(DevMedium M, IceConst
                                                            double* __restrict__ out, size_t ld,
                                                            uint8_t* __restrict__ ok) {
   const long long k = (long long)blockIdx.x * kBlock + threadIdx.x;
+  __shared__ __align__(16) double s_logtab[1 << kLogTableBits][2];
+  stage_log_table(s_logtab);
   if (k >= Q.n) return;
   double thR;
   const Geometry g = load_query<IN_CM>(M, Q, k, thR);
   const double x = out[4 * ld + k];
   const int st = (int)out[0 * ld + k];
-  const Solved S = evaluate_root(M, I, g, x, st);
+  const Solved S = evaluate_root(M, I, g, x, st, &s_logtab[0][0]);
   const double thd = S.thd_ice + S.thd_air;
   double tS, tP;
   fresnel_from_sine(S.ice_n, I.ice0.n, S.ice_n / I.ice0.n, sin_start(S.inc * M.d2r), tS, tP);
@@ -1336,13 +1349,15 @@ __global__ __launch_bounds__(kBlock) void lookup_fallback_out_kernel(
     DevMedium M, IceConsts I, QueryArgs Q, double* __restrict__ out, size_t ld,
     uint8_t* __restrict__ ok) {
   const long long k = (long long)blockIdx.x * kBlock + threadIdx.x;
+  __shared__ __align__(16) double s_logtab[1 << kLogTableBits][2];
+  stage_log_table(s_logtab);
   if (k >= Q.n) return;
   if (!(Q.mask[k] & AIRICE_LOOKUP_FALLBACK)) return;
   double thR;
   const Geometry g = load_query<IN_CM100>(M, Q, k, thR);
   const double x = out[4 * ld + k];
   const int st = (int)out[0 * ld + k];
-  const Solved S = evaluate_root(M, I, g, x, st);
+  const Solved S = evaluate_root(M, I, g, x, st, &s_logtab[0][0]);
   const double thd = S.thd_ice + S.thd_air;
   double tS, tP;
   fresnel_from_sine(S.ice_n, I.ice0.n, S.ice_n / I.ice0.n, sin_start(S.inc * M.d2r), tS, tP);
@@ -1364,13 +1379,15 @@ __global__ __launch_bounds__(kBlock) void lookup_fallback_out_kernel(
 __global__ __launch_bounds__(kBlock) void trace_out_kernel(DevMedium M, IceConsts I, QueryArgs Q,
                                                            double* __restrict__ out10) {
   const long long k = (long long)blockIdx.x * kBlock + threadIdx.x;
+  __shared__ __align__(16) double s_logtab[1 << kLogTableBits][2];
+  stage_log_table(s_logtab);
   if (k >= Q.n) return;
   double thR;
   const Geometry g = load_query<IN_TRACE>(M, Q, k, thR);
   double* o = out10 + 10 * k;
   const double x = o[5];
   const int st = (int)o[9];
-  const Solved S = evaluate_root(M, I, g, x, st);
+  const Solved S = evaluate_root(M, I, g, x, st, &s_logtab[0][0]);
   const double thd = S.thd_ice + S.thd_air;
   const double aoi = k_asin((S.ice_n / I.ice0.n) * sin_start(S.inc * M.d2r)) * M.r2d;
   if (check_solution(thd, g.D)) {
@@ -1434,7 +1451,10 @@ static int launch_roots(const DevMedium& M, const IceConsts& I, const QueryArgs&
                         const Park& park, size_t n, hipStream_t st) {
   static const int group_min = getenv("AIRICE_GROUP_MIN") ? atoi(getenv("AIRICE_GROUP_MIN"))
                                                            : AIRICE_GROUP_MIN;
-  if (group_min <= 0 || n < (size_t)group_min || park.stats != nullptr || n >= (1ull << 31)) {
+  // (the table lookup's fallback pass stays block-local: its batch is the whole lookup batch,
+  // of which typically well under 1 % of lanes are fallback lanes)
+  if (IN == IN_CM100 || group_min <= 0 || n < (size_t)group_min || park.stats != nullptr ||
+      n >= (1ull << 31)) {
     hipLaunchKernelGGL(roots_kernel<IN>, roots_grid(n), dim3(kRootsBlock), 0, st, M, I, Q, park);
     return launch_ok();
   }

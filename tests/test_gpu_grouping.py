@@ -2,10 +2,10 @@
 form (roots_kernel): large batches are sorted across the whole batch by straight-line angle and
 solved in that order, but every query is still solved on its own and written by its index, so
 the two schedules must give bit-identical outputs.  Both are run in fresh processes
-(AIRICE_GROUP_MIN=0: never group; =1: always group) through all four minimizer entries --
-airice_solve_launch, airice_hdtip_launch, the table lookup's fallback pass and
-airice_trace_ice_to_air_launch -- and the grouped solve is also checked against the oracle on a
-strided sample."""
+(AIRICE_GROUP_MIN=0: never group; =1: always group) through the minimizer entries --
+airice_solve_launch, airice_hdtip_launch and airice_trace_ice_to_air_launch, plus the table
+lookup, whose fallback pass stays block-local in both -- and the grouped solve is also checked
+against the oracle on a strided sample."""
 import os
 import subprocess
 import sys
