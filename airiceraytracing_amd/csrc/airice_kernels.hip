@@ -1057,6 +1057,9 @@ constexpr int kRootsBlock = AIRICE_ROOTS_BS;
 #ifndef AIRICE_GROUP_BUCKETS
 #define AIRICE_GROUP_BUCKETS 8
 #endif
+#ifndef AIRICE_GROUP_HBINS
+#define AIRICE_GROUP_HBINS 1
+#endif
 #ifndef AIRICE_GROUP_ITEMS
 #define AIRICE_GROUP_ITEMS 8
 #endif
@@ -1125,7 +1128,9 @@ __global__ __launch_bounds__(kRootsBlock, AIRICE_ROOTS_WAVES) void roots_kernel(
 // queries in that order in small blocks that the CU replaces independently.  Each query is still
 // solved on its own and written by its index: results are identical either way.
 // ---------------------------------------------------------------------------
-constexpr int kGroupBuckets = AIRICE_GROUP_BUCKETS;
+constexpr int kGroupAngles = AIRICE_GROUP_BUCKETS;   // straight-line-angle classes
+constexpr int kGroupHeights = AIRICE_GROUP_HBINS;     // Tx-height classes within each
+constexpr int kGroupBuckets = kGroupAngles * kGroupHeights;
 constexpr int kGroupItems = AIRICE_GROUP_ITEMS;  // queries per thread in the sort passes
 constexpr int kGroupChunk = kBlock * kGroupItems;     // queries per block and round
 constexpr int kGroupBlocks = 512;                     // blocks of the sort passes (at most)
@@ -1136,7 +1141,7 @@ constexpr int kSortedBlock = AIRICE_SORTED_BS;
 // when x <= tan(90 deg * (1 - j / B)), so b counts the host-computed thresholds x lies below.
 // (The key only orders the work; results do not depend on it.)
 struct GroupKey {
-  double t[kGroupBuckets];  // t[j - 1] = tan(90 deg * (1 - j / B)), j = 1 .. B-1
+  double t[kGroupAngles];  // t[j - 1] = tan(90 deg * (1 - j / B)), j = 1 .. B-1
 };
 
 template <int IN>
@@ -1146,10 +1151,17 @@ __device__ __forceinline__ int query_bucket(const DevMedium& M, const QueryArgs&
   double thR_unused;
   const Geometry g = load_query<IN>(M, Q, k, thR_unused);
   const double den = g.H - g.ice - g.depth;
-  if (!(den > 0)) return den < 0 ? kGroupBuckets - 1 : 0;  // thR > 180 (clamped) / 90 or NaN
   int b = 0;
+  if (!(den > 0)) {
+    b = den < 0 ? kGroupAngles - 1 : 0;  // thR > 180 (clamped) / 90 or NaN
+  } else {
 #pragma unroll
-  for (int j = 0; j < kGroupBuckets - 1; ++j) b += (g.D <= K.t[j] * den) ? 1 : 0;
+    for (int j = 0; j < kGroupAngles - 1; ++j) b += (g.D <= K.t[j] * den) ? 1 : 0;
+  }
+  if (kGroupHeights > 1) {  // Tx height between the ice and the top of the atmosphere
+    const double h = (g.H - g.ice) / (M.atm[kMaxLayers] - g.ice) * kGroupHeights;
+    b = b * kGroupHeights + ((h > 0) ? ((h < kGroupHeights) ? (int)h : kGroupHeights - 1) : 0);
+  }
   return b;
 }
 
@@ -1460,7 +1472,7 @@ static int launch_roots(const DevMedium& M, const IceConsts& I, const QueryArgs&
   }
   static const GroupKey key_t = [] {
     GroupKey K{};
-    for (int j = 1; j < kGroupBuckets; ++j) K.t[j - 1] = tan(M_PI / 2 * (1.0 - (double)j / kGroupBuckets));
+    for (int j = 1; j < kGroupAngles; ++j) K.t[j - 1] = tan(M_PI / 2 * (1.0 - (double)j / kGroupAngles));
     return K;
   }();
   // at most kGroupBlocks blocks in the two passes (each scatter block reads every block's
