@@ -1205,6 +1205,11 @@ __global__ __launch_bounds__(kBlock) void group_scatter_kernel(const int8_t* __r
   __shared__ int s_tot[kGroupBuckets][kLanesPerBucket], s_pre[kGroupBuckets][kLanesPerBucket];
   __shared__ int s_base[kGroupBuckets];
   const int nb = gridDim.x, blk = blockIdx.x;
+  // this block's first-round keys, loaded before the prefix work so their latency overlaps it
+  int b0[kGroupItems];
+  const long long kb = (long long)blk * rounds * kGroupChunk + threadIdx.x;
+#pragma unroll
+  for (int i = 0; i < kGroupItems; ++i) b0[i] = kb + i * kBlock < n ? (int)key[kb + i * kBlock] : -1;
   {
     const int bb = threadIdx.x / kLanesPerBucket, l = threadIdx.x % kLanesPerBucket;
     const int* c = cnt + (long long)bb * nb;
@@ -1236,7 +1241,7 @@ __global__ __launch_bounds__(kBlock) void group_scatter_kernel(const int8_t* __r
 #pragma unroll
     for (int i = 0; i < kGroupItems; ++i) {
       const long long k = k0 + i * kBlock;
-      const int b = k < n ? (int)key[k] : -1;
+      const int b = rr == 0 ? b0[i] : (k < n ? (int)key[k] : -1);
       if (b >= 0) perm[atomicAdd(&s_base[b], 1)] = (int)k;
     }
   }
