@@ -1061,7 +1061,10 @@ constexpr int kRootsBlock = AIRICE_ROOTS_BS;
 #define AIRICE_GROUP_HBINS 1
 #endif
 #ifndef AIRICE_GROUP_ITEMS
-#define AIRICE_GROUP_ITEMS 8
+#define AIRICE_GROUP_ITEMS 2
+#endif
+#ifndef AIRICE_GROUP_THREADS
+#define AIRICE_GROUP_THREADS 1024
 #endif
 #ifndef AIRICE_SORTED_WAVES
 #define AIRICE_SORTED_WAVES AIRICE_ROOTS_WAVES
@@ -1132,7 +1135,8 @@ constexpr int kGroupAngles = AIRICE_GROUP_BUCKETS;   // straight-line-angle clas
 constexpr int kGroupHeights = AIRICE_GROUP_HBINS;     // Tx-height classes within each
 constexpr int kGroupBuckets = kGroupAngles * kGroupHeights;
 constexpr int kGroupItems = AIRICE_GROUP_ITEMS;  // queries per thread in the sort passes
-constexpr int kGroupChunk = kBlock * kGroupItems;     // queries per block and round
+constexpr int kGroupThreads = AIRICE_GROUP_THREADS;  // threads per block of the sort passes
+constexpr int kGroupChunk = kGroupThreads * kGroupItems;  // queries per block and round
 constexpr int kGroupBlocks = 512;                     // blocks of the sort passes (at most)
 constexpr int kSortedBlock = AIRICE_SORTED_BS;
 
@@ -1167,11 +1171,13 @@ __device__ __forceinline__ int query_bucket(const DevMedium& M, const QueryArgs&
 
 // Pass 1: the key of every query and each block's bucket counts, bucket-major:
 // cnt[b * nblocks + block] (no global atomics: thousands of blocks adding into a few counters
-// serialise on them).
+// serialise on them).  Both passes use at most kGroupBlocks blocks of kGroupThreads threads
+// (8 waves/SIMD when the batch fills them), each block taking `rounds` chunks in turn.
 template <int IN>
-__global__ __launch_bounds__(kBlock) void group_count_kernel(DevMedium M, QueryArgs Q, GroupKey K,
-                                                             int rounds, int8_t* __restrict__ key,
-                                                             int* __restrict__ cnt) {
+__global__ __launch_bounds__(kGroupThreads) void group_count_kernel(DevMedium M, QueryArgs Q,
+                                                                    GroupKey K, int rounds,
+                                                                    int8_t* __restrict__ key,
+                                                                    int* __restrict__ cnt) {
   __shared__ int s_c[kGroupBuckets];
   if (threadIdx.x < kGroupBuckets) s_c[threadIdx.x] = 0;
   __syncthreads();
@@ -1179,7 +1185,7 @@ __global__ __launch_bounds__(kBlock) void group_count_kernel(DevMedium M, QueryA
     const long long k0 = ((long long)blockIdx.x * rounds + rr) * kGroupChunk + threadIdx.x;
 #pragma unroll
     for (int i = 0; i < kGroupItems; ++i) {
-      const long long k = k0 + i * kBlock;
+      const long long k = k0 + i * kGroupThreads;
       if (k < Q.n) {
         const int b = query_bucket<IN>(M, Q, k, K);
         key[k] = (int8_t)b;
@@ -1193,15 +1199,15 @@ __global__ __launch_bounds__(kBlock) void group_count_kernel(DevMedium M, QueryA
 
 // Pass 2: perm[position] = query index, positions grouped by bucket.  Each block first derives
 // its own first position per bucket from all blocks' counts (bucket b's earlier buckets in full,
-// plus bucket b of the blocks before it): 16 lanes per bucket sum strided slices of cnt[], so no
-// separate scan pass is needed.  A block's queries of one bucket take consecutive positions.
-static_assert(kBlock % kGroupBuckets == 0, "lanes per bucket");
-constexpr int kLanesPerBucket = kBlock / kGroupBuckets;
-__global__ __launch_bounds__(kBlock) void group_scatter_kernel(const int8_t* __restrict__ key,
-                                                               long long n, int rounds,
-                                                               const int* __restrict__ cnt,
-                                                               int* __restrict__ grouped,
-                                                               int* __restrict__ perm) {
+// plus bucket b of the blocks before it): kLanesPerBucket lanes per bucket sum strided slices of
+// cnt[] and a tree in LDS adds them up, so no separate scan pass is needed.  A block's queries
+// of one bucket take consecutive positions.
+static_assert(kGroupThreads % kGroupBuckets == 0, "lanes per bucket");
+constexpr int kLanesPerBucket = kGroupThreads / kGroupBuckets;
+static_assert((kLanesPerBucket & (kLanesPerBucket - 1)) == 0, "power-of-two lanes per bucket");
+__global__ __launch_bounds__(kGroupThreads) void group_scatter_kernel(
+    const int8_t* __restrict__ key, long long n, int rounds, const int* __restrict__ cnt,
+    int* __restrict__ grouped, int* __restrict__ perm) {
   __shared__ int s_tot[kGroupBuckets][kLanesPerBucket], s_pre[kGroupBuckets][kLanesPerBucket];
   __shared__ int s_base[kGroupBuckets];
   const int nb = gridDim.x, blk = blockIdx.x;
@@ -1209,12 +1215,13 @@ __global__ __launch_bounds__(kBlock) void group_scatter_kernel(const int8_t* __r
   int b0[kGroupItems];
   const long long kb = (long long)blk * rounds * kGroupChunk + threadIdx.x;
 #pragma unroll
-  for (int i = 0; i < kGroupItems; ++i) b0[i] = kb + i * kBlock < n ? (int)key[kb + i * kBlock] : -1;
+  for (int i = 0; i < kGroupItems; ++i)
+    b0[i] = kb + i * kGroupThreads < n ? (int)key[kb + i * kGroupThreads] : -1;
+  const int bb = threadIdx.x / kLanesPerBucket, l = threadIdx.x % kLanesPerBucket;
   {
-    const int bb = threadIdx.x / kLanesPerBucket, l = threadIdx.x % kLanesPerBucket;
     const int* c = cnt + (long long)bb * nb;
     int tot = 0, pre = 0;
-#pragma unroll 8
+#pragma unroll 4
     for (int j = l; j < nb; j += kLanesPerBucket) {
       const int v = c[j];
       tot += v;
@@ -1224,23 +1231,27 @@ __global__ __launch_bounds__(kBlock) void group_scatter_kernel(const int8_t* __r
     s_pre[bb][l] = pre;
   }
   __syncthreads();
-  if (threadIdx.x < kGroupBuckets) {
-    int base = 0;
-    for (int b = 0; b < (int)threadIdx.x; ++b)
-      for (int l = 0; l < kLanesPerBucket; ++l) base += s_tot[b][l];
-    for (int l = 0; l < kLanesPerBucket; ++l) base += s_pre[threadIdx.x][l];
-    s_base[threadIdx.x] = base;
-    if (blk == 0 && threadIdx.x == kGroupBuckets - 1) {  // number of queries with a bucket
-      for (int l = 0; l < kLanesPerBucket; ++l) base += s_tot[kGroupBuckets - 1][l];
-      *grouped = base;
+#pragma unroll
+  for (int h = kLanesPerBucket / 2; h > 0; h >>= 1) {
+    if (l < h) {
+      s_tot[bb][l] += s_tot[bb][l + h];
+      s_pre[bb][l] += s_pre[bb][l + h];
     }
+    __syncthreads();
+  }
+  if (threadIdx.x < kGroupBuckets) {
+    int base = s_pre[threadIdx.x][0];
+    for (int b = 0; b < (int)threadIdx.x; ++b) base += s_tot[b][0];
+    s_base[threadIdx.x] = base;
+    if (blk == 0 && threadIdx.x == kGroupBuckets - 1)  // number of queries with a bucket
+      *grouped = base + s_tot[kGroupBuckets - 1][0];
   }
   __syncthreads();
   for (int rr = 0; rr < rounds; ++rr) {
     const long long k0 = ((long long)blk * rounds + rr) * kGroupChunk + threadIdx.x;
 #pragma unroll
     for (int i = 0; i < kGroupItems; ++i) {
-      const long long k = k0 + i * kBlock;
+      const long long k = k0 + i * kGroupThreads;
       const int b = rr == 0 ? b0[i] : (k < n ? (int)key[k] : -1);
       if (b >= 0) perm[atomicAdd(&s_base[b], 1)] = (int)k;
     }
@@ -1493,9 +1504,9 @@ static int launch_roots(const DevMedium& M, const IceConsts& I, const QueryArgs&
   int* grouped = cnt + m;
   int* perm = grouped + 1;
   int8_t* key = reinterpret_cast<int8_t*>(perm + n);
-  hipLaunchKernelGGL(group_count_kernel<IN>, dim3(nb), dim3(kBlock), 0, st, M, Q, key_t, rounds,
+  hipLaunchKernelGGL(group_count_kernel<IN>, dim3(nb), dim3(kGroupThreads), 0, st, M, Q, key_t, rounds,
                      key, cnt);
-  hipLaunchKernelGGL(group_scatter_kernel, dim3(nb), dim3(kBlock), 0, st, key, (long long)n,
+  hipLaunchKernelGGL(group_scatter_kernel, dim3(nb), dim3(kGroupThreads), 0, st, key, (long long)n,
                      rounds, cnt, grouped, perm);
   hipLaunchKernelGGL(roots_sorted_kernel<IN>, dim3((unsigned)((n + kSortedBlock - 1) / kSortedBlock)),
                      dim3(kSortedBlock), 0, st, M, I, Q, park, perm, grouped);
