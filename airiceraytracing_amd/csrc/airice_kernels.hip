@@ -1449,7 +1449,7 @@ static inline dim3 roots_grid(size_t n) {
 // Stream-ordered scratch for the grouping passes: a library-owned pool per device whose release
 // threshold keeps freed blocks for reuse (the default pool returns them at every synchronisation,
 // and re-growing it made each launch wait on the host).
-static hipError_t scratch_alloc(void** p, size_t bytes, hipStream_t st) {
+hipError_t scratch_alloc(void** p, size_t bytes, hipStream_t st) {
   static std::mutex mu;
   static std::vector<hipMemPool_t> pools;
   int dev = 0;
@@ -1472,16 +1472,21 @@ static hipError_t scratch_alloc(void** p, size_t bytes, hipStream_t st) {
   return hipMallocFromPoolAsync(p, bytes, pool, st);
 }
 
+size_t group_min_batch() {
+  static const long long v = getenv("AIRICE_GROUP_MIN") ? atoll(getenv("AIRICE_GROUP_MIN"))
+                                                         : AIRICE_GROUP_MIN;
+  return v > 0 ? (size_t)v : 0;
+}
+
 // Stage 1 of every minimizer launch: roots_kernel (block-local grouping) for small batches and
 // debug statistics, the batch-wide grouping otherwise (stream-ordered scratch from the HIP pool).
 template <int IN>
 static int launch_roots(const DevMedium& M, const IceConsts& I, const QueryArgs& Q,
                         const Park& park, size_t n, hipStream_t st) {
-  static const int group_min = getenv("AIRICE_GROUP_MIN") ? atoi(getenv("AIRICE_GROUP_MIN"))
-                                                           : AIRICE_GROUP_MIN;
+  const size_t group_min = group_min_batch();
   // (the table lookup's fallback pass stays block-local: its batch is the whole lookup batch,
   // of which typically well under 1 % of lanes are fallback lanes)
-  if (IN == IN_CM100 || group_min <= 0 || n < (size_t)group_min || park.stats != nullptr ||
+  if (IN == IN_CM100 || group_min == 0 || n < group_min || park.stats != nullptr ||
       n >= (1ull << 31)) {
     hipLaunchKernelGGL(roots_kernel<IN>, roots_grid(n), dim3(kRootsBlock), 0, st, M, I, Q, park);
     return launch_ok();
