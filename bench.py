@@ -46,6 +46,8 @@ def parse():
     p.add_argument("--no-solve", action="store_true", help="skip the minimizer line item")
     p.add_argument("--no-lookup", action="store_true", help="skip the table-lookup line item")
     p.add_argument("--no-pcie", action="store_true", help="skip the table-to-host line item")
+    p.add_argument("--no-multi", action="store_true",
+                   help="skip the several-antenna line item (tables on concurrent streams)")
     p.add_argument("--default-grid", action="store_true",
                    help="also time the reference default grid (8.7M rays; off by default so "
                         "every table_kernel launch of the run is the cfg2 workload)")
@@ -282,6 +284,38 @@ def main():
             "value": args.lookup_n / (lms * 1e-3), "unit": "lookups/s", "ms": lms,
             "ok_fraction": float(lok.cpu().numpy().mean()),
             "pack_ms": pack_ms, "packed": True}
+    if not args.no_multi:
+        # Several antennas' cfg2 tables (MakeRayTracingTable per AntennaNumber, .cc:2019) built
+        # concurrently, one HIP stream per antenna: a single table's launch ramp and drain
+        # (~15 us of its 36 us) overlap the other antennas' work.  Secondary
+        # line item; the headline above stays one table per step on one stream.
+        multi = {}
+        for n_ant in (2, 4):
+            grids = [make_grid(depth_cm - 1000.0 * a, CFG2["ice_cm"], CFG2["height_step"],
+                               CFG2["start_angle"], CFG2["stop_angle"], CFG2["angle_step"])
+                     for a in range(n_ant)]
+            tabs = [torch.empty((11, g.n_rays), dtype=torch.float32, device=dev) for g in grids]
+            streams = [torch.cuda.Stream(device=dev) for _ in range(n_ant)]
+            rays = sum(g.n_rays for g in grids)
+
+            def build_all():
+                for g, t, s_ in zip(grids, tabs, streams):
+                    solver.table_device(g, t, None, stream=s_)
+
+            for _ in range(3):
+                build_all()
+            torch.cuda.synchronize()
+            reps = 50
+            t1 = time.perf_counter()
+            for _ in range(reps):
+                build_all()
+            torch.cuda.synchronize()
+            sec = time.perf_counter() - t1
+            multi[f"{n_ant}_antennas"] = {"rays_per_s": rays * reps / sec,
+                                          "ms_per_round": sec / reps * 1e3}
+        extra["multi_antenna_tables"] = {
+            "metric": "cfg2 tables of several antennas on concurrent HIP streams (rays/s)",
+            **multi}
     if not args.no_pcie:
         # host-buffer callers (AllTableAllAntData is host memory): table build + D2H copy of the
         # 11 float columns into pinned memory, in stream order; never the headline value
