@@ -1071,8 +1071,10 @@ constexpr int kRootsBlock = AIRICE_ROOTS_BS;
 #endif
 
 template <int IN>
-__global__ __launch_bounds__(kRootsBlock, AIRICE_ROOTS_WAVES) void roots_kernel(DevMedium M, IceConsts I, QueryArgs Q,
-                                                       Park park) {
+__global__ __launch_bounds__(kRootsBlock, AIRICE_ROOTS_WAVES) void roots_kernel(DevMedium M,
+                                                                                IceConsts I,
+                                                                                QueryArgs Q,
+                                                                                Park park) {
   __shared__ int s_count[kSortBuckets + 1];
   __shared__ int s_slot[kRootsBlock];
   // the log table in LDS (one 16-byte entry per thread), as in table_kernel: every evaluation's
@@ -1479,7 +1481,7 @@ size_t group_min_batch() {
 }
 
 // Stage 1 of every minimizer launch: roots_kernel (block-local grouping) for small batches and
-// debug statistics, the batch-wide grouping otherwise (stream-ordered scratch from the HIP pool).
+// debug statistics, the batch-wide grouping otherwise (stream-ordered scratch, scratch_alloc).
 template <int IN>
 static int launch_roots(const DevMedium& M, const IceConsts& I, const QueryArgs& Q,
                         const Park& park, size_t n, hipStream_t st) {
@@ -1491,9 +1493,10 @@ static int launch_roots(const DevMedium& M, const IceConsts& I, const QueryArgs&
     hipLaunchKernelGGL(roots_kernel<IN>, roots_grid(n), dim3(kRootsBlock), 0, st, M, I, Q, park);
     return launch_ok();
   }
-  static const GroupKey key_t = [] {
+  static const GroupKey thresholds = [] {
     GroupKey K{};
-    for (int j = 1; j < kGroupAngles; ++j) K.t[j - 1] = tan(M_PI / 2 * (1.0 - (double)j / kGroupAngles));
+    for (int j = 1; j < kGroupAngles; ++j)
+      K.t[j - 1] = tan(M_PI / 2 * (1.0 - (double)j / kGroupAngles));
     return K;
   }();
   // at most kGroupBlocks blocks in the two passes (each scatter block reads every block's
@@ -1509,12 +1512,13 @@ static int launch_roots(const DevMedium& M, const IceConsts& I, const QueryArgs&
   int* grouped = cnt + m;
   int* perm = grouped + 1;
   int8_t* key = reinterpret_cast<int8_t*>(perm + n);
-  hipLaunchKernelGGL(group_count_kernel<IN>, dim3(nb), dim3(kGroupThreads), 0, st, M, Q, key_t, rounds,
-                     key, cnt);
-  hipLaunchKernelGGL(group_scatter_kernel, dim3(nb), dim3(kGroupThreads), 0, st, key, (long long)n,
-                     rounds, cnt, grouped, perm);
-  hipLaunchKernelGGL(roots_sorted_kernel<IN>, dim3((unsigned)((n + kSortedBlock - 1) / kSortedBlock)),
-                     dim3(kSortedBlock), 0, st, M, I, Q, park, perm, grouped);
+  hipLaunchKernelGGL(group_count_kernel<IN>, dim3(nb), dim3(kGroupThreads), 0, st, M, Q,
+                     thresholds, rounds, key, cnt);
+  hipLaunchKernelGGL(group_scatter_kernel, dim3(nb), dim3(kGroupThreads), 0, st, key,
+                     (long long)n, rounds, cnt, grouped, perm);
+  const unsigned sorted_blocks = (unsigned)((n + kSortedBlock - 1) / kSortedBlock);
+  hipLaunchKernelGGL(roots_sorted_kernel<IN>, dim3(sorted_blocks), dim3(kSortedBlock), 0, st, M, I,
+                     Q, park, perm, grouped);
   const int rc = launch_ok();
   if (hipFreeAsync(ws, st) != hipSuccess) return AIRICE_EHIP;
   return rc;
