@@ -131,6 +131,7 @@ EXPORTED_SYMBOLS = (
     "airice_single_ray_launch", "airice_single_ray_host", "airice_trace_ice_to_air_launch",
     "airice_trace_ice_to_air_host", "airice_rtf_outputs", "airice_rtf_eval", "Py_TraceIceToAir", "airice_device_count", "airice_set_device", "airice_malloc",
     "airice_free", "airice_memcpy_h2d", "airice_memcpy_d2h", "airice_synchronize",
+    "airice_kernel_timing", "airice_kernel_time",
 )
 
 
@@ -200,6 +201,9 @@ def lib() -> ctypes.CDLL:
         "airice_memcpy_h2d": ([P, P, S], I),
         "airice_memcpy_d2h": ([P, P, S], I),
         "airice_synchronize": ([], I),
+        "airice_kernel_timing": ([I], I),
+        "airice_kernel_time": ([ctypes.c_char_p, ctypes.POINTER(D), ctypes.POINTER(ctypes.c_int64),
+                                I], I),
     }
     for name, (args, res) in sig.items():
         fn = getattr(L, name)
@@ -254,3 +258,17 @@ def load_medium(path: str | None = None, variant: int = VARIANT_MULTIRAY) -> Med
     check(lib().airice_atmosphere_parse(text, len(text), variant, ctypes.byref(m)),
           "airice_atmosphere_parse")
     return m
+
+
+def kernel_timing(on: bool) -> None:
+    """Bracket launches of the timed kernels with hipEvent pairs (airice_kernel_timing)."""
+    check(lib().airice_kernel_timing(1 if on else 0), "airice_kernel_timing")
+
+
+def kernel_time(name: str, reset: bool = True) -> tuple[float, int]:
+    """(summed ms, launches) of one timed kernel since the last reset (airice_kernel_time)."""
+    ms = ctypes.c_double(0.0)
+    cnt = ctypes.c_int64(0)
+    check(lib().airice_kernel_time(name.encode(), ctypes.byref(ms), ctypes.byref(cnt),
+                                   1 if reset else 0), "airice_kernel_time")
+    return ms.value, cnt.value

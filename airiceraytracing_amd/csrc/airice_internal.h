@@ -55,4 +55,16 @@ int launch_trace(const DevMedium& M, const IceConsts& I, const double* depth, co
 
 void set_error(const char* fmt, ...);
 
+// Kernel timing for the bench (airice_kernel_timing): when enabled, launches of the kernels
+// below are bracketed by a hipEvent pair on their stream.  Off by default: one relaxed load.
+enum KTimerId { KT_TABLE = 0, KT_ROOTS, KT_GROUP, KT_OUT, KT_LOOKUP, KT_COUNT };
+extern bool g_ktimer_on;
+void ktimer_record(int id, bool begin, hipStream_t st);
+inline void ktimer_begin(int id, hipStream_t st) {
+  if (g_ktimer_on) ktimer_record(id, true, st);
+}
+inline void ktimer_end(int id, hipStream_t st) {
+  if (g_ktimer_on) ktimer_record(id, false, st);
+}
+
 }  // namespace airice

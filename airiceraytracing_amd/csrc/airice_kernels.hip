@@ -1490,7 +1490,9 @@ static int launch_roots(const DevMedium& M, const IceConsts& I, const QueryArgs&
   // of which typically well under 1 % of lanes are fallback lanes)
   if (IN == IN_CM100 || group_min == 0 || n < group_min || park.stats != nullptr ||
       n >= (1ull << 31)) {
+    ktimer_begin(KT_ROOTS, st);
     hipLaunchKernelGGL(roots_kernel<IN>, roots_grid(n), dim3(kRootsBlock), 0, st, M, I, Q, park);
+    ktimer_end(KT_ROOTS, st);
     return launch_ok();
   }
   static const GroupKey thresholds = [] {
@@ -1512,13 +1514,17 @@ static int launch_roots(const DevMedium& M, const IceConsts& I, const QueryArgs&
   int* grouped = cnt + m;
   int* perm = grouped + 1;
   int8_t* key = reinterpret_cast<int8_t*>(perm + n);
+  ktimer_begin(KT_GROUP, st);
   hipLaunchKernelGGL(group_count_kernel<IN>, dim3(nb), dim3(kGroupThreads), 0, st, M, Q,
                      thresholds, rounds, key, cnt);
   hipLaunchKernelGGL(group_scatter_kernel, dim3(nb), dim3(kGroupThreads), 0, st, key,
                      (long long)n, rounds, cnt, grouped, perm);
+  ktimer_end(KT_GROUP, st);
   const unsigned sorted_blocks = (unsigned)((n + kSortedBlock - 1) / kSortedBlock);
+  ktimer_begin(KT_ROOTS, st);
   hipLaunchKernelGGL(roots_sorted_kernel<IN>, dim3(sorted_blocks), dim3(kSortedBlock), 0, st, M, I,
                      Q, park, perm, grouped);
+  ktimer_end(KT_ROOTS, st);
   const int rc = launch_ok();
   if (hipFreeAsync(ws, st) != hipSuccess) return AIRICE_EHIP;
   return rc;
@@ -1563,12 +1569,14 @@ int launch_table(const DevMedium& M, const IceConsts& I, const airice_grid* g, i
     const size_t lds = sizeof(RowConst) * (size_t)A.rows_per_block * R;
     const unsigned blocks = (unsigned)((A.half + kTableBlock - 1) / kTableBlock);
     if (trace_path == nullptr) {
+      ktimer_begin(KT_TABLE, st);
       if (AIRICE_TABLE_R2 && R == 2)
         hipLaunchKernelGGL((table_kernel<kTableBlock, 1 + AIRICE_TABLE_R2, false>), dim3(blocks),
                            dim3(kTableBlock), lds, st, M, I, A, tab, full, nullptr);
       else
         hipLaunchKernelGGL((table_kernel<kTableBlock, 1, false>), dim3(blocks), dim3(kTableBlock),
                            lds, st, M, I, A, tab, full, nullptr);
+      ktimer_end(KT_TABLE, st);
       if (hipGetLastError() != hipSuccess) return AIRICE_EHIP;
       continue;
     }
@@ -1625,12 +1633,14 @@ int launch_solve(const DevMedium& M, const IceConsts& I, int variant, const doub
       fclose(f);
     }
   }
+  ktimer_begin(KT_OUT, st);
   if (variant == AIRICE_VARIANT_MULTIRAY)
     hipLaunchKernelGGL(solve_out_kernel<AIRICE_VARIANT_MULTIRAY>, grid, block, 0, st, M, I, Q, out,
                        ld, status);
   else
     hipLaunchKernelGGL(solve_out_kernel<AIRICE_VARIANT_PYWRAPPER>, grid, block, 0, st, M, I, Q,
                        out, ld, status);
+  ktimer_end(KT_OUT, st);
   return launch_ok();
 }
 
@@ -1642,7 +1652,9 @@ int launch_hdtip(const DevMedium& M, const IceConsts& I, const double* src, cons
   const Park park{out + 4 * ld, out, 1, bisect_exact(), nullptr};
   const dim3 grid(grid_for((long long)n)), block(kBlock);
   if (int rc = launch_roots<IN_CM>(M, I, Q, park, n, st)) return rc;
+  ktimer_begin(KT_OUT, st);
   hipLaunchKernelGGL(hdtip_out_kernel, grid, block, 0, st, M, I, Q, out, ld, ok);
+  ktimer_end(KT_OUT, st);
   return launch_ok();
 }
 
@@ -1668,7 +1680,9 @@ int launch_trace(const DevMedium& M, const IceConsts& I, const double* depth, co
   const Park park{out10 + 5, out10 + 9, 10, bisect_exact(), nullptr};
   const dim3 grid(grid_for((long long)n)), block(kBlock);
   if (int rc = launch_roots<IN_TRACE>(M, I, Q, park, n, st)) return rc;
+  ktimer_begin(KT_OUT, st);
   hipLaunchKernelGGL(trace_out_kernel, grid, block, 0, st, M, I, Q, out10);
+  ktimer_end(KT_OUT, st);
   return launch_ok();
 }
 

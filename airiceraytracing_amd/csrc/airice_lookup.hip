@@ -328,8 +328,10 @@ int launch_lookup(const DevMedium& M, const IceConsts& I, const airice_lookup_ta
   T.hsteps = t->total_height_steps;
   T.asteps = t->total_angle_steps;
   const unsigned grid = (unsigned)((n + kLkBlock - 1) / kLkBlock);
+  ktimer_begin(KT_LOOKUP, st);
   hipLaunchKernelGGL(lookup_kernel, dim3(grid), dim3(kLkBlock), 0, st, T, src, dist, ice_cm,
                      (long long)n, M.d2r, out, ld, ok, flags);
+  ktimer_end(KT_LOOKUP, st);
   if (hipGetLastError() != hipSuccess) return AIRICE_EHIP;
   return launch_lookup_fallback(M, I, src, dist, depth, ice_cm, n, out, ld, ok, flags, st);
 }

@@ -251,9 +251,70 @@ void build_ice_consts(const DevMedium& M, double ice_h, double rx_depth, IceCons
   out->iceseg = make_segconst(out->ice0, rx);
 }
 
+// ---- kernel timer (bench only) ---------------------------------------------------------
+bool g_ktimer_on = false;
+static std::mutex g_kt_mu;
+struct KtPair {
+  hipEvent_t a = nullptr, b = nullptr;
+};
+static std::vector<KtPair> g_kt_done[KT_COUNT];   // closed pairs
+static KtPair g_kt_open[KT_COUNT];                // pair whose end is pending
+static const char* const kKtNames[KT_COUNT] = {"table_kernel", "roots_kernel", "group_passes",
+                                               "out_kernel", "lookup_kernel"};
+
+void ktimer_record(int id, bool begin, hipStream_t st) {
+  std::lock_guard<std::mutex> lock(g_kt_mu);
+  if (begin) {
+    KtPair p;
+    if (hipEventCreate(&p.a) != hipSuccess || hipEventCreate(&p.b) != hipSuccess) return;
+    (void)hipEventRecord(p.a, st);
+    g_kt_open[id] = p;
+  } else if (g_kt_open[id].a != nullptr) {
+    (void)hipEventRecord(g_kt_open[id].b, st);
+    g_kt_done[id].push_back(g_kt_open[id]);
+    g_kt_open[id] = KtPair();
+  }
+}
+
 }  // namespace airice
 
 using namespace airice;
+
+extern "C" int airice_kernel_timing(int on) {
+  g_ktimer_on = on != 0;
+  return AIRICE_OK;
+}
+
+extern "C" int airice_kernel_time(const char* name, double* total_ms, int64_t* launches,
+                                  int reset) {
+  int id = -1;
+  for (int i = 0; i < KT_COUNT; ++i)
+    if (name != nullptr && std::strcmp(name, kKtNames[i]) == 0) id = i;
+  if (id < 0) {
+    set_error("unknown timed kernel '%s'", name ? name : "(null)");
+    return AIRICE_EINVAL;
+  }
+  std::lock_guard<std::mutex> lock(g_kt_mu);
+  double sum = 0;
+  for (KtPair& p : g_kt_done[id]) {
+    float ms = 0;
+    if (hipEventSynchronize(p.b) != hipSuccess || hipEventElapsedTime(&ms, p.a, p.b) != hipSuccess) {
+      set_error("kernel timer: event query failed");
+      return AIRICE_EHIP;
+    }
+    sum += ms;
+  }
+  if (total_ms) *total_ms = sum;
+  if (launches) *launches = (int64_t)g_kt_done[id].size();
+  if (reset) {
+    for (KtPair& p : g_kt_done[id]) {
+      (void)hipEventDestroy(p.a);
+      (void)hipEventDestroy(p.b);
+    }
+    g_kt_done[id].clear();
+  }
+  return AIRICE_OK;
+}
 
 #define HIP_TRY(expr)                                                          \
   do {                                                                         \

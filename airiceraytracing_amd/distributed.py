@@ -78,3 +78,67 @@ def gpu_table_compute(solver, grid, stream=None):
         solver.table_device(grid, out, None, row_begin=begin, row_count=count,
                             ld=out.shape[1], stream=stream)
     return compute
+
+
+def sharded_step_grid_step(base_step: float, world: int) -> float:
+    """TxH step of the N-GPU weak-scaling table: the base grid refined N-fold in TxH, so each
+    of the N contiguous row slabs holds about as many rows as the base grid."""
+    return base_step / world
+
+
+def run_sharded_table(grid, compute: Callable[[int, int, torch.Tensor], None], steps: int,
+                      warmup: int, device=None, coll_device=None, sync: Callable[[], None] = None,
+                      gather_reps: int = 3, cols: int = 11, dtype=torch.float32, root: int = 0,
+                      group=None) -> dict:
+    """The north_star's multi-GPU table: rank r builds its contiguous slab of TxH rows
+    (shard_rows; the TxH-descending / angle-ascending order the lookup expects,
+    MultiRayAirIceRefraction.cc:1035-1039) ``steps`` times between barriers, then the slabs
+    are assembled on ``root`` by one gather (RCCL over xGMI for backend "nccl"), timed in its
+    own barrier bracket ``gather_reps`` times.  The reference assembles one table the same way
+    in its row loop (.cc:2079-2136).  ``compute(row_begin, row_count, slab)`` fills the slab
+    (stride = rows_per_rank x angle_steps); ``sync`` waits for the device (torch.cuda.synchronize
+    on a GPU).  Returns the per-rank timings reduced by max over ranks and, on root, the
+    assembled (cols, n_rays) table."""
+    import time
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    sync = sync or (lambda: None)
+    coll_device = coll_device if coll_device is not None else device
+    asteps = int(grid.angle_steps)
+    begin, count, per = shard_rows(int(grid.height_steps), world, rank)
+    slab = torch.zeros((cols, per * asteps), dtype=dtype, device=device)
+
+    def step():
+        if count:
+            compute(begin, count, slab)
+
+    for _ in range(warmup):
+        step()
+    sync()
+    dist.barrier(group)
+    sync()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    sync()
+    elapsed = time.perf_counter() - t0
+    dist.barrier(group)
+    counts = [shard_rows(int(grid.height_steps), world, r)[1] * asteps for r in range(world)]
+    send = slab if coll_device is None or slab.device == torch.device(coll_device) \
+        else slab.to(coll_device)
+    assembled = None
+    gather_s = []
+    for _ in range(max(1, gather_reps)):
+        sync()
+        dist.barrier(group)
+        g0 = time.perf_counter()
+        assembled = gather_slabs(send, per * asteps, counts, root, group)
+        sync()
+        gather_s.append(time.perf_counter() - g0)
+    red = torch.tensor([elapsed, min(gather_s)], dtype=torch.float64, device=coll_device)
+    dist.all_reduce(red, op=dist.ReduceOp.MAX, group=group)
+    return {"elapsed_s": float(red[0]), "gather_s": float(red[1]), "row_begin": begin,
+            "row_count": count, "rows_per_rank": per, "rays_this_rank": count * asteps,
+            "bytes_to_root": sum(counts[r] for r in range(world) if r != root) * cols
+            * slab.element_size(),
+            "slab": slab, "assembled": assembled}

@@ -6,14 +6,22 @@ Workload (N=1): BASELINE cfg2 = MakeRayTracingTable on one MI355X, TxH 100000 ->
 4,851 x 177 = 858,627 rays per step.  One step = one table build, i.e.
 one launch of table_kernel writing the 11 float columns of AllTableAllAntData into HBM.
 
-N>1 (torch.distributed.run, one process per GPU): weak scaling -- rank r builds the table
-of its own antenna (depth 200 + 10 r m), as the reference builds one table per antenna
-(RunMultiRayCode.C:29-52); no collective in the data path.  Timing: W untimed warm-up
-steps, then K steps bracketed by barrier + synchronize, max over ranks.
+N>1 (torch.distributed.run, one process per GPU), default ``--mode sharded``: the
+north_star's design -- one table over the (TxH x angle) grid, split into contiguous TxH-row
+slabs, one slab per GPU, assembled on rank 0 by one RCCL gather over xGMI
+(airiceraytracing_amd.distributed.run_sharded_table; the reference assembles its table in the
+row loop MultiRayAirIceRefraction.cc:2079-2136).  Weak scaling: the grid is cfg2 refined N-fold
+in TxH (step 20/N m), so every GPU builds about one cfg2 table per step.  The gather is timed
+in its own barrier bracket (``sharded.gather_ms``); ``value`` counts the steps only and
+``sharded.value_incl_gather`` adds one gather per step.  ``--mode replicas``: one antenna table
+per GPU, no collective (RunMultiRayCode.C:29-52).  Timing: W untimed warm-up steps, then K
+steps bracketed by barrier + synchronize, max over ranks.
 
-Also reported: the minimizer (cfg3, 1e6 Air2IceRayTracing solves) as a secondary line item,
-the roofline of table_kernel (FP64 VALU bound), the CPU baseline (the oracle, OpenMP, on
-the box's host cores, on the same cfg2 grid) and max |delta| of the GPU table vs the CPU path.
+Also reported (rank 0): the roofline of table_kernel from executed FP64 VALU instructions
+(profiles/pmc_summary.json) over the live kernel time; the minimizer (cfg3, 1e6 Air2IceRayTracing
+solves) with its own roofline, CPU baseline and parity on a stride of the timed batch; the
+pythonwrapper batch (cfg5, 1e7 Py_TraceIceToAir rows) with parity; the table lookup; the CPU
+baseline of the table (the oracle, OpenMP on the box's host cores) and the table's parity.
 """
 from __future__ import annotations
 
@@ -29,10 +37,19 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 # FP64 VALU peak of one MI355X: 256 CU x 64 FP64 lane-ops/clk x 2.4 GHz (= 78.6 TFLOP/s with
-# FMA counted twice; MI355X spec FP64 vector rate).  Work is counted in lane-ops.
+# FMA counted twice; MI355X spec FP64 vector rate).  Work is counted in lane-ops (one executed
+# FP64 VALU instruction x 64 lanes = 64 lane-ops, FMA = 1).
 PEAK_FP64_VALU_TOPS = 256 * 64 * 2.4e9 / 1e12
 CFG2 = dict(depth_cm=-20000.0, ice_cm=300000.0, height_step=20.0, start_angle=92.0,
             stop_angle=180.0, angle_step=0.5)
+# survey-session probe of the real reference (8-core container Xeon, g++ -O2,
+# compiled against a GSL stand-in): quoted beside the oracle's CPU baseline, never measured here
+SURVEY_REFERENCE_PROBE = {
+    "table_rays_per_s": {"1_thread": 2.42e5, "8_threads": 5.58e5},
+    "minimizer_solves_per_s": {"1_thread": 8.80e3, "8_threads": 6.22e4},
+    "py_trace_ice_to_air_ms_per_call": 12.1,
+    "source": "BASELINE.md §2 (survey container, not this box)"}
+PMC_FILE = os.path.join(ROOT, "profiles", "pmc_summary.json")
 
 
 def parse():
@@ -40,48 +57,101 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=50)
     p.add_argument("--warmup", type=int, default=5)
+    p.add_argument("--mode", choices=("sharded", "replicas"), default="sharded",
+                   help="N>1: one table sharded by TxH rows + RCCL gather (default), or one "
+                        "antenna table per GPU")
     p.add_argument("--solve-n", type=int, default=1_000_000)
     p.add_argument("--solve-steps", type=int, default=5)
-    p.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
+    p.add_argument("--no-cpu", action="store_true", help="skip the CPU legs (baselines, parity)")
     p.add_argument("--no-solve", action="store_true", help="skip the minimizer line item")
     p.add_argument("--no-lookup", action="store_true", help="skip the table-lookup line item")
     p.add_argument("--no-pcie", action="store_true", help="skip the table-to-host line item")
     p.add_argument("--no-multi", action="store_true",
                    help="skip the several-antenna line item (tables on concurrent streams)")
+    p.add_argument("--no-scalar", action="store_true", help="skip the scalar-call latencies")
     p.add_argument("--default-grid", action="store_true",
                    help="also time the reference default grid (8.7M rays; off by default so "
                         "every table_kernel launch of the run is the cfg2 workload)")
     p.add_argument("--lookup-n", type=int, default=1_000_000)
     p.add_argument("--trace-n", type=int, default=10_000_000)
     p.add_argument("--no-trace", action="store_true", help="skip the cfg5 pythonwrapper line item")
-    p.add_argument("--cpu-threads", type=int, default=16)
+    p.add_argument("--cpu-threads", type=int, default=16,
+                   help="host threads of the CPU legs (the GPU box's CPU share is 16 per GPU)")
     p.add_argument("--cpu-seconds", type=float, default=10.0,
-                   help="wall time of the CPU-baseline sample (whole cfg2 grids)")
+                   help="wall time of each CPU-baseline sample")
+    p.add_argument("--parity-stride", type=int, default=97,
+                   help="every k-th query of the timed batches is checked against the oracle")
     return p.parse_args()
 
 
-def load_opweights():
+def load_pmc() -> dict:
+    try:
+        with open(PMC_FILE) as f:
+            return json.load(f)
+    except (OSError, ValueError):
+        return {}
+
+
+def cpu_info(nthr: int) -> dict:
+    model = None
+    try:
+        with open("/proc/cpuinfo") as f:
+            for ln in f:
+                if ln.startswith("model name"):
+                    model = ln.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except AttributeError:
+        aff = os.cpu_count()
+    return {"cpu_model": model, "threads_used": nthr, "affinity_cpus": aff,
+            "compiler": "gcc -O2 -ffp-contract=off -fopenmp (oracle/Makefile)"}
+
+
+def counter_roofline(kernel_key: str, units: int, kernel_ms: float, pmc: dict,
+                     algorithmic_bytes_per_unit: float) -> dict:
+    """Roofline of one kernel from its executed FP64 VALU instructions (PMC, per unit) over the
+    live kernel time: achieved = FP64 lane-ops per launch / launch duration."""
+    p = pmc.get(kernel_key, {})
+    ops_per_unit = p.get("fp64_valu_insts_per_unit")
+    achieved = (ops_per_unit * units / (kernel_ms * 1e-3) / 1e12
+                if ops_per_unit and kernel_ms else None)
+    traffic_per_unit = (p["hbm_bytes_per_launch"] / p["units_per_launch"]
+                        if p.get("hbm_bytes_per_launch") and p.get("units_per_launch") else None)
+    return {
+        "bound": "valu",
+        "kernel": p.get("kernel", kernel_key),
+        "achieved": achieved, "peak": PEAK_FP64_VALU_TOPS,
+        "unit": "TFLOP/s (FP64 VALU lane-ops/s x 1e-12, FMA = 1)",
+        "frac": achieved / PEAK_FP64_VALU_TOPS if achieved else None,
+        "traffic": traffic_per_unit * units if traffic_per_unit else None,
+        "work_source": "executed FP64 VALU instructions (SQ_INSTS_VALU_{ADD,MUL,FMA,TRANS}_F64 "
+                       "x 64 lanes) per unit from " + os.path.relpath(PMC_FILE, ROOT),
+        "fp64_lane_ops_per_unit": ops_per_unit,
+        "valu_insts_per_unit": p.get("valu_insts_per_unit"),
+        "valu_busy_pct": p.get("valu_busy_pct"),
+        "units_per_launch": units, "kernel_ms": kernel_ms,
+        "hbm_bytes_per_launch_algorithmic": algorithmic_bytes_per_unit * units,
+        "hbm_GBps_algorithmic": algorithmic_bytes_per_unit * units / (kernel_ms * 1e-3) / 1e9
+        if kernel_ms else None,
+    }
+
+
+def ocml_priced(grid, rays: int, kernel_ms: float) -> dict:
+    """Secondary figure: the algorithm's FP64 work priced at the gfx950 ocml cost of each
+    function (tools/workmodel.py, tools/opweights.json).  The kernel runs cheaper forms of the
+    same functions, so this is NOT a hardware fraction."""
+    from tools.workmodel import ray_ops, segments_per_ray
     with open(os.path.join(ROOT, "tools", "opweights.json")) as f:
-        return json.load(f)
-
-
-def table_work_per_ray(grid, weights) -> tuple[float, dict]:
-    """Algorithmic FP64 VALU lane-ops per table ray: per-segment counts of
-    the CSE'd kernel x the number of segments of each ray of the grid, + per-ray terms."""
-    from tools.workmodel import segments_per_ray, ray_ops
+        weights = json.load(f)
     segs = segments_per_ray(grid)
     ops = ray_ops(segs, weights, rays_per_row=grid.angle_steps)
-    return ops["W"], {"mean_air_segments": segs["mean_air"], **ops}
-
-
-def pmc_traffic(kernel: str):
-    path = os.path.join(ROOT, "profiles", "pmc_summary.json")
-    try:
-        with open(path) as f:
-            d = json.load(f)
-        return d.get(kernel, {}).get("hbm_bytes_per_launch")
-    except (OSError, ValueError):
-        return None
+    ach = rays * ops["W"] / (kernel_ms * 1e-3) / 1e12
+    return {"W_lane_ops_per_ray": ops["W"], "achieved": ach,
+            "frac_of_peak": ach / PEAK_FP64_VALU_TOPS, "mean_air_segments": segs["mean_air"],
+            "note": "library-priced work model, not executed instructions"}
 
 
 def main():
@@ -112,51 +182,108 @@ def main():
     coll_dev = dev if backend == "nccl" else torch.device("cpu")
 
     from airiceraytracing_amd import AirIceSolver, make_grid
+    from airiceraytracing_amd import _lib
+    from airiceraytracing_amd.distributed import run_sharded_table, sharded_step_grid_step
     solver = AirIceSolver()
-    depth_cm = CFG2["depth_cm"] - 1000.0 * rank  # rank r: antenna at 200 + 10 r m
-    grid = make_grid(depth_cm, CFG2["ice_cm"], CFG2["height_step"], CFG2["start_angle"],
-                     CFG2["stop_angle"], CFG2["angle_step"])
-    n = grid.n_rays
-    table = torch.empty((11, n), dtype=torch.float32, device=dev)
+    pmc = load_pmc()
     stream = torch.cuda.current_stream()
+    sharded = world > 1 and args.mode == "sharded"
 
     def barrier():
         if distributed:
             dist.barrier()
 
-    def step():
-        solver.table_device(grid, table, None, stream=stream)
-
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize()
-    barrier()
-    torch.cuda.synchronize()
-    # HIP events on the launch stream around the K steps: the GPU time per step (kernel plus the
-    # in-stream gap to the next launch); no event packets between the launches themselves
+    # ---------------------------------------------------------------- headline: table steps
+    if sharded:
+        depth_cm = CFG2["depth_cm"]
+        grid = make_grid(depth_cm, CFG2["ice_cm"],
+                         sharded_step_grid_step(CFG2["height_step"], world), CFG2["start_angle"],
+                         CFG2["stop_angle"], CFG2["angle_step"])
+    else:
+        depth_cm = CFG2["depth_cm"] - 1000.0 * rank  # replicas: rank r's antenna at 200 + 10 r m
+        grid = make_grid(depth_cm, CFG2["ice_cm"], CFG2["height_step"], CFG2["start_angle"],
+                         CFG2["stop_angle"], CFG2["angle_step"])
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    t0 = time.perf_counter()
-    ev0.record(stream)
-    for i in range(args.steps):
-        step()
-    ev1.record(stream)
-    torch.cuda.synchronize()
-    # the clock stops when this rank's K steps are done; the trailing barrier (an RCCL
-    # all-reduce, ~0.1-0.3 ms) closes the bracket but is not step work -- the max over ranks
-    # below covers rank skew.  Both figures are reported.
-    elapsed = time.perf_counter() - t0
-    barrier()
-    torch.cuda.synchronize()
-    elapsed_bar = time.perf_counter() - t0
-    kern_ms = ev0.elapsed_time(ev1) / args.steps
-    el = torch.tensor([elapsed, elapsed_bar], dtype=torch.float64, device=coll_dev)
-    if distributed:
-        dist.all_reduce(el, op=dist.ReduceOp.MAX)
-    elapsed, elapsed_bar = (float(x) for x in el.tolist())
-    total_rays = world * n * args.steps
-    value = total_rays / elapsed
+    shard_rep = None
+    if sharded:
+        def compute(begin, count, slab):
+            solver.table_device(grid, slab, None, row_begin=begin, row_count=count,
+                                ld=slab.shape[1], stream=stream)
 
-    # minimizer line item (cfg3: 1e6 random queries, ice 3000 m)
+        # the kernel time comes from a HIP-event pair around the K launches on the launch
+        # stream, recorded inside compute's stream order
+        state = {"i": 0}
+
+        def timed_compute(begin, count, slab):
+            if state["i"] == args.warmup:
+                ev0.record(stream)
+            compute(begin, count, slab)
+            state["i"] += 1
+            if state["i"] == args.warmup + args.steps:
+                ev1.record(stream)
+
+        r = run_sharded_table(grid, timed_compute, args.steps, args.warmup, device=dev,
+                              coll_device=coll_dev, sync=torch.cuda.synchronize, gather_reps=3)
+        elapsed = elapsed_bar = r["elapsed_s"]
+        n_local = r["rays_this_rank"]
+        total_rays = grid.n_rays * args.steps
+        table = r["slab"][:, :n_local]
+        shard_rep = {
+            "grid": f"TxH 100000->3000 m @{grid.height_step:g} m x 92->180 deg @0.5 deg "
+                    f"({grid.height_steps} rows x {grid.angle_steps} = {grid.n_rays} rays)",
+            "rows_per_rank": r["rows_per_rank"],
+            "gather_ms": r["gather_s"] * 1e3,
+            "gather_bytes_to_root": r["bytes_to_root"],
+            "gather_GBps_root_ingress": r["bytes_to_root"] / r["gather_s"] / 1e9
+            if r["gather_s"] > 0 else None,
+            "value_incl_gather": grid.n_rays / (elapsed / args.steps + r["gather_s"]),
+            "collective": "torch.distributed.gather (backend %s) of the row slabs to rank 0"
+                          % backend}
+        if rank == 0:
+            # the assembled table equals the whole grid built on one GPU, bit for bit
+            full = torch.empty((11, grid.n_rays), dtype=torch.float32, device=dev)
+            solver.table_device(grid, full, None, stream=stream)
+            torch.cuda.synchronize()
+            shard_rep["assembled_bitwise_equal_single_gpu"] = bool(
+                torch.equal(r["assembled"].to(dev).view(torch.int32), full.view(torch.int32)))
+            del full
+        del r
+    else:
+        n_local = grid.n_rays
+        table = torch.empty((11, n_local), dtype=torch.float32, device=dev)
+
+        def step():
+            solver.table_device(grid, table, None, stream=stream)
+
+        for _ in range(args.warmup):
+            step()
+        torch.cuda.synchronize()
+        barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        ev0.record(stream)
+        for _ in range(args.steps):
+            step()
+        ev1.record(stream)
+        torch.cuda.synchronize()
+        # the clock stops when this rank's K steps are done; the trailing barrier (an RCCL
+        # all-reduce, ~0.1-0.3 ms) closes the bracket but is not step work -- the max over ranks
+        # below covers rank skew.  Both figures are reported.
+        elapsed = time.perf_counter() - t0
+        barrier()
+        torch.cuda.synchronize()
+        elapsed_bar = time.perf_counter() - t0
+        el = torch.tensor([elapsed, elapsed_bar], dtype=torch.float64, device=coll_dev)
+        if distributed:
+            dist.all_reduce(el, op=dist.ReduceOp.MAX)
+        elapsed, elapsed_bar = (float(x) for x in el.tolist())
+        total_rays = world * n_local * args.steps
+    torch.cuda.synchronize()
+    kern_ms = ev0.elapsed_time(ev1) / args.steps
+    value = total_rays / elapsed
+    extra = {}
+
+    # ---------------------------------------------------------------- minimizer (cfg3)
     solve = None
     if not args.no_solve:
         from tests.parity import cfg3_queries
@@ -164,7 +291,11 @@ def main():
         tq = [torch.from_numpy(a).to(dev) for a in (txh, dst, dep)]
         out = torch.empty((17, args.solve_n), dtype=torch.float64, device=dev)
         stt = torch.empty(args.solve_n, dtype=torch.uint8, device=dev)
-        solver.solve_device(tq[0], tq[1], tq[2], 3000.0, out, stt, stream=stream)
+
+        def solve_call():
+            solver.solve_device(tq[0], tq[1], tq[2], 3000.0, out, stt, stream=stream)
+
+        solve_call()
         torch.cuda.synchronize()
         barrier()
         torch.cuda.synchronize()
@@ -172,35 +303,58 @@ def main():
         t1 = time.perf_counter()
         e0.record(stream)
         for _ in range(args.solve_steps):
-            solver.solve_device(tq[0], tq[1], tq[2], 3000.0, out, stt, stream=stream)
+            solve_call()
         e1.record(stream)
         torch.cuda.synchronize()
         se = torch.tensor([time.perf_counter() - t1], dtype=torch.float64, device=coll_dev)
         barrier()
         if distributed:
             dist.all_reduce(se, op=dist.ReduceOp.MAX)
+        call_ms = e0.elapsed_time(e1) / args.solve_steps
+        # per-kernel durations of the same calls: HIP-event pairs around each stage's launch on
+        # the launch stream (airice_kernel_timing), separate pass so the timed calls above carry
+        # no event packets between their kernels
+        _lib.kernel_time("roots_kernel"), _lib.kernel_time("out_kernel")
+        _lib.kernel_time("group_passes")
+        _lib.kernel_timing(True)
+        for _ in range(args.solve_steps):
+            solve_call()
+        torch.cuda.synchronize()
+        _lib.kernel_timing(False)
+        stage = {}
+        for k in ("roots_kernel", "group_passes", "out_kernel"):
+            ms, cnt = _lib.kernel_time(k)
+            stage[k + "_ms"] = ms / cnt if cnt else None
+        # CheckSolution (.cc:978-983) on the last batch, and the rows whose bracket set-up
+        # reads uninitialised GSL state in the reference (AIRICE_SOLVE 1|2|32)
+        thd = out[1].cpu().numpy()
+        st_h = stt.cpu().numpy()
+        err = np.abs(thd - dst)
+        solved = (((err / dst < 0.01) & (dst <= 100)) | ((err < 1) & (dst > 100))) & (thd >= 0)
         solve = {
             "metric": "Air2IceRayTracing solves/s (cfg3, 1e6 random queries per GPU)",
             "value": world * args.solve_n * args.solve_steps / float(se.item()),
             "unit": "solves/s",
-            "kernel_ms": e0.elapsed_time(e1) / args.solve_steps,
+            "ms_per_call": call_ms, "kernel_ms": call_ms, **stage,
+            "solved_fraction": float(solved.mean()),
+            "unpinned_fraction": float(((st_h & 35) != 0).mean()),
+            # dominant kernel: the root finder; algorithmic bytes per query = 24 B of inputs +
+            # 4 B perm read, 8 B root + 1 B status parked
+            "roofline": counter_roofline("roots_sorted_kernel", args.solve_n,
+                                         stage.get("roots_kernel_ms"), pmc, 37.0),
         }
-        # CheckSolution (.cc:978-983) on the last batch, and the rows whose bracket set-up
-        # reads uninitialised GSL state in the reference (AIRICE_SOLVE 1|2|32)
-        thd = out[1].cpu().numpy()
-        err = np.abs(thd - dst)
-        solved = (((err / dst < 0.01) & (dst <= 100)) | ((err < 1) & (dst > 100))) & (thd >= 0)
-        solve["solved_fraction"] = float(solved.mean())
-        solve["unpinned_fraction"] = float(((stt.cpu().numpy() & 35) != 0).mean())
+        out_h = out.cpu().numpy()
 
-    extra = {}
+    # ---------------------------------------------------------------- pythonwrapper (cfg5)
+    trace_h = None
     if not args.no_trace:
         # BASELINE cfg5: the pythonwrapper Py_TraceIceToAir rows (TraceIceToAir.C:5-73) for 1e7
         # queries through the batch entry (airice_trace_ice_to_air_launch), inputs in HBM
         from tests.parity import cfg5_queries
         from airiceraytracing_amd import VARIANT_PYWRAPPER
         psolver = AirIceSolver(variant=VARIANT_PYWRAPPER)
-        q = [torch.from_numpy(a).to(dev) for a in cfg5_queries(args.trace_n, seed=777 + rank)]
+        q5 = cfg5_queries(args.trace_n, seed=777 + rank)
+        q = [torch.from_numpy(a).to(dev) for a in q5]
         tout = torch.empty((args.trace_n, 10), dtype=torch.float64, device=dev)
         psolver.trace_ice_to_air_device(*q, tout, stream=stream)
         torch.cuda.synchronize()
@@ -216,43 +370,28 @@ def main():
             "metric": "Py_TraceIceToAir rows/s (cfg5, batch entry, 1e7 queries per GPU)",
             "value": args.trace_n / (tms * 1e-3), "unit": "queries/s", "ms": tms,
             "solved_fraction": float((tout[:, 0] != -1000).double().mean().item())}
+        idx5 = np.arange(0, args.trace_n, args.parity_stride)
+        trace_h = (q5, idx5, tout[torch.from_numpy(idx5).to(dev)].cpu().numpy())
         del q, tout
-        # the scalar ctypes symbol itself (one query per call, host arrays, as the reference's
-        # TraceIceToAir.py calls it) on a subsample of the same queries
-        import ctypes
-        from airiceraytracing_amd import lib
-        d5 = cfg5_queries(2000, seed=777 + rank)
-        arr = (ctypes.c_double * 10)()
-        # Py_TraceIceToAir reads ./Atmosphere.dat, else $AIRICE_ATMOSPHERE (plain text)
-        import gzip
-        import tempfile
-        atm = os.path.join(tempfile.gettempdir(), f"airice_bench_atm_{os.getpid()}.dat")
-        with gzip.open(os.path.join(ROOT, "airiceraytracing_amd", "data",
-                                    "Atmosphere.dat.gz")) as fz, open(atm, "wb") as fo:
-            fo.write(fz.read())
-        os.environ.setdefault("AIRICE_ATMOSPHERE", atm)
-        lib().Py_TraceIceToAir(float(d5[0][0]), float(d5[1][0]), float(d5[2][0]),
-                               float(d5[3][0]), arr)  # first call parses the atmosphere
-        c0 = time.perf_counter()
-        for i in range(2000):
-            lib().Py_TraceIceToAir(float(d5[0][i]), float(d5[1][i]), float(d5[2][i]),
-                                   float(d5[3][i]), arr)
-        cus = (time.perf_counter() - c0) / 2000 * 1e6
-        os.remove(atm)
-        extra["pywrapper_trace"]["scalar_call_us"] = cus
-        extra["pywrapper_trace"]["scalar_sample"] = "2000 Py_TraceIceToAir ctypes calls"
     if not args.no_lookup:
         # batched GetHorizontalDistanceToIntersectionPoint_Table on this step's table (HBM
         # resident), cfg3-distributed queries (cm) for the table's own antenna
         from tests.parity import cfg3_queries
-        txh, dst, _ = cfg3_queries(args.lookup_n, seed=4242 + rank)
-        src = torch.from_numpy(txh * 100).to(dev)
-        dcm = torch.from_numpy(dst * 100).to(dev)
-        dep = torch.full((args.lookup_n,), depth_cm, dtype=torch.float64, device=dev)
+        lgrid = grid
+        ltable = table
+        if sharded:  # the lookup runs on a whole table: rank 0's cfg2 table
+            lgrid = make_grid(CFG2["depth_cm"], CFG2["ice_cm"], CFG2["height_step"],
+                              CFG2["start_angle"], CFG2["stop_angle"], CFG2["angle_step"])
+            ltable = torch.empty((11, lgrid.n_rays), dtype=torch.float32, device=dev)
+            solver.table_device(lgrid, ltable, None, stream=stream)
+        lk_txh, lk_dst, _ = cfg3_queries(args.lookup_n, seed=4242 + rank)
+        src = torch.from_numpy(lk_txh * 100).to(dev)
+        dcm = torch.from_numpy(lk_dst * 100).to(dev)
+        ldep = torch.full((args.lookup_n,), depth_cm, dtype=torch.float64, device=dev)
         lout = torch.empty((9, args.lookup_n), dtype=torch.float64, device=dev)
         lok = torch.empty(args.lookup_n, dtype=torch.uint8, device=dev)
         lfl = torch.empty(args.lookup_n, dtype=torch.uint8, device=dev)
-        lt = solver.lookup_table(table, grid)
+        lt = solver.lookup_table(ltable, lgrid)
         # packed copy for the lookup (airice_lookup_pack, once per table; timed separately)
         solver.lookup_pack(lt, stream=stream)
         torch.cuda.synchronize()
@@ -265,7 +404,7 @@ def main():
         pack_ms = e0.elapsed_time(e1) / 10
 
         def lookup():
-            solver.table_lookup_device(lt, src, dcm, dep, CFG2["ice_cm"], lout, lok, lfl,
+            solver.table_lookup_device(lt, src, dcm, ldep, CFG2["ice_cm"], lout, lok, lfl,
                                        stream=stream)
 
         lookup()
@@ -278,12 +417,21 @@ def main():
         e1.record(stream)
         torch.cuda.synchronize()
         lms = e0.elapsed_time(e1) / reps
+        _lib.kernel_time("lookup_kernel")
+        _lib.kernel_timing(True)
+        lookup()
+        torch.cuda.synchronize()
+        _lib.kernel_timing(False)
+        lk_ms, lk_n = _lib.kernel_time("lookup_kernel")
         extra["table_lookup"] = {
             "metric": "GetHorizontalDistanceToIntersectionPoint_Table lookups/s (1e6 cfg3 "
                       "queries on the cfg2 table, incl. the minimizer fallback pass)",
             "value": args.lookup_n / (lms * 1e-3), "unit": "lookups/s", "ms": lms,
+            "lookup_kernel_ms": lk_ms / lk_n if lk_n else None,
             "ok_fraction": float(lok.cpu().numpy().mean()),
             "pack_ms": pack_ms, "packed": True}
+        if sharded:
+            del ltable
     if not args.no_multi:
         # Several antennas' cfg2 tables (MakeRayTracingTable per AntennaNumber, .cc:2019) built
         # concurrently, one HIP stream per antenna: a single table's launch ramp and drain
@@ -291,9 +439,9 @@ def main():
         # line item; the headline above stays one table per step on one stream.
         multi = {}
         for n_ant in (2, 4):
-            grids = [make_grid(depth_cm - 1000.0 * a, CFG2["ice_cm"], CFG2["height_step"],
-                               CFG2["start_angle"], CFG2["stop_angle"], CFG2["angle_step"])
-                     for a in range(n_ant)]
+            grids = [make_grid(CFG2["depth_cm"] - 1000.0 * a, CFG2["ice_cm"],
+                               CFG2["height_step"], CFG2["start_angle"], CFG2["stop_angle"],
+                               CFG2["angle_step"]) for a in range(n_ant)]
             tabs = [torch.empty((11, g.n_rays), dtype=torch.float32, device=dev) for g in grids]
             streams = [torch.cuda.Stream(device=dev) for _ in range(n_ant)]
             rays = sum(g.n_rays for g in grids)
@@ -316,18 +464,18 @@ def main():
         extra["multi_antenna_tables"] = {
             "metric": "cfg2 tables of several antennas on concurrent HIP streams (rays/s)",
             **multi}
-    if not args.no_pcie:
+    if not args.no_pcie and not sharded:
         # host-buffer callers (AllTableAllAntData is host memory): table build + D2H copy of the
         # 11 float columns into pinned memory, in stream order; never the headline value
-        host = torch.empty((11, n), dtype=torch.float32, pin_memory=True)
+        host = torch.empty((11, n_local), dtype=torch.float32, pin_memory=True)
         e0, e1, e2 = (torch.cuda.Event(enable_timing=True) for _ in range(3))
         reps = 10
-        step()
+        solver.table_device(grid, table, None, stream=stream)
         host.copy_(table, non_blocking=True)
         torch.cuda.synchronize()
         e0.record(stream)
         for _ in range(reps):
-            step()
+            solver.table_device(grid, table, None, stream=stream)
             host.copy_(table, non_blocking=True)
         e1.record(stream)
         for _ in range(reps):
@@ -338,8 +486,8 @@ def main():
         cms = e1.elapsed_time(e2) / reps
         extra["table_to_host"] = {
             "metric": "cfg2 table build + D2H copy to pinned host memory (PCIe-inclusive rays/s)",
-            "value": n / (pms * 1e-3), "unit": "rays/s", "ms": pms, "d2h_ms": cms,
-            "d2h_GBps": 44 * n / (cms * 1e-3) / 1e9}
+            "value": n_local / (pms * 1e-3), "unit": "rays/s", "ms": pms, "d2h_ms": cms,
+            "d2h_GBps": 44 * n_local / (cms * 1e-3) / 1e9}
         del host
     if args.default_grid:
         # the reference's default grid (10 m x 0.1 deg, 8,730,900 rays): throughput at a size
@@ -358,18 +506,21 @@ def main():
         extra["table_default_grid"] = {"rays": gd.n_rays, "ms": dms,
                                        "value": gd.n_rays / (dms * 1e-3), "unit": "rays/s"}
         del td
+    if rank == 0 and not args.no_scalar:
+        extra["scalar_latency_us"] = scalar_latencies(args)
 
-    # parity of this step's table vs the CPU path + CPU baseline (rank 0, N=1 only)
+    # ------------------------------------------- CPU legs: baselines + parity (rank 0, N=1)
     cpu = None
     parity_rep = None
     if rank == 0 and world == 1 and not args.no_cpu:
         import oracle
         from tests import parity
+        nthr = max(1, min(args.cpu_threads, len(os.sched_getaffinity(0))))
+        info = cpu_info(nthr)
         om = oracle.load_atmosphere(os.path.join(ROOT, "airiceraytracing_amd", "data",
                                                  "Atmosphere.dat.gz"))
         og = oracle.grid_init(depth_cm, CFG2["ice_cm"], CFG2["height_step"], CFG2["start_angle"],
                               CFG2["stop_angle"], CFG2["angle_step"])
-        nthr = max(1, min(args.cpu_threads, os.cpu_count() or 1))
         # bounded sample: whole cfg2 grids, repeated until >= cpu_seconds of wall time
         c0 = time.perf_counter()
         grids = 0
@@ -384,19 +535,21 @@ def main():
         c1 = time.perf_counter()
         passes = 0
         while True:
-            for r in rows1:
-                oracle.table_rows(om, og, r, r + 1)
+            for r_ in rows1:
+                oracle.table_rows(om, og, r_, r_ + 1)
             passes += 1
             c1dt = time.perf_counter() - c1
             if c1dt >= args.cpu_seconds / 4:
                 break
+        one = passes * len(rows1) * og.angle_steps / c1dt
         cpu = {"value": grids * og.height_steps * og.angle_steps / cdt, "unit": "rays/s",
                "cores": nthr, "kind": "port",
                "sample": f"{grids} x the full cfg2 grid ({og.height_steps * og.angle_steps} rays "
-                         f"each) in {cdt:.1f} s, oracle C restatement, OpenMP {nthr} threads, "
-                         f"gcc -O2; 1-thread {passes * len(rows1) * og.angle_steps / c1dt:.3e} "
-                         f"rays/s ({passes} x {len(rows1)} strided rows in {c1dt:.1f} s)",
-               "seconds": cdt}
+                         f"each) in {cdt:.1f} s, oracle C restatement (faithful call structure), "
+                         f"OpenMP {nthr} threads",
+               "one_thread_value": one, "seconds": cdt, **info,
+               "survey_reference_probe": SURVEY_REFERENCE_PROBE["table_rays_per_s"],
+               "survey_reference_probe_source": SURVEY_REFERENCE_PROBE["source"]}
         gt = table.cpu().numpy()
         ulps = parity.float_ulp_diff(gt, ot)
         finite = np.isfinite(ot) & np.isfinite(gt)
@@ -405,21 +558,26 @@ def main():
                       "table_max_abs": float(np.max(np.abs(gt - ot)[finite])),
                       "table_max_rel": float(np.max(rel[finite])),
                       "nan_pattern_equal": bool(np.array_equal(np.isnan(gt), np.isnan(ot)))}
+        if solve is not None:
+            solve["cpu_baseline"] = minimizer_cpu_baseline(args, om, txh, dst, dep, nthr, info)
+            solve["parity_vs_cpu"] = minimizer_parity(args, om, txh, dst, dep, out_h, st_h, nthr)
+        if trace_h is not None:
+            extra["pywrapper_trace"]["parity_vs_cpu"] = trace_parity(trace_h, nthr)
+        if isinstance(extra.get("scalar_latency_us"), dict):
+            extra["scalar_latency_us"]["cpu_oracle_per_call_us"] = scalar_cpu_per_call(om, og, ot)
 
-    weights = load_opweights()
-    W, work = table_work_per_ray(grid, weights)
-    achieved = n * W / (kern_ms * 1e-3) / 1e12
-    roof = {"bound": "valu",
-            "bound_note": "FP64 VALU: neither HBM (the 44 B/ray store is ~14 % of 8 TB/s) nor MFMA "
-                          "applies -- per-lane transcendental chains, no contraction; peak = the "
-                          "MI355X FP64 vector rate (78.6 TFLOP/s with FMA as 2 = 39.3 T lane-ops/s)",
-            "kernel": "table_kernel", "achieved": achieved,
-            "peak": PEAK_FP64_VALU_TOPS, "unit": "TFLOP/s (FP64 VALU lane-ops/s x 1e-12)",
-            "frac": achieved / PEAK_FP64_VALU_TOPS, "traffic": pmc_traffic("table_kernel"),
-            "algorithmic_ops_per_ray": W, "rays_per_launch": n, "kernel_ms": kern_ms,
-            "hbm_bytes_per_launch_algorithmic": 44 * n}
+    roof = counter_roofline("table_kernel", n_local, kern_ms, pmc, 44.0)
+    roof["ocml_priced"] = ocml_priced(grid, n_local, kern_ms)
 
     if rank == 0:
+        if sharded:
+            par = f"rows-sharded+gather (dp{world}: TxH-row slabs, one RCCL gather to rank 0)"
+            workload = ("MakeRayTracingTable cfg2 grid refined %dx in TxH (step %g m), one "
+                        "table sharded by TxH rows over %d GPUs" % (world, grid.height_step, world))
+        else:
+            par = f"replicas{world} (one antenna table per GPU)" if world > 1 else "single GPU"
+            workload = ("MakeRayTracingTable cfg2: TxH 100000->3000 m @20 m x 92->180 deg @0.5 "
+                        "deg, antenna 200 m below 3000 m ice")
         line = {
             "metric": "solved air->ice rays/sec (MakeRayTracingTable rays)",
             "value": value,
@@ -434,21 +592,137 @@ def main():
             "vs_baseline": None,
             "dtype": "f64",
             "data": "synthetic (BASELINE cfg2 grid) over the reference GDAS Atmosphere.dat",
-            "config": {"workload": "MakeRayTracingTable cfg2: TxH 100000->3000 m @20 m x "
-                                   "92->180 deg @0.5 deg, antenna 200 m below 3000 m ice",
-                       "rays_per_gpu_step": n, "table_columns": 11, "store": "f32",
-                       "parallelism": f"replicas{world} (one antenna table per GPU)"},
+            "config": {"workload": workload, "rays_per_gpu_step": n_local, "table_columns": 11,
+                       "store": "f32", "parallelism": par},
             "roofline": roof,
             "cpu_baseline": cpu,
             "parity_vs_cpu": parity_rep,
+            "sharded": shard_rep,
             "minimizer": solve,
             **extra,
-            "work_model": work,
         }
         sys.stdout.flush()
         os.write(json_fd, (json.dumps(line) + "\n").encode())
     if distributed:
         dist.destroy_process_group()
+
+
+def minimizer_cpu_baseline(args, om, txh, dst, dep, nthr, info) -> dict:
+    """The oracle's Air2IceRayTracing (faithful GSL-bisection restatement) over the head of the
+    same cfg3 batch, OpenMP on nthr host threads, until ~cpu_seconds; plus a 1-thread sample."""
+    import oracle
+    n = len(txh)
+    m = min(n, 20000)
+    t0 = time.perf_counter()
+    oracle.solve_batch(om, txh[:m], dst[:m], dep[:m], 3000.0, nthreads=nthr)
+    rate = m / max(time.perf_counter() - t0, 1e-9)
+    m = int(min(n, max(m, rate * args.cpu_seconds)))
+    done = 0
+    t0 = time.perf_counter()
+    while True:
+        oracle.solve_batch(om, txh[:m], dst[:m], dep[:m], 3000.0, nthreads=nthr)
+        done += m
+        dt = time.perf_counter() - t0
+        if dt >= args.cpu_seconds / 2:
+            break
+    m1 = 2000
+    t1 = time.perf_counter()
+    oracle.solve_batch(om, txh[:m1], dst[:m1], dep[:m1], 3000.0, nthreads=1)
+    one = m1 / (time.perf_counter() - t1)
+    return {"value": done / dt, "unit": "solves/s", "cores": nthr, "kind": "port",
+            "sample": f"{done} cfg3 queries (the head of the timed batch) in {dt:.1f} s, oracle "
+                      f"GSL-bisection restatement, OpenMP {nthr} threads; 1-thread on {m1}",
+            "one_thread_value": one, **info,
+            "survey_reference_probe": SURVEY_REFERENCE_PROBE["minimizer_solves_per_s"]}
+
+
+def minimizer_parity(args, om, txh, dst, dep, out_h, st_h, nthr) -> dict:
+    """Every k-th query of the timed 1e6 batch against the oracle: per-column relative error
+    (tests/parity.py rule), NaN positions, status bits on the pinned rows."""
+    import oracle
+    from tests import parity
+    idx = np.arange(0, len(txh), args.parity_stride)
+    ref, rst = oracle.solve_batch(om, txh[idx], dst[idx], dep[idx], 3000.0, nthreads=nthr)
+    pinned = (rst & oracle.SOLVE_UNPINNED) == 0
+    rep = parity.compare_columns(out_h[:, idx], ref, parity.SOLVE_FLOORS, mask=pinned)
+    return {"sample": f"every {args.parity_stride}th query of the timed batch ({idx.size})",
+            "max_rel": rep["max_rel"], "max_abs": rep["max_abs"], "n_bad": rep["n_bad"],
+            "nan_mask_equal": rep["nan_mismatch"] == 0 and rep["inf_mismatch"] == 0,
+            "status_bits_equal": bool(np.array_equal(st_h[idx][pinned] & 0x1F,
+                                                     rst[pinned] & 0x1F)),
+            "masked_unpinned": int((~pinned).sum()), "ok": rep["ok"]}
+
+
+def trace_parity(trace_h, nthr) -> dict:
+    import oracle
+    from tests import parity
+    (depth, ice, txh, dist_), idx, got = trace_h
+    om = oracle.load_atmosphere(os.path.join(ROOT, "airiceraytracing_amd", "data",
+                                             "Atmosphere.dat.gz"), pi=oracle.PI_EXACT)
+    ref = oracle.py_trace_batch(om, depth[idx], ice[idx], txh[idx], dist_[idx], nthreads=nthr)
+    rep = parity.compare_columns(got.T, ref.T, parity.TRACE_FLOORS)
+    return {"sample": f"every {idx[1] - idx[0] if idx.size > 1 else 1}th query of the timed "
+                      f"1e7 batch ({idx.size})",
+            "max_rel": rep["max_rel"], "max_abs": rep["max_abs"], "n_bad": rep["n_bad"],
+            "nan_mask_equal": rep["nan_mismatch"] == 0 and rep["inf_mismatch"] == 0,
+            "solved_mask_equal": bool(np.array_equal(got[:, 0] != -1000, ref[:, 0] != -1000)),
+            "ok": rep["ok"]}
+
+
+def scalar_cpu_per_call(om, og, ot) -> dict:
+    """The same scalar operations on the CPU oracle, one thread, per call (batch time / n):
+    the comparison the scalar drop-in latencies are held against."""
+    import oracle
+    from tests.parity import cfg3_queries
+    n = 400
+    txh, dst, dep = cfg3_queries(n, seed=31337)
+    res = {}
+    t0 = time.perf_counter()
+    oracle.solve_batch(om, txh, dst, dep, 3000.0, nthreads=1)
+    res["Air2IceRayTracing"] = (time.perf_counter() - t0) / n * 1e6
+    t0 = time.perf_counter()
+    for i in range(n):
+        oracle.hdtip(om, txh[i] * 100, dst[i] * 100, -20000.0, 300000.0)
+    res["GetHorizontalDistanceToIntersectionPoint"] = (time.perf_counter() - t0) / n * 1e6
+    lt = oracle.lookup_table(ot, og)
+    src, dcm = txh * 100, dst * 100
+    t0 = time.perf_counter()
+    oracle.table_lookup_batch(om, lt, src, dcm, np.full(n, -20000.0), 300000.0, nthreads=1)
+    res["GetHorizontalDistanceToIntersectionPoint_Table"] = (time.perf_counter() - t0) / n * 1e6
+    t0 = time.perf_counter()
+    rows = 8
+    oracle.table_rows(om, og, 0, rows)
+    res["GetRayTracingSolutions"] = (time.perf_counter() - t0) / (rows * og.angle_steps) * 1e6
+    omp = oracle.load_atmosphere(os.path.join(ROOT, "airiceraytracing_amd", "data",
+                                              "Atmosphere.dat.gz"), pi=oracle.PI_EXACT)
+    t0 = time.perf_counter()
+    oracle.py_trace_batch(omp, dep, np.full(n, 3000.0), np.minimum(txh, 20000.0), dst * 0.6,
+                          nthreads=1)
+    res["Py_TraceIceToAir"] = (time.perf_counter() - t0) / n * 1e6
+    res["note"] = ("oracle restatement, 1 thread, same query distribution; Python loop overhead "
+                   "included only for GetHorizontalDistanceToIntersectionPoint")
+    return res
+
+
+def scalar_latencies(args) -> dict | None:
+    """Per-call latency of the scalar drop-in entry points (one query per call, host arguments,
+    as CoREAS and TraceIceToAir.py call them), measured by tests/cpp/latency_driver (C++, linked
+    against libairice.so) in a child process."""
+    import subprocess
+    exe = os.path.join(ROOT, "tests", "cpp", "latency_driver")
+    if not os.path.exists(exe):
+        return None
+    import gzip
+    import tempfile
+    with tempfile.TemporaryDirectory() as td:
+        with gzip.open(os.path.join(ROOT, "airiceraytracing_amd", "data",
+                                    "Atmosphere.dat.gz")) as fz, \
+                open(os.path.join(td, "Atmosphere.dat"), "wb") as fo:
+            fo.write(fz.read())
+        r = subprocess.run([exe], cwd=td, capture_output=True, text=True, timeout=300)
+    if r.returncode != 0:
+        return {"error": r.stderr[-500:]}
+    return json.loads(r.stdout.strip().splitlines()[-1])
 
 
 if __name__ == "__main__":

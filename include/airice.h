@@ -278,6 +278,15 @@ int airice_memcpy_h2d(void *dst, const void *src, size_t bytes);
 int airice_memcpy_d2h(void *dst, const void *src, size_t bytes);
 int airice_synchronize(void);
 
+/* Kernel timing (bench.py's roofline legs; no reference counterpart).  When on, each launch
+ * of a timed kernel is bracketed by a hipEvent pair on its own stream.  Names:
+ * "table_kernel", "roots_kernel" (roots_kernel / roots_sorted_kernel, the minimizer's root
+ * finder), "group_passes" (the batch-wide grouping passes), "out_kernel" (solve_out /
+ * hdtip_out / trace_out), "lookup_kernel".  airice_kernel_time waits for the recorded pairs
+ * and returns their summed duration and count; reset != 0 clears them. */
+int airice_kernel_timing(int on);
+int airice_kernel_time(const char *name, double *total_ms, int64_t *launches, int reset);
+
 #ifdef __cplusplus
 }
 #endif

@@ -82,3 +82,57 @@ def test_gloo_world2_sharded_equals_single_process():
     txh, dst, dep = cfg3_queries(301, seed=99)
     refq, _ = oracle.solve_batch(m, txh, dst, dep, 3000.0)
     np.testing.assert_array_equal(sol, refq)
+
+
+def _bench_sharded_worker(rank, world, port, q):
+    """bench.py --mode sharded logic (run_sharded_table) with the oracle as the slab compute."""
+    import oracle
+    from airiceraytracing_amd.distributed import run_sharded_table, sharded_step_grid_step
+    from tests.conftest import ATMOSPHERE_GZ
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    m = oracle.load_atmosphere(ATMOSPHERE_GZ)
+    # bench's weak-scaling grid, coarsened for the CPU: base step 1000 m refined world-fold
+    g = oracle.grid_init(-20000.0, 300000.0, sharded_step_grid_step(1000.0, world), 92.0, 180.0,
+                         4.0)
+    calls = []
+
+    def compute(begin, count, slab):
+        calls.append((begin, count))
+        t = oracle.table_rows(m, g, begin, begin + count)
+        slab[:, :t.shape[1]] = torch.from_numpy(t)
+
+    r = run_sharded_table(g, compute, steps=2, warmup=1, gather_reps=2)
+    if rank == 0:
+        q.put((r["assembled"].numpy(), r["rows_per_rank"], r["bytes_to_root"], len(calls),
+               r["gather_s"] >= 0))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_gloo_bench_sharded_mode_assembles_table_bitwise(world):
+    import oracle
+    from airiceraytracing_amd.distributed import sharded_step_grid_step
+    from tests.conftest import ATMOSPHERE_GZ
+    ctx = mp.get_context("spawn")
+    q = ctx.SimpleQueue()
+    port = _free_port()
+    procs = [ctx.Process(target=_bench_sharded_worker, args=(r, world, port, q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    table, per, nbytes, ncalls, gathered = q.get()
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    m = oracle.load_atmosphere(ATMOSPHERE_GZ)
+    g = oracle.grid_init(-20000.0, 300000.0, sharded_step_grid_step(1000.0, world), 92.0, 180.0,
+                         4.0)
+    ref = oracle.table_rows(m, g, 0, g.height_steps)
+    assert table.shape == ref.shape
+    np.testing.assert_array_equal(table.view(np.int32), ref.view(np.int32))
+    assert per == -(-g.height_steps // world)
+    assert ncalls == 3 and gathered
+    # every rank but the root sends its rows: 11 float columns per ray
+    assert nbytes == (g.height_steps - shard_rows(g.height_steps, world, 0)[1]) * g.angle_steps * 44

@@ -39,8 +39,15 @@ def main():
         if "::table_kernel<" in r["Name"]:
             check["rocprof_table_kernel_avg_ms"] = float(r["AverageNs"]) / 1e6
             check["rocprof_table_kernel_calls"] = int(r["Calls"])
+        if "::roots_sorted_kernel<0>" in r["Name"]:
+            check["rocprof_roots_sorted_kernel_avg_ms"] = float(r["AverageNs"]) / 1e6
+            check["rocprof_roots_sorted_kernel_calls"] = int(r["Calls"])
     check["bench_hip_event_kernel_ms"] = bench["roofline"]["kernel_ms"]
     check["ratio"] = check["rocprof_table_kernel_avg_ms"] / check["bench_hip_event_kernel_ms"]
+    mz = (bench.get("minimizer") or {}).get("roofline") or {}
+    if mz.get("kernel_ms") and "rocprof_roots_sorted_kernel_avg_ms" in check:
+        check["bench_hip_event_roots_kernel_ms"] = mz["kernel_ms"]
+        check["roots_ratio"] = check["rocprof_roots_sorted_kernel_avg_ms"] / mz["kernel_ms"]
     with open(os.path.join(DST, f"{rnd}_timing_check.json"), "w") as f:
         json.dump(check, f, indent=1)
     print(json.dumps(check, indent=1))

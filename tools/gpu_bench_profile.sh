@@ -11,6 +11,6 @@ cat $OUT/bench.json
 cd /tmp
 # --no-multi: the several-antenna item runs table_kernel on concurrent streams, which would skew
 # the per-launch table_kernel average that collect_profiles.py checks against the headline.
-timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run --output-format csv -- python $R/bench.py --no-cpu --no-multi > $OUT/prof_bench.json 2> $OUT/prof.err || { echo "rocprof failed rc=$?"; tail -20 $OUT/prof.err; exit 1; }
+timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run --output-format csv -- python $R/bench.py --no-cpu --no-multi --no-scalar > $OUT/prof_bench.json 2> $OUT/prof.err || { echo "rocprof failed rc=$?"; tail -20 $OUT/prof.err; exit 1; }
 timeout -k 10 120 rocprofv3 -L > $OUT/counters.txt 2>&1 || true
 find $OUT/prof -name "*stats*" | head
