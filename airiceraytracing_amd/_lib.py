@@ -78,11 +78,13 @@ class Grid(ctypes.Structure):
         ("depth_m", ctypes.c_double),
         ("ice_m", ctypes.c_double),
         ("in_ice", ctypes.c_int32),
+        ("table_rows", ctypes.c_int32),
     ]
 
     @property
     def n_rays(self) -> int:
-        return int(self.height_steps) * int(self.angle_steps)
+        """Entries of the table: table_rows x angle_steps (rows with Tx <= 0 are skipped)."""
+        return int(self.table_rows) * int(self.angle_steps)
 
 
 class LookupTable(ctypes.Structure):

@@ -2,6 +2,8 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <mutex>
+
 #include "airice.h"
 #include "airice_device.hpp"
 
@@ -54,6 +56,33 @@ int launch_trace(const DevMedium& M, const IceConsts& I, const double* depth, co
                  const double* txh, const double* dist, size_t n, double* out10, hipStream_t st);
 
 void set_error(const char* fmt, ...);
+
+// One-query calls of the scalar drop-ins (the C++ MultiRayAirIceRefraction:: / RayTracingFunctions::
+// functions, Py_TraceIceToAir, airice_rtf_eval): a pinned, device-mapped staging block per device
+// that the host fills with the inputs and the kernels read and write in place (no copies), and a
+// library-owned non-blocking stream; a call is its launches plus one stream synchronisation.
+// The slot of the current device (hipGetDevice) is created on first use and locked for the call.
+struct ScalarSlot {
+  double* h = nullptr;  // host view
+  double* d = nullptr;  // device view of the same memory
+  hipStream_t st = nullptr;
+};
+constexpr size_t kScalarSlotDoubles = 512;
+class ScalarCall {
+ public:
+  ScalarCall();  // on failure ok() is false and airice_last_error() says why
+  ~ScalarCall();
+  bool ok() const { return slot_ != nullptr; }
+  ScalarSlot& slot() { return *slot_; }
+  int sync();  // waits for the slot's stream; AIRICE_OK or AIRICE_EHIP
+ private:
+  ScalarSlot* slot_ = nullptr;
+  void* lock_ = nullptr;
+};
+// The table lookup's minimizer fallback for one query that lk_query flagged one-sided
+// (.cc:1418-1420), on the device through the scalar slot: out9 / *ok as the batch lookup.
+int lookup_fallback_one(const airice_medium* m, double src_cm, double dist_cm, double depth_cm,
+                        double ice_cm, bool good, int flags, double out9[9], bool* ok);
 
 // Kernel timing for the bench (airice_kernel_timing): when enabled, launches of the kernels
 // below are bracketed by a hipEvent pair on their stream.  Off by default: one relaxed load.

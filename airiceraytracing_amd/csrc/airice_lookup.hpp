@@ -1,0 +1,267 @@
+// airice_lookup.hpp -- the table lookup's per-query code (GetHorizontalDistanceToIntersectionPoint
+// _Table and its helpers, MultiRayAirIceRefraction.cc:992-1462), compiled for the device (the
+// batch lookup_kernel, airice_lookup.hip) AND the host (the scalar C++ _Table and the
+// FindClosest* / GetParValues exports, compat_multiray.cpp): same source, same float->double
+// arithmetic, same bits.  Reads the reference makes outside the table are bounded and flagged
+// AIRICE_LOOKUP_UNPINNED.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdint>
+
+#include "airice.h"
+
+namespace airice {
+
+struct LkTable {
+  const float* col[AIRICE_TABLE_COLUMNS];  // column c of entry i at col[c][i]
+  const float* e;                          // packed entries (airice_lookup_pack) or nullptr
+  long long n;
+  double stop_h, step_h;  // LoopStopHeight, HeightStepSize of the last table made
+  int hsteps, asteps;     // TotalHeightSteps, TotalAngleSteps
+};
+struct LkTxhBins {
+  long long s1, e1, s2, e2;
+  double c1, c2;
+};
+struct LkThdBins {
+  long long s, e;
+  double c;
+};
+
+// One table entry's 11 columns, from the packed copy when there is one (three 16-byte loads of
+// one 48-byte record) or else column by column.  Out-of-range entries: NaN, flagged, as lk_at.
+struct LkRec {
+  float c[AIRICE_LOOKUP_ENTRY_FLOATS];
+};
+
+__host__ __device__ __forceinline__ LkRec lk_rec(const LkTable& T, long long i, int& fl) {
+  LkRec r;
+  if (i < 0 || i >= T.n) {
+    fl |= AIRICE_LOOKUP_UNPINNED;
+#pragma unroll
+    for (int c = 0; c < AIRICE_LOOKUP_ENTRY_FLOATS; ++c) r.c[c] = __builtin_nanf("");
+    return r;
+  }
+  if (T.e != nullptr) {
+    const float4* p = reinterpret_cast<const float4*>(T.e + (long long)AIRICE_LOOKUP_ENTRY_FLOATS * i);
+    const float4 a = p[0], b = p[1], d = p[2];
+    r.c[0] = a.x, r.c[1] = a.y, r.c[2] = a.z, r.c[3] = a.w;
+    r.c[4] = b.x, r.c[5] = b.y, r.c[6] = b.z, r.c[7] = b.w;
+    r.c[8] = d.x, r.c[9] = d.y, r.c[10] = d.z, r.c[11] = d.w;
+    return r;
+  }
+#pragma unroll
+  for (int c = 0; c < 11; ++c) r.c[c] = T.col[c][i];
+  r.c[11] = 0.0f;
+  return r;
+}
+
+__host__ __device__ __forceinline__ double lk_at(const LkTable& T, int c, long long i, int& fl) {
+  if (i < 0 || i >= T.n) {
+    fl |= AIRICE_LOOKUP_UNPINNED;
+    return __builtin_nan("");
+  }
+  return (double)T.col[c][i];
+}
+
+// oneDLinearInterpolation (.cc:992-995)
+__host__ __device__ __forceinline__ double lk_interp(double x, double xa, double ya, double xb, double yb) {
+  return ya + (yb - ya) * ((x - xa) / (xb - xa));
+}
+
+// FindClosestAirTxHeight (.cc:1033-1126): the row of height P and the span of entries with a
+// usable THD (not NaN, not in (-inf, 0.01) except exactly 0), scanned inwards from both ends.
+__host__ __device__ __forceinline__ LkTxhBins lk_closest_txh(const LkTable& T, double P, int& fl) {
+  const long long step = (long long)floor((P - T.stop_h) / T.step_h);
+  const long long index = T.hsteps - step - 1;
+  const long long max_bin = index * T.asteps + T.asteps - 1;
+  const long long min_bin = index * T.asteps;
+  double val = -0.001;
+  long long start_bin = max_bin;
+  bool went = false;
+  while ((val != 0 && val < 0.01) || __builtin_isnan(val)) {
+    if (start_bin < 0) {  // the reference reads before the table
+      fl |= AIRICE_LOOKUP_UNPINNED;
+      break;
+    }
+    val = lk_at(T, 1, start_bin, fl);
+    --start_bin;
+    went = true;
+  }
+  if (went) ++start_bin;
+  val = -0.001;
+  long long end_bin = min_bin;
+  went = false;
+  while ((val != 0 && val < 0.01) || __builtin_isnan(val)) {
+    if (end_bin >= T.n) {  // ... or past its end
+      fl |= AIRICE_LOOKUP_UNPINNED;
+      break;
+    }
+    val = lk_at(T, 1, end_bin, fl);
+    ++end_bin;
+    went = true;
+  }
+  if (went) --end_bin;
+  LkTxhBins b;
+  b.s1 = end_bin;
+  b.e1 = start_bin;
+  b.c1 = fabs(lk_at(T, 0, index, fl) - P);  // sic (.cc:1076): row index used as an entry index
+  b.s2 = b.s1 - T.asteps;
+  b.e2 = b.e1 - T.asteps;
+  if (b.s2 < 0) b.s2 = b.s1 + T.asteps;
+  if (b.e2 < 0) b.e2 = b.e1 + T.asteps;
+  b.c2 = b.c1;  // ClosestVal2 (.cc:1123) is the same expression
+  return b;
+}
+
+// FindClosestTHD (.cc:1128-1169)
+__host__ __device__ __forceinline__ LkThdBins lk_closest_thd(const LkTable& T, double P, long long s, long long e,
+                                            int& fl) {
+#pragma unroll 1
+  for (int i = 0; i < 8; ++i) {
+    if (e - s >= 3) {
+      const long long mid = (s + e) / 2;
+      const double v = lk_at(T, 1, mid, fl);
+      if (v - P > 0) s = mid;
+      if (v - P < 0) e = mid;
+    }
+  }
+  double minimum = 100000000000.0;
+  long long index2 = 0;
+#pragma unroll 1
+  for (long long ip = s; ip < e + 1; ++ip) {
+    const double v = lk_at(T, 1, ip, fl);
+    const double minval = fabs(v - P);
+    if (minval < minimum && v > P) {
+      minimum = minval;
+    } else {
+      index2 = ip;
+      break;
+    }
+  }
+  const long long index1 = index2 - 1;
+  const double v2 = lk_at(T, 1, index2, fl);
+  const double v1 = lk_at(T, 1, index1, fl);
+  minimum = fabs(P - v2);
+  if (minimum > fabs(P - v1)) minimum = fabs(P - v1);
+  return LkThdBins{index1, index2, minimum};
+}
+
+// The 10 parameters of one table row at horizontal distance D (.cc:1199-1240 / 1250-1289).
+__host__ __device__ __forceinline__ void lk_row_params(const LkTable& T, double D, long long s, long long e,
+                                              double par[10], double* closest, int& fl) {
+  const double max_thd = lk_at(T, 1, s, fl);
+  if (D <= max_thd) {
+    const LkThdBins b = lk_closest_thd(T, D, s, e, fl);
+    *closest = b.c;
+    if (b.c != 0) {
+      const double x1 = lk_at(T, 1, b.s, fl), x2 = lk_at(T, 1, b.e, fl);
+      const LkRec rs = lk_rec(T, b.s, fl), re = lk_rec(T, b.e, fl);
+#pragma unroll
+      for (int ip = 0; ip < 10; ++ip)
+        par[ip] = lk_interp(D, x1, (double)rs.c[1 + ip], x2, (double)re.c[1 + ip]);
+    } else {
+      const LkRec r = lk_rec(T, b.s + 1, fl);
+#pragma unroll
+      for (int ip = 0; ip < 10; ++ip) par[ip] = (double)r.c[1 + ip];
+    }
+  } else {
+#pragma unroll
+    for (int ip = 0; ip < 10; ++ip) par[ip] = -1e9;
+  }
+}
+
+// GetParValues (.cc:1172-1302) for a Tx height inside the table's range
+__host__ __device__ __forceinline__ void lk_par_values(const LkTable& T, double H, double D, double* h1,
+                                       double par1[10], double* h2, double par2[10], int& fl) {
+  const double min_h = lk_at(T, 0, T.n - 1, fl);
+  const LkTxhBins b = lk_closest_txh(T, H, fl);
+  double c1 = 0;
+  *h1 = lk_at(T, 0, b.s1, fl);
+  lk_row_params(T, D, b.s1, b.e1, par1, &c1, fl);
+  *h2 = *h1;
+  if (b.c1 != 0 && H > min_h && b.s2 < T.n - 1) {
+    *h2 = lk_at(T, 0, b.s2, fl);
+    double c2 = 0;
+    lk_row_params(T, D, b.s2, b.e2, par2, &c2, fl);
+  } else {
+#pragma unroll
+    for (int ip = 0; ip < 10; ++ip) par2[ip] = par1[ip];
+  }
+}
+
+// GetHorizontalDistanceToIntersectionPoint_Table (.cc:1305-1462) for one query (metres): out9
+// in the reference's argument order, *good = CheckSolution.  Returns true when the query hits the
+// one-sided extrapolation case, whose outputs the minimizer fallback (.cc:1418-1420) rewrites.
+__host__ __device__ __forceinline__ bool lk_query(const LkTable& T, double H, double D, double d2r, double out[9],
+                                  bool* good_out, int& fl) {
+  const double max_h = lk_at(T, 0, 0, fl);
+  const double min_h = lk_at(T, 0, T.n - 1, fl);
+  double x1 = 0, x2 = 0, y1 = 0, y2 = 0;
+  double piv[10];
+  unsigned set = 0;
+#pragma unroll
+  for (int i = 0; i < 10; ++i) piv[i] = 0;
+  if (H <= max_h && H >= min_h && H > 0) {
+    double par1[10], par2[10];
+    lk_par_values(T, H, D, &x1, par1, &x2, par2, fl);
+    // interpolation in height (.cc:1376-1401); a parameter missing at both heights ends the
+    // loop writing its value into slot 9 (the reference sets ipar = 9 before the store)
+    bool done = false;
+#pragma unroll
+    for (int ip = 0; ip < 10; ++ip) {
+      if (!done) {
+        y1 = par1[ip];
+        y2 = par2[ip];
+        double v = 0;
+        const bool missing = (y1 == -1e9 || y2 == -1e9);
+        if (x1 != x2 && !missing) {
+          v = lk_interp(H, x1, y1, x2, y2);
+        } else if (x1 == x2 && y1 == y2) {
+          v = par1[ip];
+        }
+        if ((x1 == x2 || missing) && y2 == -1e9 && y1 == -1e9) {
+          piv[9] = v;
+          set |= 1u << 9;
+          done = true;
+        } else {
+          piv[ip] = v;
+          set |= 1u << ip;
+        }
+      }
+    }
+  }
+  if (set != 0x3ffu) fl |= AIRICE_LOOKUP_UNPINNED;
+  const double thd = piv[0];
+  const bool one_sided = (y1 == -1e9 && y2 != -1e9) || (y2 == -1e9 && y1 != -1e9);
+  bool good = true;
+  if (y2 == -1e9 && y1 == -1e9) good = false;
+  if (H > max_h) good = false;
+  if (H < min_h) good = false;
+  if (H < 0) good = false;
+  if ((fabs(thd - D) / D > 0.01 && D <= 100) || (fabs(thd - D) > 1 && D > 100)) good = false;
+  *good_out = good;
+  if (one_sided) {
+    // finished by the fallback pass: every output slot is rewritten there, and the checks
+    // above are completed with CheckSolBool and launchAngle < 0
+    fl |= AIRICE_LOOKUP_FALLBACK;
+    return true;
+  }
+  const double la = piv[3] * d2r;  // pi/180 (.cc:1410)
+  if (la < 0) good = false;
+  *good_out = good;
+  out[0] = good ? piv[1] * 100 : 0.0;  // opticalPathLengthInIce
+  out[1] = good ? piv[2] * 100 : 0.0;  // opticalPathLengthInAir
+  out[2] = piv[8] * 100;               // geometricalPathLengthInIce
+  out[3] = piv[7] * 100;               // geometricalPathLengthInAir
+  out[4] = good ? la : 0.0;            // launchAngle
+  out[5] = good ? piv[4] * 100 : 0.0;  // horizontalDistanceToIntersectionPoint
+  out[6] = piv[5];                     // transmissionCoefficientS
+  out[7] = piv[6];                     // transmissionCoefficientP
+  out[8] = piv[9] * d2r;               // RecievedAngleInIce
+  return false;
+}
+
+}  // namespace airice

@@ -399,6 +399,105 @@ __device__ void rtf_air2ice(const DevMedium& M, double AirTxHeight, double Horiz
   o[15] = nf;
 }
 
+// ---- MultiRayAirIceRefraction:: forms (MultiRayAirIceRefraction.cc:377-917): the same
+// expressions plus the geometric path, 5-wide outputs {THD, Recv deg, L, t, geo} ----------------
+
+// fpathD (.cc:434-447), the reference's expression
+__device__ double mr_fpathD(double x, double A, double B, double C, double L) {
+  return (log((A + B * exp(C * x)) *
+              (sqrt((A * A + 2 * A * B * exp(C * x) + B * B * exp(2 * C * x) - L * L) /
+                    ((A + B * exp(C * x)) * (A + B * exp(C * x)))) +
+               1)) -
+          (A * log(A * sqrt(A * A - L * L) *
+                       sqrt((A * A + 2 * A * B * exp(C * x) + B * B * exp(2 * C * x) - L * L) /
+                            ((A + B * exp(C * x)) * (A + B * exp(C * x)))) +
+                   B * sqrt(A * A - L * L) * exp(C * x) *
+                       sqrt((A * A + 2 * A * B * exp(C * x) + B * B * exp(2 * C * x) - L * L) /
+                            ((A + B * exp(C * x)) * (A + B * exp(C * x)))) +
+                   A * A + A * B * exp(C * x) - L * L)) /
+              sqrt(A * A - L * L) +
+          (A * C * x) / sqrt(A * A - L * L)) /
+         C;
+}
+
+// GetRayGeometricPath (.cc:494-513)
+__device__ double mr_geo_path(const DevMedium& M, double A, double Rx, double Tx, double L,
+                              int air) {
+  double g = mr_fpathD(Rx, A, rtf_B(M, Rx, air), -rtf_C(M, Rx, air), L) -
+             mr_fpathD(Tx, A, rtf_B(M, Tx, air), -rtf_C(M, Tx, air), L);
+  if (air) g *= -1;
+  return g;
+}
+
+// GetLayerHitPointPar (.cc:521-646): {x1, ReceiveAngle (deg), L, time, x1_Geo}
+__device__ void mr_hit_point(const DevMedium& M, double n_layer1, double Rx, double Tx,
+                             double IncidentAng, int air, double out[5]) {
+  rtf_hit_point(M, n_layer1, Rx, Tx, IncidentAng, air, out);
+  out[4] = mr_geo_path(M, air ? M.A_air : M.A_ice, Rx, Tx, out[2], air);
+}
+
+// GetAirPropagationPar (.cc:661-804): out[5*MaxLayers + 2], per layer {THD, Recv, L, t, geo},
+// the filled-layer count at [5*MaxLayers+1] ([5*MaxLayers] is never written by the reference;
+// 0 here)
+__device__ int mr_air_prop(const DevMedium& M, double LaunchAngleAir, double AirTxHeight,
+                           double IceLayerHeight, double* out) {
+  const int SkipLayersAbove = rtf_skip_above(M, AirTxHeight);
+  const int SkipLayersBelow = rtf_skip_below(M, IceLayerHeight);
+  const int top = M.ml - SkipLayersAbove - 1;
+  double StartAngle = 0, StartHeight = 0, Start_nh = 0, StopHeight = 0, L0 = 0;
+  int nf = 0;
+  for (int il = top; il > SkipLayersBelow - 1; il--) {
+    StartHeight = (il == top) ? AirTxHeight : M.atm[il + 1] - 0.00001;
+    Start_nh = rtf_nz_air(M, StartHeight);
+    StopHeight = (il == (SkipLayersBelow - 1) + 1) ? IceLayerHeight : M.atm[il];
+    if (il == top) {
+      StartAngle = 180 - LaunchAngleAir;
+      double hp[5];
+      mr_hit_point(M, Start_nh, StopHeight, StartHeight, StartAngle, 1, hp);
+      for (int j = 0; j < 5; j++) out[5 * nf + j] = hp[j];
+      L0 = hp[2];
+      StartAngle = hp[1];
+    } else {
+      const double nzStopHeight = rtf_nz_air(M, StopHeight);
+      const double RecAng = asin(L0 / nzStopHeight) * M.r2d;
+      out[5 * nf + 0] = rtf_optical_path(M, M.A_air, StopHeight, StartHeight, L0, 1);
+      out[5 * nf + 1] = RecAng;
+      out[5 * nf + 2] = L0;
+      out[5 * nf + 3] = rtf_prop_time(M, M.A_air, StopHeight, StartHeight, L0, 1);
+      out[5 * nf + 4] = mr_geo_path(M, M.A_air, StopHeight, StartHeight, L0, 1);
+      StartAngle = RecAng;
+    }
+    nf++;
+  }
+  out[5 * M.ml + 1] = nf;
+  return nf;
+}
+
+// GetIcePropagationPar (.cc:807-869), TransitionBoundary == 0 (.h:70)
+__device__ void mr_ice_prop(const DevMedium& M, double AntennaDepth, double Lvalue,
+                            double out[5]) {
+  rtf_ice_prop(M, AntennaDepth, Lvalue, out);
+  out[4] = mr_geo_path(M, M.A_ice, AntennaDepth, 0.0, Lvalue, 0);
+}
+
+// MinimizeforLaunchAngle (.cc:873-917)
+__device__ double mr_min_launch(const DevMedium& M, double x, double AirTxHeight,
+                                double IceLayerHeight, double AntennaDepth, double D) {
+  double air[5 * kMaxLayers + 2];
+  const int nf = mr_air_prop(M, x, AirTxHeight, IceLayerHeight, air);
+  double thd_air = 0;
+  for (int i = 0; i < nf; i++) thd_air += air[i * 5];
+  // no air layer: the reference reads air[-4] and an unset air[2] (UB), modelled as NaN
+  const double Lvalue = nf > 0 ? air[2] : __builtin_nan("");
+  double thd_ice = 0;
+  if (AntennaDepth != 0) {
+    double ice[5];
+    mr_ice_prop(M, AntennaDepth, Lvalue, ice);
+    thd_ice += ice[0];
+  }
+  return D - (thd_ice + thd_air);
+}
+
 struct RtfCall {
   int op, n_out;
   double a[8];
@@ -406,8 +505,8 @@ struct RtfCall {
 
 __global__ void rtf_kernel(DevMedium M, RtfCall c, double* __restrict__ out) {
   if (threadIdx.x != 0 || blockIdx.x != 0) return;
-  double r[AIRICE_RTF_AIR2ICE_FIELDS > 4 * kMaxLayers + 1 ? AIRICE_RTF_AIR2ICE_FIELDS
-                                                         : 4 * kMaxLayers + 1];
+  double r[AIRICE_RTF_AIR2ICE_FIELDS > 5 * kMaxLayers + 2 ? AIRICE_RTF_AIR2ICE_FIELDS
+                                                         : 5 * kMaxLayers + 2];
   for (int i = 0; i < (int)(sizeof(r) / sizeof(r[0])); i++) r[i] = 0;
   switch (c.op) {
     case AIRICE_RTF_HIT_POINT:
@@ -437,6 +536,24 @@ __global__ void rtf_kernel(DevMedium M, RtfCall c, double* __restrict__ out) {
     case AIRICE_RTF_AIR2ICE:
       rtf_air2ice(M, c.a[0], c.a[1], c.a[2], c.a[3], r);
       break;
+    case AIRICE_MR_FPATHD:  // (x, a, b, c, speedc, l): speedc unused by the formula
+      r[0] = mr_fpathD(c.a[0], c.a[1], c.a[2], c.a[3], c.a[5]);
+      break;
+    case AIRICE_MR_GEOMETRIC_PATH:
+      r[0] = mr_geo_path(M, c.a[0], c.a[1], c.a[2], c.a[3], (int)c.a[4]);
+      break;
+    case AIRICE_MR_HIT_POINT:
+      mr_hit_point(M, c.a[0], c.a[1], c.a[2], c.a[3], (int)c.a[4], r);
+      break;
+    case AIRICE_MR_AIR_PROPAGATION:
+      mr_air_prop(M, c.a[0], c.a[1], c.a[2], r);
+      break;
+    case AIRICE_MR_ICE_PROPAGATION:  // (IncidentAngleonIce, IceLayerHeight unused, .cc:807)
+      mr_ice_prop(M, c.a[2], c.a[3], r);
+      break;
+    case AIRICE_MR_MIN_LAUNCH:
+      r[0] = mr_min_launch(M, c.a[0], c.a[1], c.a[2], c.a[3], c.a[4]);
+      break;
     default:
       break;
   }
@@ -460,6 +577,15 @@ int rtf_outputs(int op, int max_layers) {
       return 1;
     case AIRICE_RTF_AIR2ICE:
       return AIRICE_RTF_AIR2ICE_FIELDS;
+    case AIRICE_MR_FPATHD:
+    case AIRICE_MR_GEOMETRIC_PATH:
+    case AIRICE_MR_MIN_LAUNCH:
+      return 1;
+    case AIRICE_MR_HIT_POINT:
+    case AIRICE_MR_ICE_PROPAGATION:
+      return 5;
+    case AIRICE_MR_AIR_PROPAGATION:
+      return 5 * max_layers + 2;
     default:
       return -1;
   }

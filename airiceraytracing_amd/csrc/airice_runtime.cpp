@@ -276,6 +276,90 @@ void ktimer_record(int id, bool begin, hipStream_t st) {
   }
 }
 
+// ---- scalar slots ------------------------------------------------------------------------
+namespace {
+struct SlotEntry {
+  std::mutex mu;
+  ScalarSlot slot;
+};
+std::mutex g_slots_mu;
+std::vector<SlotEntry*> g_slots;  // by device ordinal; never freed (process lifetime)
+}  // namespace
+
+ScalarCall::ScalarCall() {
+  int dev = 0;
+  hipError_t e = hipGetDevice(&dev);
+  if (e != hipSuccess || dev < 0) {
+    set_error("scalar call: hipGetDevice failed: %s", hipGetErrorString(e));
+    return;
+  }
+  SlotEntry* ent = nullptr;
+  {
+    std::lock_guard<std::mutex> g(g_slots_mu);
+    if (g_slots.size() <= (size_t)dev) g_slots.resize(dev + 1, nullptr);
+    if (g_slots[dev] == nullptr) g_slots[dev] = new SlotEntry();
+    ent = g_slots[dev];
+  }
+  auto* lk = new std::unique_lock<std::mutex>(ent->mu);
+  ScalarSlot& sl = ent->slot;
+  if (sl.h == nullptr) {
+    void* h = nullptr;
+    void* d = nullptr;
+    hipStream_t st = nullptr;
+    if ((e = hipHostMalloc(&h, sizeof(double) * kScalarSlotDoubles, hipHostMallocMapped)) !=
+            hipSuccess ||
+        (e = hipHostGetDevicePointer(&d, h, 0)) != hipSuccess ||
+        (e = hipStreamCreateWithFlags(&st, hipStreamNonBlocking)) != hipSuccess) {
+      set_error("scalar call: pinned staging set-up failed: %s", hipGetErrorString(e));
+      if (h != nullptr) (void)hipHostFree(h);
+      delete lk;
+      return;
+    }
+    sl.h = static_cast<double*>(h);
+    sl.d = static_cast<double*>(d);
+    sl.st = st;
+  }
+  slot_ = &sl;
+  lock_ = lk;
+}
+
+ScalarCall::~ScalarCall() { delete static_cast<std::unique_lock<std::mutex>*>(lock_); }
+
+int ScalarCall::sync() {
+  const hipError_t e = hipStreamSynchronize(slot_->st);
+  if (e != hipSuccess) {
+    set_error("scalar call: %s", hipGetErrorString(e));
+    return AIRICE_EHIP;
+  }
+  return AIRICE_OK;
+}
+
+int lookup_fallback_one(const airice_medium* m, double src_cm, double dist_cm, double depth_cm,
+                        double ice_cm, bool good, int flags, double out9[9], bool* ok) {
+  DevMedium M;
+  int rc = build_dev_medium(m, AIRICE_VARIANT_MULTIRAY, &M);
+  if (rc) return rc;
+  IceConsts I;
+  build_ice_consts(M, ice_cm / 100, 0.0, &I);  // as airice_table_lookup_launch
+  ScalarCall call;
+  if (!call.ok()) return AIRICE_EHIP;
+  ScalarSlot& sl = call.slot();
+  sl.h[0] = src_cm;
+  sl.h[1] = dist_cm;
+  sl.h[2] = depth_cm;
+  uint8_t* hb = reinterpret_cast<uint8_t*>(sl.h + 12);
+  hb[0] = good ? 1 : 0;
+  hb[1] = (uint8_t)flags;
+  uint8_t* db = reinterpret_cast<uint8_t*>(sl.d + 12);
+  rc = launch_lookup_fallback(M, I, sl.d, sl.d + 1, sl.d + 2, ice_cm, 1, sl.d + 3, 1, db, db + 1,
+                              sl.st);
+  if (rc == AIRICE_OK) rc = call.sync();
+  if (rc) return rc;
+  for (int c = 0; c < 9; ++c) out9[c] = sl.h[3 + c];
+  *ok = hb[0] != 0;
+  return AIRICE_OK;
+}
+
 }  // namespace airice
 
 using namespace airice;
@@ -315,6 +399,17 @@ extern "C" int airice_kernel_time(const char* name, double* total_ms, int64_t* l
   }
   return AIRICE_OK;
 }
+
+namespace {
+// Device buffer freed on every exit path of the *_host entry points.
+struct DevBuffer {
+  void* p = nullptr;
+  hipError_t alloc(size_t bytes) { return hipMalloc(&p, bytes); }
+  ~DevBuffer() {
+    if (p != nullptr) (void)hipFree(p);
+  }
+};
+}  // namespace
 
 #define HIP_TRY(expr)                                                          \
   do {                                                                         \
@@ -390,11 +485,11 @@ int airice_grid_init(airice_grid* g, double depth_cm, double ice_cm, double heig
     set_error("empty grid");
     return AIRICE_EINVAL;
   }
-  // The reference skips rows with AirTxHeight <= 0 (.cc:2082); such grids are rejected.
-  if (!(g->start_height - g->height_step * (g->height_steps - 1) > 0)) {
-    set_error("grid reaches non-positive Tx heights");
-    return AIRICE_EINVAL;
-  }
+  // The reference skips rows whose (unforced) AirTxHeight is not > 0 (.cc:2081-2082); heights
+  // fall with the row index, so the kept rows are a prefix
+  int32_t rows = g->height_steps;
+  while (rows > 0 && !(g->start_height - g->height_step * (rows - 1) > 0)) --rows;
+  g->table_rows = rows;
   return AIRICE_OK;
 }
 
@@ -437,6 +532,11 @@ static int table_prepare(const airice_medium* m, const airice_grid* g, int32_t r
   return AIRICE_OK;
 }
 
+// rows of [row_begin, row_begin+row_count) the table holds (the reference skips Tx <= 0, .cc:2082)
+static int32_t kept_rows(const airice_grid* g, int32_t row_begin, int32_t row_count) {
+  return std::max<int32_t>(0, std::min<int32_t>(row_count, g->table_rows - row_begin));
+}
+
 int airice_table_launch(const airice_medium* m, const airice_grid* g, int32_t row_begin,
                         int32_t row_count, float* d_table, double* d_full, size_t ld,
                         void* stream) {
@@ -448,7 +548,8 @@ int airice_table_launch(const airice_medium* m, const airice_grid* g, int32_t ro
     set_error("null table");
     return AIRICE_EINVAL;
   }
-  rc = launch_table(M, I, g, row_begin, row_count, d_table, d_full, ld, (hipStream_t)stream);
+  rc = launch_table(M, I, g, row_begin, kept_rows(g, row_begin, row_count), d_table, d_full, ld,
+                    (hipStream_t)stream);
   if (rc) set_error("table launch failed: %s", hipGetErrorString(hipGetLastError()));
   return rc;
 }
@@ -459,17 +560,20 @@ int airice_table_host(const airice_medium* m, const airice_grid* g, int32_t row_
   IceConsts I;
   int rc = table_prepare(m, g, row_begin, row_count, ld, &M, &I);
   if (rc) return rc;
-  float* dt = nullptr;
-  double* df = nullptr;
-  HIP_TRY(hipMalloc(&dt, sizeof(float) * 11 * ld));
-  if (h_full) HIP_TRY(hipMalloc(&df, sizeof(double) * 18 * ld));
-  rc = launch_table(M, I, g, row_begin, row_count, dt, df, ld, nullptr);
-  if (rc == AIRICE_OK) {
-    HIP_TRY(hipMemcpy(h_table, dt, sizeof(float) * 11 * ld, hipMemcpyDeviceToHost));
-    if (h_full) HIP_TRY(hipMemcpy(h_full, df, sizeof(double) * 18 * ld, hipMemcpyDeviceToHost));
+  DevBuffer dt, df;
+  HIP_TRY(dt.alloc(sizeof(float) * 11 * ld));
+  if (h_full) HIP_TRY(df.alloc(sizeof(double) * 18 * ld));
+  const int32_t rows = kept_rows(g, row_begin, row_count);
+  if (rows < row_count) {  // entries of skipped rows come back as NaN (0xFF bytes)
+    HIP_TRY(hipMemset(dt.p, 0xFF, sizeof(float) * 11 * ld));
+    if (h_full) HIP_TRY(hipMemset(df.p, 0xFF, sizeof(double) * 18 * ld));
   }
-  (void)hipFree(dt);
-  if (df) (void)hipFree(df);
+  rc = launch_table(M, I, g, row_begin, rows, static_cast<float*>(dt.p),
+                    static_cast<double*>(df.p), ld, nullptr);
+  if (rc == AIRICE_OK) {
+    HIP_TRY(hipMemcpy(h_table, dt.p, sizeof(float) * 11 * ld, hipMemcpyDeviceToHost));
+    if (h_full) HIP_TRY(hipMemcpy(h_full, df.p, sizeof(double) * 18 * ld, hipMemcpyDeviceToHost));
+  }
   return rc;
 }
 
@@ -518,31 +622,24 @@ int airice_solve_host(const airice_medium* m, int variant, double ice_h_m, const
     return AIRICE_EINVAL;
   }
   const int fields = variant == AIRICE_VARIANT_PYWRAPPER ? AIRICE_PYSOLVE_FIELDS : AIRICE_SOLVE_FIELDS;
-  double *dt = nullptr, *dd = nullptr, *dp = nullptr, *dthr = nullptr, *dout = nullptr;
-  uint8_t* dst = nullptr;
-  HIP_TRY(hipMalloc(&dt, sizeof(double) * n));
-  HIP_TRY(hipMalloc(&dd, sizeof(double) * n));
-  HIP_TRY(hipMalloc(&dp, sizeof(double) * n));
-  HIP_TRY(hipMalloc(&dout, sizeof(double) * fields * ld));
-  HIP_TRY(hipMalloc(&dst, n));
+  // one device block: txh | dist | depth | [straight angle] | out (fields x ld) | status
+  const size_t nin = straight_angle != nullptr ? 4 : 3;
+  DevBuffer buf;
+  HIP_TRY(buf.alloc(sizeof(double) * (nin * n + (size_t)fields * ld) + n));
+  double* dt = static_cast<double*>(buf.p);
+  double *dd = dt + n, *dp = dt + 2 * n, *dthr = straight_angle != nullptr ? dt + 3 * n : nullptr;
+  double* dout = dt + nin * n;
+  uint8_t* dst = reinterpret_cast<uint8_t*>(dout + (size_t)fields * ld);
   HIP_TRY(hipMemcpy(dt, txh, sizeof(double) * n, hipMemcpyHostToDevice));
   HIP_TRY(hipMemcpy(dd, dist, sizeof(double) * n, hipMemcpyHostToDevice));
   HIP_TRY(hipMemcpy(dp, depth, sizeof(double) * n, hipMemcpyHostToDevice));
-  if (straight_angle != nullptr) {
-    HIP_TRY(hipMalloc(&dthr, sizeof(double) * n));
+  if (dthr != nullptr)
     HIP_TRY(hipMemcpy(dthr, straight_angle, sizeof(double) * n, hipMemcpyHostToDevice));
-  }
   int rc = airice_solve_launch(m, variant, ice_h_m, dt, dd, dp, dthr, n, dout, ld, dst, nullptr);
   if (rc == AIRICE_OK) {
     HIP_TRY(hipMemcpy(out, dout, sizeof(double) * fields * ld, hipMemcpyDeviceToHost));
     if (status) HIP_TRY(hipMemcpy(status, dst, n, hipMemcpyDeviceToHost));
   }
-  (void)hipFree(dt);
-  (void)hipFree(dd);
-  (void)hipFree(dp);
-  (void)hipFree(dout);
-  (void)hipFree(dst);
-  if (dthr) (void)hipFree(dthr);
   return rc;
 }
 
@@ -652,15 +749,15 @@ int airice_rtf_eval(const airice_medium* m, int op, const double* args, size_t n
     set_error("rtf op %d: %zu outputs (need %d), %zu args (max 8)", op, n_out, need, n_args);
     return AIRICE_EINVAL;
   }
-  thread_local double* d = nullptr;  // per-thread result slot, kept for the next call
-  if (d == nullptr)
-    HIP_TRY(hipMalloc(&d, sizeof(double) * std::max(4 * kMaxLayers + 1, AIRICE_RTF_AIR2ICE_FIELDS)));
-  rc = airice::launch_rtf(M, op, args, n_args, d, nullptr);
+  ScalarCall call;  // the kernel writes its outputs straight into the pinned slot
+  if (!call.ok()) return AIRICE_EHIP;
+  rc = airice::launch_rtf(M, op, args, n_args, call.slot().d, call.slot().st);
   if (rc) {
     set_error("rtf launch failed: %s", hipGetErrorString(hipGetLastError()));
     return rc;
   }
-  HIP_TRY(hipMemcpy(out, d, sizeof(double) * need, hipMemcpyDeviceToHost));
+  if ((rc = call.sync())) return rc;
+  std::memcpy(out, call.slot().h, sizeof(double) * need);
   return AIRICE_OK;
 }
 
@@ -676,9 +773,10 @@ int airice_single_ray_host(const airice_medium* m, double antenna_depth_m, doubl
     set_error("single ray: %zu path samples exceed capacity %zu", n, cap);
     return AIRICE_EINVAL;
   }
-  double* d = nullptr;
+  DevBuffer buf;
   const size_t words = AIRICE_SINGLE_RAY_WORK + (path ? 2 * n : 0);
-  HIP_TRY(hipMalloc(&d, sizeof(double) * words));
+  HIP_TRY(buf.alloc(sizeof(double) * words));
+  double* d = static_cast<double*>(buf.p);
   double* dx = path ? d + AIRICE_SINGLE_RAY_WORK : nullptr;
   double* dz = path ? dx + n : nullptr;
   rc = airice_single_ray_launch(m, antenna_depth_m, launch_deg, txh_m, ice_m, d, dx, dz, n, nullptr);
@@ -692,7 +790,6 @@ int airice_single_ray_host(const airice_medium* m, double antenna_depth_m, doubl
       rc = AIRICE_EHIP;
     }
   }
-  (void)hipFree(d);
   return rc;
 }
 
@@ -710,8 +807,9 @@ int airice_trace_ice_to_air_launch(const airice_medium* m, const double* d_depth
 int airice_trace_ice_to_air_host(const airice_medium* m, const double* depth, const double* ice,
                                  const double* txh, const double* dist, size_t n, double* out10) {
   if (n == 0) return AIRICE_OK;
-  double* buf = nullptr;
-  HIP_TRY(hipMalloc(&buf, sizeof(double) * 14 * n));
+  DevBuffer mem;
+  HIP_TRY(mem.alloc(sizeof(double) * 14 * n));
+  double* buf = static_cast<double*>(mem.p);
   double *dd = buf, *di = buf + n, *dt = buf + 2 * n, *ds = buf + 3 * n, *dout = buf + 4 * n;
   HIP_TRY(hipMemcpy(dd, depth, sizeof(double) * n, hipMemcpyHostToDevice));
   HIP_TRY(hipMemcpy(di, ice, sizeof(double) * n, hipMemcpyHostToDevice));
@@ -719,17 +817,15 @@ int airice_trace_ice_to_air_host(const airice_medium* m, const double* depth, co
   HIP_TRY(hipMemcpy(ds, dist, sizeof(double) * n, hipMemcpyHostToDevice));
   int rc = airice_trace_ice_to_air_launch(m, dd, di, dt, ds, n, dout, nullptr);
   if (rc == AIRICE_OK) HIP_TRY(hipMemcpy(out10, dout, sizeof(double) * 10 * n, hipMemcpyDeviceToHost));
-  (void)hipFree(buf);
   return rc;
 }
 
 // Py_TraceIceToAir drop-in (TraceIceToAir.C:75-79).  The reference re-parses
 // "Atmosphere.dat" from the working directory on every call (TraceIceToAir.C:25);
-// here it is parsed once per process and kept with a small device scratch buffer.
+// here it is parsed once per process; each call runs in the current device's scalar slot.
 static std::mutex g_py_mu;
 static bool g_py_ready = false;
 static airice_medium g_py_medium;
-static double* g_py_dev = nullptr;
 
 void Py_TraceIceToAir(double AntennaDepth, double IceLayerHeight, double AirTxHeight,
                       double HorizontalDistance, double ArrayParameters[10]) {
@@ -745,20 +841,25 @@ void Py_TraceIceToAir(double AntennaDepth, double IceLayerHeight, double AirTxHe
         return;
       }
     }
-    if (hipMalloc(&g_py_dev, sizeof(double) * 14) != hipSuccess) {
-      std::fprintf(stderr, "Py_TraceIceToAir: hipMalloc failed\n");
-      return;
-    }
     g_py_ready = true;
   }
-  double in[4] = {AntennaDepth, IceLayerHeight, AirTxHeight, HorizontalDistance};
-  if (hipMemcpy(g_py_dev, in, sizeof(in), hipMemcpyHostToDevice) != hipSuccess) return;
-  if (airice_trace_ice_to_air_launch(&g_py_medium, g_py_dev, g_py_dev + 1, g_py_dev + 2,
-                                     g_py_dev + 3, 1, g_py_dev + 4, nullptr) != AIRICE_OK) {
+  ScalarCall call;
+  if (!call.ok()) {
     std::fprintf(stderr, "Py_TraceIceToAir: %s\n", airice_last_error());
     return;
   }
-  (void)hipMemcpy(ArrayParameters, g_py_dev + 4, sizeof(double) * 10, hipMemcpyDeviceToHost);
+  ScalarSlot& sl = call.slot();
+  sl.h[0] = AntennaDepth;
+  sl.h[1] = IceLayerHeight;
+  sl.h[2] = AirTxHeight;
+  sl.h[3] = HorizontalDistance;
+  if (airice_trace_ice_to_air_launch(&g_py_medium, sl.d, sl.d + 1, sl.d + 2, sl.d + 3, 1,
+                                     sl.d + 4, sl.st) != AIRICE_OK ||
+      call.sync() != AIRICE_OK) {
+    std::fprintf(stderr, "Py_TraceIceToAir: %s\n", airice_last_error());
+    return;
+  }
+  std::memcpy(ArrayParameters, sl.h + 4, sizeof(double) * 10);
 }
 
 int airice_device_count(int* count) {

@@ -1,16 +1,32 @@
 // compat_multiray.cpp -- MultiRayAirIceRefraction:: C++ surface over the C-ABI
-// (include/MultiRayAirIceRefraction.h).  Keeps the reference's globals and call semantics;
-// every ray / solve is computed by the gfx950 kernels.
+// (include/MultiRayAirIceRefraction.h).  Keeps the reference's globals and call semantics.
+// Ray quantities and solves run on the GPU: batches through the batch kernels, one-query calls
+// through the current device's pinned scalar slot (ScalarCall, airice_runtime.cpp: the kernels
+// read their inputs from and write their outputs to pinned host memory, one synchronisation per
+// call).  Table walks (_Table, GetParValues, FindClosest*) run the batch lookup kernel's own
+// code (airice_lookup.hpp) on the host against the caller's host columns.
 #include <hip/hip_runtime.h>
 
 #include <cmath>
+#include <cstdint>
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
+#include <initializer_list>
 #include <mutex>
 #include <vector>
 
 #include "MultiRayAirIceRefraction.h"
 #include "airice.h"
+#include "airice_internal.h"
+#include "airice_lookup.hpp"
+#include "compat_common.h"
+
+// The caller owns these (reference .h:23-24, RunMultiRayCode.C:3-4); only _Table reads them.
+// Weak references: a process that never defines them (a ctypes user of the C-ABI) still loads
+// the library, and _Table then skips the antenna remap.
+#pragma weak AntennaDepths
+#pragma weak AntennaTableAlreadyMade
 
 // ---- reference globals (.cc:3-21) --------------------------------------------------------
 double MaxAirTxHeight = 0;
@@ -25,41 +41,83 @@ double LoopStartHeight = 0;
 double LoopStopHeight = 0;
 int TotalHeightSteps = 0;
 
+// ---- namespace data (.h:33-84): one shared copy -------------------------------------------
+namespace MultiRayAirIceRefraction {
+std::vector<std::vector<double>> nh_data;
+std::vector<std::vector<double>> lognh_data;
+std::vector<std::vector<double>> h_data;
+std::vector<double> GridPositionH;
+std::vector<double> GridPositionTh;
+std::vector<double> GridZValue[10];
+double GridStartTh = 90.05;
+double GridStopTh = 179.95;
+double GridStepSizeH_O = 25;
+double GridStepSizeTh_O = 0.01;
+double GridWidthH = 1000;
+double GridWidthTh = GridStopTh - GridStartTh;
+int GridPoints = 100;
+int TotalStepsH_O = 100;
+int TotalStepsTh_O = 100;
+double GridStartH = 1000;
+double GridStopH = 100000;
+double ATMLAY[5];
+double abc[5][3];
+double C_air[5];
+double B_air[5];
+double A_ice = A_ice_def;
+double B_ice = B_ice_def;
+double C_ice = C_ice_def;
+int MaxLayers = 0;
+}  // namespace MultiRayAirIceRefraction
+
 namespace {
 
-std::mutex g_mu;
+namespace MR = MultiRayAirIceRefraction;
+
+std::mutex g_mu;  // the medium and the HBM table copies
 airice_medium g_medium;
 bool g_have_medium = false;
-double* g_scratch = nullptr;  // device scratch for scalar calls
-constexpr size_t kScratch = 64;
 
-void die(const char* what) {
+[[noreturn]] void die(const char* what) {
   std::fprintf(stderr, "MultiRayAirIceRefraction: %s failed: %s\n", what, airice_last_error());
   std::abort();  // the reference has no error channel here; fail loudly, never fall back
 }
 
-const airice_medium& medium() {
-  if (!g_have_medium) MultiRayAirIceRefraction::MakeAtmosphere();
-  return g_medium;
+std::string atmosphere_text() { return airice_compat::atmosphere_text("MultiRayAirIceRefraction"); }
+
+// The parsed medium with the namespace's current ice model (A_ice / B_ice / C_ice are mutable
+// namespace variables in the reference, read by Getnz_ice at every call).
+airice_medium medium() {
+  std::lock_guard<std::mutex> lock(g_mu);
+  if (!g_have_medium) {
+    const std::string text = atmosphere_text();
+    if (airice_atmosphere_parse(text.data(), text.size(), AIRICE_VARIANT_MULTIRAY, &g_medium) !=
+        AIRICE_OK)
+      die("MakeAtmosphere");
+    g_have_medium = true;
+  }
+  airice_medium m = g_medium;
+  m.A_ice = MR::A_ice;
+  m.B_ice = MR::B_ice;
+  m.C_ice = MR::C_ice;
+  return m;
 }
 
-double* scratch() {
-  if (g_scratch == nullptr && hipMalloc(&g_scratch, kScratch * sizeof(double)) != hipSuccess)
-    die("hipMalloc");
-  return g_scratch;
+// one GPU evaluation of a ray-layer quantity (AIRICE_RTF_* / AIRICE_MR_* op)
+void ray_op(int op, std::initializer_list<double> args, double* out, size_t n_out) {
+  const airice_medium m = medium();
+  const std::vector<double> a(args);
+  if (airice_rtf_eval(&m, op, a.data(), a.size(), out, n_out) != AIRICE_OK) die("ray layer");
 }
 
-// HBM copy of AllTableAllAntData[i]: adopted from MakeRayTracingTable, or uploaded when the
-// host table at that index is not the one last seen (a caller-filled or replaced table).
-struct DevTable {
-  const float* host0 = nullptr;  // AllTableAllAntData[i][0].data() when mirrored
-  size_t n = 0;
-  float* dev = nullptr;
-  float* packed = nullptr;  // airice_lookup_pack copy, made at the first lookup
-};
-std::vector<DevTable> g_tables;
+double ray_op1(int op, std::initializer_list<double> args) {
+  double r = 0;
+  ray_op(op, args, &r, 1);
+  return r;
+}
 
-const float* device_table(int index, size_t* n_out) {
+// ---- tables --------------------------------------------------------------------------------
+const std::vector<std::vector<float>>& host_table(int index) {
   if (index < 0 || index >= (int)AllTableAllAntData.size()) {
     std::fprintf(stderr, "MultiRayAirIceRefraction: no table %d (%zu made)\n", index,
                  AllTableAllAntData.size());
@@ -67,62 +125,142 @@ const float* device_table(int index, size_t* n_out) {
   }
   const std::vector<std::vector<float>>& cols = AllTableAllAntData[index];
   if (cols.size() < AIRICE_TABLE_COLUMNS || cols[0].empty()) die("table lookup (malformed table)");
+  for (int c = 1; c < AIRICE_TABLE_COLUMNS; ++c)
+    if (cols[c].size() != cols[0].size()) die("table lookup (ragged table)");
+  return cols;
+}
+
+// The lookup's view of a host table and the grid globals of the last table made (.cc:1035-1039)
+airice::LkTable host_lk(const std::vector<std::vector<float>>& cols) {
+  airice::LkTable T;
+  for (int c = 0; c < AIRICE_TABLE_COLUMNS; ++c) T.col[c] = cols[c].data();
+  T.e = nullptr;
+  T.n = (long long)cols[0].size();
+  T.stop_h = LoopStopHeight;
+  T.step_h = HeightStepSize;
+  T.hsteps = TotalHeightSteps;
+  T.asteps = TotalAngleSteps;
+  return T;
+}
+
+// Cheap content fingerprint of a host table: the column buffers, their length and 64 sampled
+// entries per column.  The HBM copy of a table is reused only while this is unchanged.
+uint64_t table_fingerprint(const std::vector<std::vector<float>>& cols) {
+  uint64_t h = 1469598103934665603ull;
+  auto mix = [&h](uint64_t v) {
+    h ^= v;
+    h *= 1099511628211ull;
+  };
+  const size_t n = cols[0].size();
+  mix(n);
+  for (int c = 0; c < AIRICE_TABLE_COLUMNS; ++c) {
+    mix(reinterpret_cast<uintptr_t>(cols[c].data()));
+    for (size_t k = 0; k < 64; ++k) {
+      uint32_t bits;
+      std::memcpy(&bits, &cols[c][(n - 1) * k / 63], 4);
+      mix(bits);
+    }
+  }
+  return h;
+}
+
+// HBM copy of AllTableAllAntData[i] for the batch lookup: the copy MakeRayTracingTable left
+// behind, or an upload.  A table whose fingerprint changed since (a caller-filled, replaced or
+// edited table) is uploaded again.
+struct DevTable {
+  uint64_t fp = 0;
+  size_t n = 0;
+  float* dev = nullptr;
+  float* packed = nullptr;  // airice_lookup_pack copy, made at the first batch lookup
+};
+std::vector<DevTable> g_tables;
+
+void drop(DevTable& t) {
+  if (t.dev != nullptr) (void)hipFree(t.dev);
+  if (t.packed != nullptr) (void)hipFree(t.packed);
+  t = DevTable();
+}
+
+DevTable& device_table(int index) {
+  const std::vector<std::vector<float>>& cols = host_table(index);
   const size_t n = cols[0].size();
   if (g_tables.size() <= (size_t)index) g_tables.resize(index + 1);
   DevTable& t = g_tables[index];
-  *n_out = n;
-  if (t.dev != nullptr && t.host0 == cols[0].data() && t.n == n) return t.dev;
-  if (t.dev != nullptr) (void)hipFree(t.dev);
-  if (t.packed != nullptr) (void)hipFree(t.packed);
-  t.dev = nullptr;
-  t.packed = nullptr;
+  const uint64_t fp = table_fingerprint(cols);
+  if (t.dev != nullptr && t.fp == fp && t.n == n) return t;
+  drop(t);
   if (hipMalloc(&t.dev, sizeof(float) * AIRICE_TABLE_COLUMNS * n) != hipSuccess) die("hipMalloc");
-  for (int c = 0; c < AIRICE_TABLE_COLUMNS; ++c) {
-    if (cols[c].size() != n) die("table lookup (ragged table)");
+  for (int c = 0; c < AIRICE_TABLE_COLUMNS; ++c)
     if (hipMemcpy(t.dev + (size_t)c * n, cols[c].data(), sizeof(float) * n,
                   hipMemcpyHostToDevice) != hipSuccess)
       die("hipMemcpy table");
-  }
-  t.host0 = cols[0].data();
+  t.fp = fp;
   t.n = n;
-  return t.dev;
+  return t;
 }
 
-airice_lookup_table lookup_desc(const float* dev, size_t n) {
-  airice_lookup_table t;
-  t.entries = nullptr;
-  t.table = dev;
-  t.ld = n;
-  t.n_entries = n;
-  t.loop_stop_height = LoopStopHeight;  // globals of the last table made (.cc:1035-1039)
-  t.height_step = HeightStepSize;
-  t.total_height_steps = TotalHeightSteps;
-  t.total_angle_steps = TotalAngleSteps;
-  return t;
+void set_minmax(const std::vector<std::vector<float>>& cols) {  // .cc:1357-1360 / 1175-1177
+  MaxAirTxHeight = cols[0][0];
+  MinAirTxHeight = cols[0][cols[0].size() - 1];
 }
 
 }  // namespace
 
 namespace MultiRayAirIceRefraction {
 
-int MakeAtmosphere() {
-  std::lock_guard<std::mutex> lock(g_mu);
-  int rc = airice_atmosphere_load("Atmosphere.dat", AIRICE_VARIANT_MULTIRAY, &g_medium);
-  if (rc != AIRICE_OK) {
-    const char* env = std::getenv("AIRICE_ATMOSPHERE");
-    if (env == nullptr || airice_atmosphere_load(env, AIRICE_VARIANT_MULTIRAY, &g_medium) != AIRICE_OK)
-      die("MakeAtmosphere (Atmosphere.dat not found in the working directory or $AIRICE_ATMOSPHERE)");
-  }
-  g_have_medium = true;
+// ---- atmosphere (.cc:24-213, 920-942) ------------------------------------------------------
+int readATMpar() {
+  airice_compat::read_atm_par(atmosphere_text(), ATMLAY, abc);
   return 0;
 }
 
-double GetB_ice(double) { return medium().B_ice; }
-double GetC_ice(double) { return medium().C_ice; }
-double Getnz_ice(double z) { return airice_nz_ice(&medium(), z); }
+int readnhFromFile() {
+  MaxLayers = airice_compat::read_nh(atmosphere_text(), ATMLAY, h_data, nh_data, lognh_data);
+  if (MaxLayers == 0) {
+    std::fprintf(stderr, "MultiRayAirIceRefraction: no refractive-index profile in "
+                         "Atmosphere.dat\n");
+    std::abort();
+  }
+  return 0;
+}
+
+// N0 from the natural cubic spline of the profile at 0 m, then B_air chained for continuity
+// (.cc:193-213): the library's parse of the same file does exactly this
+int FillInAirRefractiveIndex() {
+  const std::string text = atmosphere_text();
+  std::lock_guard<std::mutex> lock(g_mu);
+  if (airice_atmosphere_parse(text.data(), text.size(), AIRICE_VARIANT_MULTIRAY, &g_medium) !=
+      AIRICE_OK)
+    die("FillInAirRefractiveIndex");
+  g_have_medium = true;
+  for (int i = 0; i < 5; i++) {
+    C_air[i] = g_medium.C_air[i];
+    B_air[i] = g_medium.B_air[i];
+  }
+  return 0;
+}
+
+std::vector<double> flatten(const std::vector<std::vector<double>>& v) {
+  return airice_compat::flatten(v);
+}
+
+int MakeAtmosphere() {
+  readATMpar();
+  readnhFromFile();
+  FillInAirRefractiveIndex();
+  return 0;
+}
+
+// GetB_ice / GetC_ice (.cc:150-185; TransitionBoundary is 0) and the air model scan (.cc:216-263)
+double GetB_ice(double) { return B_ice; }
+double GetC_ice(double) { return C_ice; }
+double Getnz_ice(double z) {
+  const airice_medium m = medium();
+  return airice_nz_ice(&m, z);
+}
 
 static int layer_of(double z) {
-  const airice_medium& m = medium();
+  const airice_medium m = medium();
   const double zabs = std::fabs(z);
   int which = 0;
   for (int l = 0; l < m.max_layers - 1; ++l)
@@ -135,7 +273,10 @@ static int layer_of(double z) {
 }
 double GetB_air(double z) { return medium().B_air[layer_of(z)]; }
 double GetC_air(double z) { return medium().C_air[layer_of(z)]; }
-double Getnz_air(double z) { return airice_nz_air(&medium(), z); }
+double Getnz_air(double z) {
+  const airice_medium m = medium();
+  return airice_nz_air(&m, z);
+}
 
 // Fresnel amplitude coefficients (.cc:267-337)
 static void fresnel(double thetai, double ice, double& rS, double& tS, double& rP, double& tP) {
@@ -163,32 +304,95 @@ double oneDLinearInterpolation(double x, double xa, double ya, double xb, double
   return ya + (yb - ya) * ((x - xa) / (xb - xa));  // .cc:992-995
 }
 
+// ---- the ray layer (.cc:377-917) on the GPU ------------------------------------------------
+double fDnfR(double x, void* params) {
+  const fDnfR_params* p = static_cast<const fDnfR_params*>(params);
+  return ray_op1(AIRICE_RTF_FDNFR, {x, p->a, p->b, p->c, p->l});
+}
+
+double ftimeD(double x, void* params) {
+  const ftimeD_params* p = static_cast<const ftimeD_params*>(params);
+  return ray_op1(AIRICE_RTF_FTIMED, {x, p->a, p->b, p->c, p->speedc, p->l, (double)p->airorice});
+}
+
+double fpathD(double x, void* params) {
+  const ftimeD_params* p = static_cast<const ftimeD_params*>(params);
+  return ray_op1(AIRICE_MR_FPATHD, {x, p->a, p->b, p->c, p->speedc, p->l});
+}
+
+double GetRayHorizontalPath(double A, double RxDepth, double TxDepth, double Lvalue, int AirOrIce) {
+  return ray_op1(AIRICE_RTF_OPTICAL_PATH, {A, RxDepth, TxDepth, Lvalue, (double)AirOrIce});
+}
+
+double GetRayPropagationTime(double A, double RxDepth, double TxDepth, double Lvalue,
+                             int AirOrIce) {
+  return ray_op1(AIRICE_RTF_PROPAGATION_TIME, {A, RxDepth, TxDepth, Lvalue, (double)AirOrIce});
+}
+
+double GetRayGeometricPath(double A, double RxDepth, double TxDepth, double Lvalue, int AirOrIce) {
+  return ray_op1(AIRICE_MR_GEOMETRIC_PATH, {A, RxDepth, TxDepth, Lvalue, (double)AirOrIce});
+}
+
+double* GetLayerHitPointPar(double n_layer1, double RxDepth, double TxDepth, double IncidentAng,
+                            int AirOrIce) {
+  double* out = new double[5];
+  ray_op(AIRICE_MR_HIT_POINT, {n_layer1, RxDepth, TxDepth, IncidentAng, (double)AirOrIce}, out,
+         5);
+  return out;
+}
+
+double* GetAirPropagationPar(double LaunchAngle, double AirTxHeight, double IceLayerHeight) {
+  const int n = 5 * medium().max_layers + 2;
+  double* out = new double[n];
+  ray_op(AIRICE_MR_AIR_PROPAGATION, {LaunchAngle, AirTxHeight, IceLayerHeight}, out, n);
+  return out;
+}
+
+double* GetIcePropagationPar(double IncidentAngleonIce, double IceLayerHeight, double AntennaDepth,
+                             double Lvalue) {
+  double* out = new double[5];
+  ray_op(AIRICE_MR_ICE_PROPAGATION, {IncidentAngleonIce, IceLayerHeight, AntennaDepth, Lvalue},
+         out, 5);
+  return out;
+}
+
+double MinimizeforLaunchAngle(double x, void* params) {
+  const MinforLAng_params* p = static_cast<const MinforLAng_params*>(params);
+  return ray_op1(AIRICE_MR_MIN_LAUNCH,
+                 {x, p->airtxheight, p->icelayerheight, p->antennadepth, p->horizontaldistance});
+}
+
+// ---- one-query solves: one launch chain through the scalar slot ----------------------------
 void Air2IceRayTracing(double AirTxHeight, double HorizontalDistance, double IceLayerHeight,
                        double AntennaDepth, double StraightAngle, double dummy[20]) {
-  const airice_medium& m = medium();
-  std::lock_guard<std::mutex> lock(g_mu);
-  double* d = scratch();
-  double in[4] = {AirTxHeight, HorizontalDistance, AntennaDepth, StraightAngle};
-  if (hipMemcpy(d, in, sizeof(in), hipMemcpyHostToDevice) != hipSuccess) die("hipMemcpy");
-  if (airice_solve_launch(&m, AIRICE_VARIANT_MULTIRAY, IceLayerHeight, d, d + 1, d + 2, d + 3, 1,
-                          d + 4, 1, nullptr, nullptr) != AIRICE_OK)
+  const airice_medium m = medium();
+  airice::ScalarCall call;
+  if (!call.ok()) die("Air2IceRayTracing");
+  airice::ScalarSlot& s = call.slot();
+  s.h[0] = AirTxHeight;
+  s.h[1] = HorizontalDistance;
+  s.h[2] = AntennaDepth;
+  s.h[3] = StraightAngle;
+  if (airice_solve_launch(&m, AIRICE_VARIANT_MULTIRAY, IceLayerHeight, s.d, s.d + 1, s.d + 2,
+                          s.d + 3, 1, s.d + 4, 1, nullptr, s.st) != AIRICE_OK ||
+      call.sync() != AIRICE_OK)
     die("Air2IceRayTracing");
-  if (hipMemcpy(dummy, d + 4, sizeof(double) * AIRICE_SOLVE_FIELDS, hipMemcpyDeviceToHost) != hipSuccess)
-    die("hipMemcpy");
+  std::memcpy(dummy, s.h + 4, sizeof(double) * AIRICE_SOLVE_FIELDS);
 }
 
 void GetRayTracingSolutions(double RayLaunchAngleInAir, double AirTxHeight, double IceLayerHeight,
                             double AntennaDepth, double dummy[20], bool& InIce) {
-  const airice_medium& m = medium();
-  std::lock_guard<std::mutex> lock(g_mu);
-  double* d = scratch();
-  double in[2] = {RayLaunchAngleInAir, AirTxHeight};
-  if (hipMemcpy(d, in, sizeof(in), hipMemcpyHostToDevice) != hipSuccess) die("hipMemcpy");
-  if (airice_rays_launch(&m, d, d + 1, IceLayerHeight, AntennaDepth, InIce ? 1 : 0, 1, d + 2, 1,
-                         nullptr) != AIRICE_OK)
+  const airice_medium m = medium();
+  airice::ScalarCall call;
+  if (!call.ok()) die("GetRayTracingSolutions");
+  airice::ScalarSlot& s = call.slot();
+  s.h[0] = RayLaunchAngleInAir;
+  s.h[1] = AirTxHeight;
+  if (airice_rays_launch(&m, s.d, s.d + 1, IceLayerHeight, AntennaDepth, InIce ? 1 : 0, 1,
+                         s.d + 2, 1, s.st) != AIRICE_OK ||
+      call.sync() != AIRICE_OK)
     die("GetRayTracingSolutions");
-  if (hipMemcpy(dummy, d + 2, sizeof(double) * AIRICE_RAY_FIELDS, hipMemcpyDeviceToHost) != hipSuccess)
-    die("hipMemcpy");
+  std::memcpy(dummy, s.h + 2, sizeof(double) * AIRICE_RAY_FIELDS);
 }
 
 bool GetHorizontalDistanceToIntersectionPoint(
@@ -197,16 +401,20 @@ bool GetHorizontalDistanceToIntersectionPoint(
     double& geometricalPathLengthInIce, double& geometricalPathLengthInAir, double& launchAngle,
     double& horizontalDistanceToIntersectionPoint, double& transmissionCoefficientS,
     double& transmissionCoefficientP, double& RecievedAngleInIce) {
-  const airice_medium& m = medium();
-  std::lock_guard<std::mutex> lock(g_mu);
-  double* d = scratch();
-  double in[3] = {SrcHeightASL, HorizontalDistanceToRx, RxDepthBelowIceBoundary};
-  if (hipMemcpy(d, in, sizeof(in), hipMemcpyHostToDevice) != hipSuccess) die("hipMemcpy");
-  uint8_t* ok = reinterpret_cast<uint8_t*>(d + 12);
-  if (airice_hdtip_launch(&m, d, d + 1, d + 2, IceLayerHeight, 1, d + 3, 1, ok, nullptr) != AIRICE_OK)
+  const airice_medium m = medium();
+  airice::ScalarCall call;
+  if (!call.ok()) die("GetHorizontalDistanceToIntersectionPoint");
+  airice::ScalarSlot& s = call.slot();
+  s.h[0] = SrcHeightASL;
+  s.h[1] = HorizontalDistanceToRx;
+  s.h[2] = RxDepthBelowIceBoundary;
+  uint8_t* ok_h = reinterpret_cast<uint8_t*>(s.h + 12);
+  uint8_t* ok_d = reinterpret_cast<uint8_t*>(s.d + 12);
+  if (airice_hdtip_launch(&m, s.d, s.d + 1, s.d + 2, IceLayerHeight, 1, s.d + 3, 1, ok_d, s.st) !=
+          AIRICE_OK ||
+      call.sync() != AIRICE_OK)
     die("GetHorizontalDistanceToIntersectionPoint");
-  double o[10];
-  if (hipMemcpy(o, d + 3, sizeof(double) * 10, hipMemcpyDeviceToHost) != hipSuccess) die("hipMemcpy");
+  const double* o = s.h + 3;
   opticalPathLengthInIce = o[0];
   opticalPathLengthInAir = o[1];
   geometricalPathLengthInIce = o[2];
@@ -216,14 +424,14 @@ bool GetHorizontalDistanceToIntersectionPoint(
   transmissionCoefficientS = o[6];
   transmissionCoefficientP = o[7];
   RecievedAngleInIce = o[8];
-  const uint8_t flag = reinterpret_cast<const uint8_t*>(&o[9])[0];
-  return flag != 0;
+  return ok_h[0] != 0;
 }
 
+// ---- MakeRayTracingTable (.cc:2019-2158) ---------------------------------------------------
 int MakeRayTracingTable(double AntennaDepth, double IceLayerHeight, int AntennaNumber) {
   (void)AntennaNumber;  // the reference appends in call order (.cc:2136)
   MakeAtmosphere();     // the reference re-reads the atmosphere on every table (.cc:2039)
-  const airice_medium& m = medium();
+  const airice_medium m = medium();
   airice_grid g;
   if (airice_grid_init(&g, AntennaDepth, IceLayerHeight, HeightStepSize, LoopStartAngle,
                        LoopStopAngle, AngleStepSize) != AIRICE_OK)
@@ -232,26 +440,86 @@ int MakeRayTracingTable(double AntennaDepth, double IceLayerHeight, int AntennaN
   LoopStartHeight = g.start_height;
   LoopStopHeight = g.stop_height;
   TotalHeightSteps = g.height_steps;
-  const size_t n = (size_t)g.height_steps * (size_t)g.angle_steps;
+  // rows with Tx <= 0 are skipped (.cc:2082): the table holds g.table_rows rows
+  const size_t n = (size_t)g.table_rows * (size_t)g.angle_steps;
   float* dt = nullptr;
-  if (hipMalloc(&dt, sizeof(float) * 11 * n) != hipSuccess) die("hipMalloc table");
-  if (airice_table_launch(&m, &g, 0, g.height_steps, dt, nullptr, n, nullptr) != AIRICE_OK)
+  if (n > 0 && hipMalloc(&dt, sizeof(float) * 11 * n) != hipSuccess) die("hipMalloc table");
+  if (n > 0 && airice_table_launch(&m, &g, 0, g.table_rows, dt, nullptr, n, nullptr) != AIRICE_OK)
     die("MakeRayTracingTable");
   std::vector<std::vector<float>> cols(11, std::vector<float>(n));
-  for (int c = 0; c < 11; ++c)
+  for (int c = 0; c < 11 && n > 0; ++c)
     if (hipMemcpy(cols[c].data(), dt + (size_t)c * n, sizeof(float) * n, hipMemcpyDeviceToHost) !=
         hipSuccess)
       die("hipMemcpy table");
   AllTableAllAntData.push_back(std::move(cols));
-  // keep the HBM copy for the lookups (moving the column vectors keeps their storage)
+  // keep the HBM copy for batch lookups (moving the column vectors keeps their storage)
+  std::lock_guard<std::mutex> lock(g_mu);
   const size_t index = AllTableAllAntData.size() - 1;
   if (g_tables.size() <= index) g_tables.resize(index + 1);
-  if (g_tables[index].dev != nullptr) (void)hipFree(g_tables[index].dev);
-  if (g_tables[index].packed != nullptr) (void)hipFree(g_tables[index].packed);
-  g_tables[index].packed = nullptr;
-  g_tables[index].dev = dt;
-  g_tables[index].host0 = AllTableAllAntData[index][0].data();
-  g_tables[index].n = n;
+  drop(g_tables[index]);
+  if (n > 0) {
+    g_tables[index].dev = dt;
+    g_tables[index].n = n;
+    g_tables[index].fp = table_fingerprint(AllTableAllAntData[index]);
+  }
+  return 0;
+}
+
+// ---- table walks (.cc:997-1302) on the host ------------------------------------------------
+double Extrapolate(int Par, int index, double TotalHorizontalDistance, int AntennaNumber) {
+  const std::vector<std::vector<float>>& t = host_table(AntennaNumber);
+  const double x1 = t[1][index], x2 = t[1][index + 1];
+  const double y1 = t[Par][index], y2 = t[Par][index + 1];
+  const double m = (y2 - y1) / (x2 - x1);
+  const double c = y1 - m * x1;
+  return m * TotalHorizontalDistance + c;
+}
+
+double FindExtrapolationLimit(int index, double TotalHorizontalDistance, int AntennaNumber) {
+  (void)TotalHorizontalDistance;  // unused by the reference (.cc:1026-1027 commented out)
+  const std::vector<std::vector<float>>& t = host_table(AntennaNumber);
+  const double x1 = t[1][index], x2 = t[1][index + 1];
+  const double y1 = t[4][index], y2 = t[4][index + 1];
+  const double m = (y1 - y2) / (x1 - x2);
+  const double c = y1 - m * x1;
+  return (90 - c) / m;
+}
+
+void FindClosestAirTxHeight(double ParValue, int& RStartIndex1, int& REndIndex1,
+                            double& ClosestVal1, int& RStartIndex2, int& REndIndex2,
+                            double& ClosestVal2, int AntennaNumber) {
+  const airice::LkTable T = host_lk(host_table(AntennaNumber));
+  int fl = 0;
+  const airice::LkTxhBins b = airice::lk_closest_txh(T, ParValue, fl);
+  RStartIndex1 = (int)b.s1;
+  REndIndex1 = (int)b.e1;
+  ClosestVal1 = b.c1;
+  RStartIndex2 = (int)b.s2;
+  REndIndex2 = (int)b.e2;
+  ClosestVal2 = b.c2;
+}
+
+int FindClosestTHD(double ParValue, int StartIndex, int EndIndex, int& RStartIndex,
+                   int& REndIndex, double& ClosestVal, int AntennaNumber) {
+  const airice::LkTable T = host_lk(host_table(AntennaNumber));
+  int fl = 0;
+  const airice::LkThdBins b = airice::lk_closest_thd(T, ParValue, StartIndex, EndIndex, fl);
+  RStartIndex = (int)b.s;
+  REndIndex = (int)b.e;
+  ClosestVal = b.c;
+  return 0;
+}
+
+int GetParValues(double AntennaNumber, double AirTxHeight, double TotalHorizontalDistance,
+                 double IceLayerHeight, double& AirTxHeight1, double Par1[10],
+                 double& AirTxHeight2, double Par2[10]) {
+  (void)IceLayerHeight;  // unused by the reference
+  const std::vector<std::vector<float>>& cols = host_table((int)AntennaNumber);
+  set_minmax(cols);
+  const airice::LkTable T = host_lk(cols);
+  int fl = 0;
+  airice::lk_par_values(T, AirTxHeight, TotalHorizontalDistance, &AirTxHeight1, Par1,
+                        &AirTxHeight2, Par2, fl);
   return 0;
 }
 
@@ -262,11 +530,22 @@ bool TableLookup(double SrcHeightASL, double HorizontalDistanceToRx,
                  double& launchAngle, double& horizontalDistanceToIntersectionPoint,
                  double& transmissionCoefficientS, double& transmissionCoefficientP,
                  double& RecievedAngleInIce) {
-  const double src[1] = {SrcHeightASL}, dist[1] = {HorizontalDistanceToRx},
-               dep[1] = {RxDepthBelowIceBoundary};
+  const std::vector<std::vector<float>>& cols = host_table(TableIndex);
+  set_minmax(cols);
+  const airice::LkTable T = host_lk(cols);
   double o[9];
-  bool ok = false;
-  TableLookupBatch(src, dist, dep, IceLayerHeight, TableIndex, 1, o, &ok);
+  bool good = false;
+  int fl = 0;
+  // pi/180 exactly as the device's DevMedium::d2r (MultiRay pi, .cc:1410)
+  if (airice::lk_query(T, SrcHeightASL / 100, HorizontalDistanceToRx / 100, pi / 180.0, o, &good,
+                       fl)) {
+    // the one-sided extrapolation case: the reference's minimizer fallback (.cc:1418-1420)
+    const airice_medium m = medium();
+    if (airice::lookup_fallback_one(&m, SrcHeightASL, HorizontalDistanceToRx,
+                                    RxDepthBelowIceBoundary, IceLayerHeight, good, fl, o,
+                                    &good) != AIRICE_OK)
+      die("GetHorizontalDistanceToIntersectionPoint_Table fallback");
+  }
   opticalPathLengthInIce = o[0];
   opticalPathLengthInAir = o[1];
   geometricalPathLengthInIce = o[2];
@@ -276,25 +555,59 @@ bool TableLookup(double SrcHeightASL, double HorizontalDistanceToRx,
   transmissionCoefficientS = o[6];
   transmissionCoefficientP = o[7];
   RecievedAngleInIce = o[8];
-  return ok;
+  return good;
+}
+
+bool GetHorizontalDistanceToIntersectionPoint_Table(
+    double SrcHeightASL, double HorizontalDistanceToRx, double RxDepthBelowIceBoundary,
+    double IceLayerHeight, int AntennaNumber, double& opticalPathLengthInIce,
+    double& opticalPathLengthInAir, double& geometricalPathLengthInIce,
+    double& geometricalPathLengthInAir, double& launchAngle,
+    double& horizontalDistanceToIntersectionPoint, double& transmissionCoefficientS,
+    double& transmissionCoefficientP, double& RecievedAngleInIce) {
+  // antenna -> table remap over the caller's vectors (.cc:1348-1352)
+  if (&AntennaDepths != nullptr && &AntennaTableAlreadyMade != nullptr) {
+    for (int j = 0; j < (int)AntennaTableAlreadyMade.size(); j++)
+      if (AntennaDepths[AntennaNumber] == AntennaDepths[AntennaTableAlreadyMade[j]])
+        AntennaNumber = j;
+  }
+  return TableLookup(SrcHeightASL, HorizontalDistanceToRx, RxDepthBelowIceBoundary,
+                     IceLayerHeight, AntennaNumber, opticalPathLengthInIce,
+                     opticalPathLengthInAir, geometricalPathLengthInIce,
+                     geometricalPathLengthInAir, launchAngle,
+                     horizontalDistanceToIntersectionPoint, transmissionCoefficientS,
+                     transmissionCoefficientP, RecievedAngleInIce);
 }
 
 void TableLookupBatch(const double* SrcHeightASL, const double* HorizontalDistanceToRx,
                       const double* RxDepthBelowIceBoundary, double IceLayerHeight, int TableIndex,
                       size_t n, double* out9, bool* ok) {
-  const airice_medium& m = medium();
-  std::lock_guard<std::mutex> lock(g_mu);
-  size_t entries = 0;
-  const float* dev = device_table(TableIndex, &entries);
-  // MaxAirTxHeight / MinAirTxHeight globals (.cc:1359-1360)
-  MaxAirTxHeight = AllTableAllAntData[TableIndex][0][0];
-  MinAirTxHeight = AllTableAllAntData[TableIndex][0][entries - 1];
+  const airice_medium m = medium();
+  const std::vector<std::vector<float>>& cols = host_table(TableIndex);
+  set_minmax(cols);
   if (n == 0) return;
+  std::lock_guard<std::mutex> lock(g_mu);
+  DevTable& dt = device_table(TableIndex);
+  const size_t entries = dt.n;
+  airice_lookup_table t;
+  t.table = dt.dev;
+  t.ld = entries;
+  t.n_entries = entries;
+  t.loop_stop_height = LoopStopHeight;  // globals of the last table made (.cc:1035-1039)
+  t.height_step = HeightStepSize;
+  t.total_height_steps = TotalHeightSteps;
+  t.total_angle_steps = TotalAngleSteps;
+  t.entries = nullptr;
+  if (dt.packed == nullptr) {
+    if (hipMalloc(&dt.packed, sizeof(float) * AIRICE_LOOKUP_ENTRY_FLOATS * entries) != hipSuccess ||
+        airice_lookup_pack(&t, dt.packed, nullptr) != AIRICE_OK)
+      die("airice_lookup_pack");
+  }
+  t.entries = dt.packed;
   // one device block: src | dist | depth | out (9 columns) | ok | flags
-  const size_t bytes = sizeof(double) * 12 * n + 2 * n;
-  const bool small = bytes <= kScratch * sizeof(double);
-  double* d = small ? scratch() : nullptr;
-  if (!small && hipMalloc(&d, bytes) != hipSuccess) die("hipMalloc");
+  void* mem = nullptr;
+  if (hipMalloc(&mem, sizeof(double) * 12 * n + 2 * n) != hipSuccess) die("hipMalloc");
+  double* d = static_cast<double*>(mem);
   if (hipMemcpy(d, SrcHeightASL, sizeof(double) * n, hipMemcpyHostToDevice) != hipSuccess ||
       hipMemcpy(d + n, HorizontalDistanceToRx, sizeof(double) * n, hipMemcpyHostToDevice) !=
           hipSuccess ||
@@ -303,16 +616,8 @@ void TableLookupBatch(const double* SrcHeightASL, const double* HorizontalDistan
     die("hipMemcpy");
   uint8_t* dok = reinterpret_cast<uint8_t*>(d + 12 * n);
   uint8_t* dfl = dok + n;
-  airice_lookup_table t = lookup_desc(dev, entries);
-  DevTable& dt = g_tables[TableIndex];
-  if (dt.packed == nullptr) {
-    if (hipMalloc(&dt.packed, sizeof(float) * AIRICE_LOOKUP_ENTRY_FLOATS * entries) != hipSuccess ||
-        airice_lookup_pack(&t, dt.packed, nullptr) != AIRICE_OK)
-      die("airice_lookup_pack");
-  }
-  t.entries = dt.packed;
-  if (airice_table_lookup_launch(&m, &t, d, d + n, d + 2 * n, IceLayerHeight, n, d + 3 * n, n,
-                                 dok, dfl, nullptr) != AIRICE_OK)
+  if (airice_table_lookup_launch(&m, &t, d, d + n, d + 2 * n, IceLayerHeight, n, d + 3 * n, n, dok,
+                                 dfl, nullptr) != AIRICE_OK)
     die("GetHorizontalDistanceToIntersectionPoint_Table");
   std::vector<double> soa(9 * n);
   std::vector<uint8_t> hok(n);
@@ -320,7 +625,7 @@ void TableLookupBatch(const double* SrcHeightASL, const double* HorizontalDistan
           hipSuccess ||
       hipMemcpy(hok.data(), dok, n, hipMemcpyDeviceToHost) != hipSuccess)
     die("hipMemcpy");
-  if (!small) (void)hipFree(d);
+  (void)hipFree(mem);
   for (size_t i = 0; i < n; ++i) {
     for (int c = 0; c < 9; ++c) out9[i * 9 + c] = soa[(size_t)c * n + i];
     ok[i] = hok[i] != 0;

@@ -4,14 +4,13 @@
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
-#include <fstream>
 #include <mutex>
-#include <sstream>
 #include <string>
 #include <vector>
 
 #include "RayTracingFunctions.h"
 #include "airice.h"
+#include "compat_common.h"
 
 namespace RayTracingFunctions {
 
@@ -39,22 +38,7 @@ bool g_have_medium = false;
   std::abort();  // the reference has no error channel; fail loudly, never fall back
 }
 
-// Atmosphere.dat from the working directory, as the reference opens it (.cc:6, 55), else
-// $AIRICE_ATMOSPHERE
-std::string atmosphere_text() {
-  const char* env = std::getenv("AIRICE_ATMOSPHERE");
-  for (const char* path : {"Atmosphere.dat", env}) {
-    if (path == nullptr) continue;
-    std::ifstream f(path, std::ios::binary);
-    if (!f.is_open()) continue;
-    std::ostringstream s;
-    s << f.rdbuf();
-    return s.str();
-  }
-  std::fprintf(stderr, "RayTracingFunctions: Atmosphere.dat not found in the working directory "
-                       "or $AIRICE_ATMOSPHERE\n");
-  std::abort();
-}
+std::string atmosphere_text() { return airice_compat::atmosphere_text("RayTracingFunctions"); }
 
 const airice_medium& medium() {
   if (!g_have_medium) R::MakeAtmosphere();
@@ -91,67 +75,19 @@ int layer_of(double z) {  // GetB_air / GetC_air scan over the globals (.cc:172-
 
 namespace RayTracingFunctions {
 
-// readATMpar (.cc:4-49): the first four value rows, read with the reference's stream pattern
-// (getline, then five >> reads from the following line); layer 4 copies layer 3, top 1500 km
+// readATMpar (.cc:4-49)
 int readATMpar() {
-  std::istringstream in(atmosphere_text());
-  std::string line;
-  double v[5] = {0, 0, 0, 0, 0};
-  for (int row = 0; std::getline(in, line); ++row) {
-    if (row < 4) in >> v[0] >> v[1] >> v[2] >> v[3] >> v[4];
-    if (row == 0) for (int i = 0; i < 5; i++) ATMLAY[i] = v[i];
-    if (row >= 1 && row <= 3) for (int i = 0; i < 5; i++) abc[i][row - 1] = v[i];
-  }
-  for (int k = 0; k < 3; k++) abc[4][k] = abc[3][k];
-  ATMLAY[4] = 150000 * 100;
+  airice_compat::read_atm_par(atmosphere_text(), ATMLAY, abc);
   return 0;
 }
 
-// readnhFromFile (.cc:51-124): (h, n) pairs from h > -1 m, grouped into layers at the ATMLAY
-// bounds, the duplicated last pair of the stream dropped; MaxLayers = layers + 1
+// readnhFromFile (.cc:51-124): MaxLayers = layers + 1
 int readnhFromFile() {
-  nh_data.clear();
-  lognh_data.clear();
-  h_data.clear();
-  std::istringstream in(atmosphere_text());
-  for (int i = 0; i < 5; i++) in.ignore(256, '\n');
-  std::string line;
-  int layer = 0;
-  double h = 0, n = 0;
-  std::vector<double> th, tn, tl;
-  while (std::getline(in, line)) {
-    in >> h >> n;
-    if (h > -1) {
-      th.push_back(h);
-      tn.push_back(n);
-      tl.push_back(std::log(n - 1));
-      if (h * 100 >= ATMLAY[layer < 4 ? layer : 4]) {  // (a profile above 1500 km would index
-                                                     //  past ATMLAY in the reference)
-        if (layer > 0) {
-          h_data.push_back(th);
-          nh_data.push_back(tn);
-          lognh_data.push_back(tl);
-          th.clear();
-          tn.clear();
-          tl.clear();
-        }
-        layer++;
-      }
-    }
-  }
-  if (layer > 0) {
-    h_data.push_back(th);
-    nh_data.push_back(tn);
-    lognh_data.push_back(tl);
-  }
-  if (h_data.empty() || h_data.back().empty()) {
+  MaxLayers = airice_compat::read_nh(atmosphere_text(), ATMLAY, h_data, nh_data, lognh_data);
+  if (MaxLayers == 0) {
     std::fprintf(stderr, "RayTracingFunctions: no refractive-index profile in Atmosphere.dat\n");
     std::abort();
   }
-  h_data.back().pop_back();
-  nh_data.back().pop_back();
-  lognh_data.back().pop_back();
-  MaxLayers = (int)h_data.size() + 1;
   return 0;
 }
 
@@ -237,9 +173,7 @@ double* GetLayerHitPointPar(double n_layer1, double RxDepth, double TxDepth, dou
 }
 
 std::vector<double> flatten(const std::vector<std::vector<double>>& v) {  // .cc:517-527
-  std::vector<double> r;
-  for (const auto& s : v) r.insert(r.end(), s.begin(), s.end());
-  return r;
+  return airice_compat::flatten(v);
 }
 
 double* GetAirPropagationPar(double LaunchAngle, double AirTxHeight, double IceLayerHeight) {

@@ -51,11 +51,11 @@ def table_sharded(grid, compute: Callable[[int, int, torch.Tensor], None], cols:
     world = dist.get_world_size(group)
     rank = dist.get_rank(group)
     asteps = int(grid.angle_steps)
-    begin, count, per = shard_rows(int(grid.height_steps), world, rank)
+    begin, count, per = shard_rows(int(grid.table_rows), world, rank)
     slab = torch.zeros((cols, per * asteps), dtype=dtype, device=device)
     if count:
         compute(begin, count, slab)
-    counts = [shard_rows(int(grid.height_steps), world, r)[1] * asteps for r in range(world)]
+    counts = [shard_rows(int(grid.table_rows), world, r)[1] * asteps for r in range(world)]
     return gather_slabs(slab, per * asteps, counts, root, group)
 
 
@@ -105,7 +105,7 @@ def run_sharded_table(grid, compute: Callable[[int, int, torch.Tensor], None], s
     sync = sync or (lambda: None)
     coll_device = coll_device if coll_device is not None else device
     asteps = int(grid.angle_steps)
-    begin, count, per = shard_rows(int(grid.height_steps), world, rank)
+    begin, count, per = shard_rows(int(grid.table_rows), world, rank)
     slab = torch.zeros((cols, per * asteps), dtype=dtype, device=device)
 
     def step():
@@ -123,7 +123,7 @@ def run_sharded_table(grid, compute: Callable[[int, int, torch.Tensor], None], s
     sync()
     elapsed = time.perf_counter() - t0
     dist.barrier(group)
-    counts = [shard_rows(int(grid.height_steps), world, r)[1] * asteps for r in range(world)]
+    counts = [shard_rows(int(grid.table_rows), world, r)[1] * asteps for r in range(world)]
     send = slab if coll_device is None or slab.device == torch.device(coll_device) \
         else slab.to(coll_device)
     assembled = None

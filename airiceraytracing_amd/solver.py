@@ -50,7 +50,7 @@ class AirIceSolver:
     def table_device(self, grid: Grid, table, full=None, row_begin: int = 0,
                      row_count: int | None = None, ld: int | None = None, stream=None) -> None:
         if row_count is None:
-            row_count = grid.height_steps - row_begin
+            row_count = grid.table_rows - row_begin
         n = row_count * grid.angle_steps
         ld = n if ld is None else ld
         check(lib().airice_table_launch(ctypes.byref(self.medium), ctypes.byref(grid), row_begin,
@@ -60,7 +60,7 @@ class AirIceSolver:
     def table_host(self, grid: Grid, row_begin: int = 0, row_count: int | None = None,
                    full: bool = False):
         if row_count is None:
-            row_count = grid.height_steps - row_begin
+            row_count = grid.table_rows - row_begin
         n = row_count * grid.angle_steps
         table = np.empty((_lib.TABLE_COLUMNS, n), dtype=np.float32)
         fullarr = np.empty((_lib.RAY_FIELDS, n), dtype=np.float64) if full else None

@@ -1,19 +1,33 @@
 /*
  * MultiRayAirIceRefraction.h -- C++ drop-in surface of libairice.so for CoREAS-style callers.
  *
- * Same namespace, function names, signatures, units and globals as the reference's
- * MultiRayAirIceRefraction.h/.cc (uzairlatif90/AirIceRayTracing), so existing call sites
- * (e.g. RunMultiRayCode.C:29-59) compile and link against libairice.so unchanged, minus the
- * `#include "MultiRayAirIceRefraction.cc"` line.  The hot path -- MakeRayTracingTable
- * (.cc:2019), GetRayTracingSolutions (.cc:1796), Air2IceRayTracing (.cc:1464),
- * GetHorizontalDistanceToIntersectionPoint (.cc:945) and its table variant _Table (.cc:1305)
- * -- runs on the MI355X.
+ * Same namespace, function names, signatures (hence mangled names), units and globals as the
+ * reference's MultiRayAirIceRefraction.h/.cc (uzairlatif90/AirIceRayTracing), so existing call
+ * sites (e.g. RunMultiRayCode.C:29-59) compile and link against libairice.so unchanged, minus the
+ * `#include "MultiRayAirIceRefraction.cc"` line.
  *
- * Not provided: the GSL-typed internals (FindFunctionRoot, gsl_* statics) and the helpers
- * that return heap scratch arrays (GetLayerHitPointPar, Get{Air,Ice}PropagationPar,
- * fDnfR/ftimeD/fpathD, MinimizeforLaunchAngle); they are implementation details of the
- * reference's CPU solver with no caller outside it.  The deprecated MakeTable /
- * GetInterpolatedValue (.cc:1618-1794, "Do not use this function") are not provided.
+ * Where each function runs:
+ *   - GPU batch kernels: MakeRayTracingTable (.cc:2019), GetRayTracingSolutions (.cc:1796),
+ *     Air2IceRayTracing (.cc:1464), GetHorizontalDistanceToIntersectionPoint (.cc:945) and the
+ *     ray layer (fDnfR, ftimeD, fpathD, GetRay{Horizontal,Geometric}Path, GetRayPropagationTime,
+ *     GetLayerHitPointPar, Get{Air,Ice}PropagationPar, MinimizeforLaunchAngle), one query per
+ *     call through a pinned, device-mapped staging slot (one launch chain + one synchronisation).
+ *   - Host, from the same source the batch lookup kernel is compiled from (airice_lookup.hpp):
+ *     GetHorizontalDistanceToIntersectionPoint_Table (.cc:1305), GetParValues (.cc:1172),
+ *     FindClosestAirTxHeight (.cc:1033), FindClosestTHD (.cc:1128) -- table walks over the
+ *     caller's host AllTableAllAntData, bit-identical to the device lookup; a query that reaches
+ *     the reference's minimizer fallback (.cc:1418) runs that solve on the GPU.  Extrapolate /
+ *     FindExtrapolationLimit (.cc:997-1031) and the atmosphere file readers are host code as in
+ *     the reference.
+ *
+ * Not provided: FindFunctionRoot and the gsl_interp_accel / gsl_spline statics (their types are
+ * GNU GSL's, absent from this build; the root finding lives in the kernels), and the deprecated
+ * MakeTable / GetInterpolatedValue (.cc:1618-1794, "Do not use this function").
+ *
+ * Namespace data: the reference defines it as header statics (one copy per translation unit,
+ * .h:33-81); here it is one shared copy, filled by MakeAtmosphere().  A_ice / B_ice / C_ice are
+ * read by every call, so a caller that changes them (as the reference allows) changes the ice
+ * model of the following calls and tables.
  *
  * Units (as the reference): CoREAS-facing functions take and return cm and radians;
  * Air2IceRayTracing / GetRayTracingSolutions take m and degrees.  AntennaDepth < 0 means
@@ -46,11 +60,37 @@ namespace MultiRayAirIceRefraction {
 
 static const double pi = 3.1415927;       /* .h:29 (sic: not M_PI) */
 static const double spedc = 299792458.0;  /* .h:30 */
+
+/* refractive-index profile of Atmosphere.dat (.h:33-35), filled by readnhFromFile() */
+extern std::vector<std::vector<double>> nh_data;
+extern std::vector<std::vector<double>> lognh_data;
+extern std::vector<std::vector<double>> h_data;
+/* interpolation grid of the deprecated MakeTable (.h:38-53), kept with the reference's values */
+extern std::vector<double> GridPositionH;
+extern std::vector<double> GridPositionTh;
+extern std::vector<double> GridZValue[10];
+extern double GridStartTh, GridStopTh, GridStepSizeH_O, GridStepSizeTh_O, GridWidthH, GridWidthTh;
+extern int GridPoints, TotalStepsH_O, TotalStepsTh_O;
+extern double GridStartH, GridStopH;
+/* ATMLAY and the mass-overburden a,b,c rows (.h:56-57), the fitted air model (.h:60-61) */
+extern double ATMLAY[5];
+extern double abc[5][3];
+extern double C_air[5];
+extern double B_air[5];
 static const double A_ice_def = 1.78;
 static const double B_ice_def = -0.43;
 static const double C_ice_def = 0.0132;
 static constexpr double TransitionBoundary = 0;
+extern double A_ice; /* .h:75-77: A_ice_def, B_ice_def, C_ice_def */
+extern double B_ice;
+extern double C_ice;
+extern int MaxLayers; /* .h:84 */
 static const double A_air = 1.00;
+
+int readATMpar();
+int readnhFromFile();
+int FillInAirRefractiveIndex();
+std::vector<double> flatten(const std::vector<std::vector<double>>& v);
 
 /* Reads "Atmosphere.dat" from the working directory (falls back to $AIRICE_ATMOSPHERE). */
 int MakeAtmosphere();
@@ -78,6 +118,39 @@ bool GetHorizontalDistanceToIntersectionPoint(
 
 double oneDLinearInterpolation(double x, double xa, double ya, double xb, double yb);
 
+/* The ray layer (.cc:377-917), evaluated on the GPU.  *Par functions return new[]'d arrays the
+ * caller delete[]s, as with the reference: GetLayerHitPointPar / GetIcePropagationPar 5 doubles
+ * {THD, receive angle deg, L, time s, geometric path}; GetAirPropagationPar 5 x MaxLayers + 2,
+ * per layer the same five, the filled-layer count at [5 * MaxLayers + 1]. */
+struct fDnfR_params { double a, b, c, l; };
+double fDnfR(double x, void* params);
+struct ftimeD_params { double a, b, c, speedc, l; int airorice; };
+double ftimeD(double x, void* params);
+double fpathD(double x, void* params);
+double GetRayHorizontalPath(double A, double RxDepth, double TxDepth, double Lvalue, int AirOrIce);
+double GetRayPropagationTime(double A, double RxDepth, double TxDepth, double Lvalue, int AirOrIce);
+double GetRayGeometricPath(double A, double RxDepth, double TxDepth, double Lvalue, int AirOrIce);
+double* GetLayerHitPointPar(double n_layer1, double RxDepth, double TxDepth, double IncidentAng,
+                            int AirOrIce);
+double* GetAirPropagationPar(double LaunchAngle, double AirTxHeight, double IceLayerHeight);
+double* GetIcePropagationPar(double IncidentAngleonIce, double IceLayerHeight, double AntennaDepth,
+                             double Lvalue);
+struct MinforLAng_params { double airtxheight, icelayerheight, antennadepth, horizontaldistance; };
+double MinimizeforLaunchAngle(double x, void* params);
+
+/* Table walks (.cc:997-1302) over AllTableAllAntData[AntennaNumber] and the grid globals of the
+ * last table made; run on the host with the batch lookup kernel's own code. */
+double Extrapolate(int Par, int index, double TotalHorizontalDistance, int AntennaNumber);
+double FindExtrapolationLimit(int index, double TotalHorizontalDistance, int AntennaNumber);
+void FindClosestAirTxHeight(double ParValue, int& RStartIndex1, int& REndIndex1,
+                            double& ClosestVal1, int& RStartIndex2, int& REndIndex2,
+                            double& ClosestVal2, int AntennaNumber);
+int FindClosestTHD(double ParValue, int StartIndex, int EndIndex, int& RStartIndex,
+                   int& REndIndex, double& ClosestVal, int AntennaNumber);
+int GetParValues(double AntennaNumber, double AirTxHeight, double TotalHorizontalDistance,
+                 double IceLayerHeight, double& AirTxHeight1, double Par1[10],
+                 double& AirTxHeight2, double Par2[10]);
+
 /* Air2IceRayTracing (.cc:1464): m / degrees; fills dummy[0..16]. */
 void Air2IceRayTracing(double AirTxHeight, double HorizontalDistance, double IceLayerHeight,
                        double AntennaDepth, double StraightAngle, double dummy[20]);
@@ -91,10 +164,20 @@ void GetRayTracingSolutions(double RayLaunchAngleInAir, double AirTxHeight, doub
  * in 10 m steps x 90.1..180 deg in 0.1 deg steps).  Returns 0. */
 int MakeRayTracingTable(double AntennaDepth, double IceLayerHeight, int AntennaNumber);
 
-/* Table lookup on an already-resolved table index (AllTableAllAntData[TableIndex]), run on the
- * GPU against the table's HBM copy (kept from MakeRayTracingTable, or uploaded on first use
- * when AllTableAllAntData[TableIndex] was filled by the caller).  Same outputs, units, globals
- * (MaxAirTxHeight / MinAirTxHeight are set) and quirks as the reference (.cc:1305-1462). */
+/* GetHorizontalDistanceToIntersectionPoint_Table (.cc:1305-1462): the antenna -> table remap
+ * over the caller's AntennaDepths / AntennaTableAlreadyMade (.cc:1348-1352), then one lookup on
+ * the host (see above).  Same outputs, units, globals (MaxAirTxHeight / MinAirTxHeight) and
+ * quirks as the reference. */
+bool GetHorizontalDistanceToIntersectionPoint_Table(
+    double SrcHeightASL, double HorizontalDistanceToRx, double RxDepthBelowIceBoundary,
+    double IceLayerHeight, int AntennaNumber, double& opticalPathLengthInIce,
+    double& opticalPathLengthInAir, double& geometricalPathLengthInIce,
+    double& geometricalPathLengthInAir, double& launchAngle,
+    double& horizontalDistanceToIntersectionPoint, double& transmissionCoefficientS,
+    double& transmissionCoefficientP, double& RecievedAngleInIce);
+
+/* Extensions (no reference counterpart). */
+/* The same lookup on an already-resolved table index (AllTableAllAntData[TableIndex]). */
 bool TableLookup(double SrcHeightASL, double HorizontalDistanceToRx,
                  double RxDepthBelowIceBoundary, double IceLayerHeight, int TableIndex,
                  double& opticalPathLengthInIce, double& opticalPathLengthInAir,
@@ -103,34 +186,13 @@ bool TableLookup(double SrcHeightASL, double HorizontalDistanceToRx,
                  double& transmissionCoefficientS, double& transmissionCoefficientP,
                  double& RecievedAngleInIce);
 
-/* Batched form: n queries (cm) against one resolved table; out is n rows of the 9 outputs in
- * the reference's argument order; ok[i] the returned bool.  One launch for the whole batch. */
+/* Batched form on the GPU: n queries (cm) against one resolved table; out is n rows of the 9
+ * outputs in the reference's argument order; ok[i] the returned bool.  One launch chain for the
+ * whole batch against the table's HBM copy (kept from MakeRayTracingTable; a table the caller
+ * filled or changed is uploaded again). */
 void TableLookupBatch(const double* SrcHeightASL, const double* HorizontalDistanceToRx,
                       const double* RxDepthBelowIceBoundary, double IceLayerHeight, int TableIndex,
                       size_t n, double* out9, bool* ok);
-
-/* GetHorizontalDistanceToIntersectionPoint_Table (.cc:1305).  The antenna -> table remap reads
- * the caller-owned AntennaDepths / AntennaTableAlreadyMade (.cc:1348-1352), so it is compiled
- * into the caller here; the lookup itself runs in libairice.so. */
-inline bool GetHorizontalDistanceToIntersectionPoint_Table(
-    double SrcHeightASL, double HorizontalDistanceToRx, double RxDepthBelowIceBoundary,
-    double IceLayerHeight, int AntennaNumber, double& opticalPathLengthInIce,
-    double& opticalPathLengthInAir, double& geometricalPathLengthInIce,
-    double& geometricalPathLengthInAir, double& launchAngle,
-    double& horizontalDistanceToIntersectionPoint, double& transmissionCoefficientS,
-    double& transmissionCoefficientP, double& RecievedAngleInIce) {
-  for (int j = 0; j < (int)AntennaTableAlreadyMade.size(); j++) {
-    if (AntennaDepths[AntennaNumber] == AntennaDepths[AntennaTableAlreadyMade[j]]) {
-      AntennaNumber = j;
-    }
-  }
-  return TableLookup(SrcHeightASL, HorizontalDistanceToRx, RxDepthBelowIceBoundary,
-                     IceLayerHeight, AntennaNumber, opticalPathLengthInIce,
-                     opticalPathLengthInAir, geometricalPathLengthInIce,
-                     geometricalPathLengthInAir, launchAngle,
-                     horizontalDistanceToIntersectionPoint, transmissionCoefficientS,
-                     transmissionCoefficientP, RecievedAngleInIce);
-}
 
 }  // namespace MultiRayAirIceRefraction
 

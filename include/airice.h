@@ -41,6 +41,13 @@ extern "C" {
 #define AIRICE_VARIANT_PYWRAPPER 1 /* AirIceRayTracing::        (pi = 4*atan(1), pythonwrapper .h:25) */
 
 /* Per-query solve status bits (GSL 2.x bisection semantics). */
+/* AIRICE_SOLVE_NONFINITE_END: f(lo) or f(hi) is non-finite, so gsl_root_fsolver_set returns before
+ * storing f_lower/f_upper and the reference's next gsl_root_fsolver_iterate reads uninitialised
+ * malloc memory.  The reference's result on such a row is undefined; this
+ * library (and the oracle) model a zero-filled solver state, which is deterministic but NOT what
+ * real GSL returns -- a consumer comparing against GSL must mask these rows (about 0.7 % of the
+ * cfg3 distribution), as the parity tests do.  AIRICE_SOLVE_BAD_BRACKET and
+ * AIRICE_SOLVE_NO_AIR_LAYER rows are undefined in the reference in the same sense. */
 #define AIRICE_SOLVE_NONFINITE_END 1 /* f(lo) or f(hi) non-finite: reference reads uninitialised GSL state */
 #define AIRICE_SOLVE_BAD_BRACKET 2   /* lo > hi: gsl_root_fsolver_set fails */
 #define AIRICE_SOLVE_STALE_MID 4     /* a bisection midpoint gave non-finite f: root frozen */
@@ -85,6 +92,10 @@ typedef struct airice_grid {
   double depth_m;        /* AntennaDepth, m (negative = in ice) */
   double ice_m;          /* IceLayerHeight, m */
   int32_t in_ice;        /* AntennaDepth < 0 */
+  int32_t table_rows;    /* rows the table holds: the reference skips every row whose Tx height
+                            start_height - height_step*row is not > 0 (.cc:2082), a suffix of the
+                            height_steps rows, so the table is table_rows x angle_steps entries
+                            (height_steps itself stays TotalHeightSteps, which the lookup reads) */
 } airice_grid;
 
 #define AIRICE_TABLE_COLUMNS 11 /* float columns of AllTableAllAntData (.cc:2101-2111) */
@@ -110,7 +121,8 @@ double airice_nz_ice(const airice_medium *m, double z);
 int airice_grid_init(airice_grid *g, double antenna_depth_cm, double ice_height_cm,
                      double height_step_m, double start_angle_deg, double stop_angle_deg,
                      double angle_step_deg);
-/* Trace rows [row_begin, row_begin+row_count) x all angles of the grid.
+/* Trace rows [row_begin, row_begin+row_count) x all angles of the grid (rows at or past
+ * table_rows are skipped, as the reference skips Tx heights <= 0).
  * d_table: 11 float columns, column c of ray r at d_table[c*ld + r - row_begin*angle_steps]
  * (the AllTableAllAntData[ant][c][r] layout).  d_full (nullable): 18 double columns,
  * same indexing (GetRayTracingSolutions dummy[] for parity checks). */
@@ -264,7 +276,24 @@ void Py_TraceIceToAir(double AntennaDepth, double IceLayerHeight, double AirTxHe
                                          IncidentAngleonAntenna, t_ice ns, THD, t ns,
                                          status (AIRICE_SOLVE_* bits), Brent iterations,
                                          probe steps, filled air layers} */
-/* Outputs written for op (4 x max_layers + 1 for AIR_PROPAGATION), or -1 for an unknown op. */
+/* MultiRayAirIceRefraction:: forms of the same layer (MultiRayAirIceRefraction.cc:377-917, the
+ * MultiRayAirIceRefraction.h drop-in): 5-wide outputs {THD, ReceiveAngle deg, L, time s,
+ * geometric path}.  fDnfR, ftimeD and GetRayPropagationTime are the AIRICE_RTF_ ops above
+ * (identical expressions), GetRayHorizontalPath is AIRICE_RTF_OPTICAL_PATH. */
+#define AIRICE_MR_FPATHD 9            /* fpathD (.cc:434-447) args {x, a, b, c, speedc, l} */
+#define AIRICE_MR_GEOMETRIC_PATH 10   /* GetRayGeometricPath (.cc:494-513)
+                                         args {A, RxDepth, TxDepth, Lvalue, AirOrIce} */
+#define AIRICE_MR_HIT_POINT 11        /* GetLayerHitPointPar (.cc:521-646)
+                                         args {n_layer1, RxDepth, TxDepth, IncidentAng, AirOrIce} */
+#define AIRICE_MR_AIR_PROPAGATION 12  /* GetAirPropagationPar (.cc:661-804) args {LaunchAngle,
+                                         AirTxHeight, IceLayerHeight} -> 5 x MaxLayers + 2,
+                                         filled-layer count at [5*MaxLayers+1] */
+#define AIRICE_MR_ICE_PROPAGATION 13  /* GetIcePropagationPar (.cc:807-869) args {IncidentAngleonIce,
+                                         IceLayerHeight, AntennaDepth, Lvalue} -> 5 */
+#define AIRICE_MR_MIN_LAUNCH 14       /* MinimizeforLaunchAngle (.cc:873-917) args {x, airtxheight,
+                                         icelayerheight, antennadepth, horizontaldistance} */
+/* Outputs written for op (4 x max_layers + 1 for AIR_PROPAGATION, 5 x max_layers + 2 for
+ * MR_AIR_PROPAGATION), or -1 for an unknown op. */
 int airice_rtf_outputs(int op, int max_layers);
 int airice_rtf_eval(const airice_medium *m, int op, const double *args, size_t n_args,
                     double *out, size_t n_out);

@@ -69,7 +69,12 @@ class Grid(ctypes.Structure):
         ("depth_m", ctypes.c_double),
         ("ice_m", ctypes.c_double),
         ("in_ice", ctypes.c_int),
+        ("table_rows", ctypes.c_int),
     ]
+
+    @property
+    def n_rays(self) -> int:
+        return int(self.table_rows) * int(self.angle_steps)
 
 
 def build() -> str:
@@ -169,6 +174,9 @@ def grid_init(depth_cm, ice_cm, height_step=10.0, start_angle=90.1, stop_angle=1
 
 
 def table_rows(m: Medium, g: Grid, row0: int, row1: int, full: bool = False, nthreads: int = 0):
+    """Rays of rows [row0, row1) clipped to the table's rows (g.table_rows: the reference skips
+    Tx heights <= 0, .cc:2082), so the arrays are as long as the reference's table slice."""
+    row1 = max(row0, min(row1, int(g.table_rows)))
     n = (row1 - row0) * g.angle_steps
     table = np.zeros((11, n), dtype=np.float32)
     fullarr = np.zeros((18, n), dtype=np.float64) if full else None
@@ -358,3 +366,31 @@ def rtf_eval(m: Medium, op: int, args) -> np.ndarray:
     if n < 0:
         raise ValueError(f"unknown op {op}")
     return out[:n].copy()
+
+
+def lookup_closest_txh(t: LookupTable, P: float):
+    """FindClosestAirTxHeight (.cc:1033-1126): ((s1, e1, s2, e2), (c1, c2), flags)."""
+    idx = (ctypes.c_long * 4)()
+    c = (ctypes.c_double * 2)()
+    fl = ctypes.c_int(0)
+    lib().or_lookup_closest_txh(ctypes.byref(t), ctypes.c_double(P), idx, c, ctypes.byref(fl))
+    return tuple(idx), tuple(c), fl.value
+
+
+def lookup_closest_thd(t: LookupTable, P: float, s: int, e: int):
+    """FindClosestTHD (.cc:1128-1169): ((start, end), closest, flags)."""
+    idx = (ctypes.c_long * 2)()
+    c = ctypes.c_double(0)
+    fl = ctypes.c_int(0)
+    lib().or_lookup_closest_thd(ctypes.byref(t), ctypes.c_double(P), ctypes.c_long(s),
+                                ctypes.c_long(e), idx, ctypes.byref(c), ctypes.byref(fl))
+    return tuple(idx), c.value, fl.value
+
+
+def lookup_par_values(t: LookupTable, H: float, D: float):
+    """GetParValues (.cc:1172-1302): (H1, Par1[10], H2, Par2[10], flags)."""
+    out = np.zeros(22)
+    fl = ctypes.c_int(0)
+    lib().or_lookup_par_values(ctypes.byref(t), ctypes.c_double(H), ctypes.c_double(D), _ptr(out),
+                               ctypes.byref(fl))
+    return out[0], out[1:11].copy(), out[11], out[12:22].copy(), fl.value

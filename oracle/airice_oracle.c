@@ -463,6 +463,11 @@ void or_grid_init(or_grid *g, double depth_cm, double ice_cm, double height_step
   g->stop_angle = stop_angle;
   g->angle_step = angle_step;
   g->angle_steps = (int)floor((stop_angle - start_angle) / angle_step) + 1;
+  /* .cc:2081-2082: rows whose unforced AirTxHeight is not > 0 push nothing, and heights fall
+     with the row index, so the table holds the leading rows only */
+  g->table_rows = g->height_steps;
+  while (g->table_rows > 0 && !(g->start_height - g->height_step * (g->table_rows - 1) > 0))
+    g->table_rows--;
 }
 
 /* Table columns (.cc:2101-2111): dummy indices */
@@ -617,6 +622,29 @@ int or_rtf_eval(const or_medium *m, int op, const double *a, double *out) {
     case 8: /* AIR2ICE: the Air2IceRayTracing CLI solve */
       or_rtf_air2ice(m, a[0], a[1], a[2], a[3], out);
       return 16;
+    /* MultiRayAirIceRefraction:: forms (AIRICE_MR_*): the restatements above, 5-wide */
+    case 9: /* MR_FPATHD (x, a, b, c, speedc, l) */
+      out[0] = fpathD(a[0], a[1], a[2], a[3], a[5]);
+      return 1;
+    case 10: /* MR_GEOMETRIC_PATH */
+      out[0] = GetRayGeometricPath(m, a[0], a[1], a[2], a[3], (int)a[4]);
+      return 1;
+    case 11: /* MR_HIT_POINT */
+      or_layer_hit_point_par(m, a[0], a[1], a[2], a[3], (int)a[4], out);
+      return 5;
+    case 12: { /* MR_AIR_PROPAGATION */
+      for (int j = 0; j < 5 * m->max_layers + 2; j++) out[j] = 0;
+      air_propagation(m, a[0], a[1], a[2], out);
+      return 5 * m->max_layers + 2;
+    }
+    case 13: /* MR_ICE_PROPAGATION */
+      ice_propagation(m, a[1], a[2], a[3], out);
+      return 5;
+    case 14: { /* MR_MIN_LAUNCH */
+      minp p = {a[1], a[2], a[3], a[4]};
+      out[0] = MinimizeforLaunchAngle(m, a[0], &p);
+      return 1;
+    }
     default:
       return -1;
   }
@@ -1134,6 +1162,22 @@ static void lk_par_values(const or_lookup_table *t, double H, double D, double *
     *H2 = *H1;
     for (int ip = 0; ip < 10; ip++) Par2[ip] = Par1[ip];
   }
+}
+
+/* The table walks above, exported for the tests of the C++ drop-in's FindClosestAirTxHeight /
+ * FindClosestTHD / GetParValues (test infrastructure, like everything here). */
+void or_lookup_closest_txh(const or_lookup_table *t, double P, long out_idx[4], double out_c[2],
+                           int *flags) {
+  lk_closest_txh(t, P, &out_idx[0], &out_idx[1], &out_c[0], &out_idx[2], &out_idx[3], &out_c[1],
+                 flags);
+}
+void or_lookup_closest_thd(const or_lookup_table *t, double P, long s, long e, long out_idx[2],
+                           double *c, int *flags) {
+  lk_closest_thd(t, P, s, e, &out_idx[0], &out_idx[1], c, flags);
+}
+void or_lookup_par_values(const or_lookup_table *t, double H, double D, double out[22],
+                          int *flags) {
+  lk_par_values(t, H, D, &out[0], out + 1, &out[11], out + 12, flags);
 }
 
 /* GetHorizontalDistanceToIntersectionPoint_Table (.cc:1305-1462); AntennaNumber already

@@ -86,6 +86,7 @@ typedef struct or_grid {
   int    angle_steps;
   double depth_m, ice_m;
   int    in_ice;
+  int    table_rows;   /* rows with Tx height > 0 (.cc:2082): the table is this prefix */
 } or_grid;
 void or_grid_init(or_grid *g, double depth_cm, double ice_cm, double height_step,
                   double start_angle, double stop_angle, double angle_step);

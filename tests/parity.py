@@ -74,24 +74,65 @@ def float_ulp_diff(gpu: np.ndarray, ref: np.ndarray) -> int:
     return int(d.max()) if d.size else 0
 
 
+_MT_N, _MT_M = 312, 156
+
+
+def _mt19937_64_raw(seed: int, count: int) -> np.ndarray:
+    """``count`` outputs of std::mt19937_64(seed) (C++ [rand.predef]; the 10000th output of the
+    default seed 5489 is 9981545732273789042, checked in tests/test_oracle.py), vectorised over
+    the 312-word state: each twist is three slices (the recurrence reads words 1 and 156 ahead)."""
+    u64 = np.uint64
+    a, um, lm = u64(0xB5026F5AA96619E9), u64(0xFFFFFFFF80000000), u64(0x7FFFFFFF)
+    one, zero = u64(1), u64(0)
+    x = int(seed) & (2**64 - 1)
+    st = [x]
+    for i in range(1, _MT_N):
+        x = (6364136223846793005 * (x ^ (x >> 62)) + i) & (2**64 - 1)
+        st.append(x)
+    mt = np.array(st, dtype=np.uint64)
+    n, m = _MT_N, _MT_M
+    blocks = -(-count // n)
+    out = np.empty(blocks * n, dtype=np.uint64)
+    for b in range(blocks):
+        y = (mt[0:n - m] & um) | (mt[1:n - m + 1] & lm)
+        mt[0:n - m] = mt[m:n] ^ (y >> one) ^ np.where((y & one) != 0, a, zero)
+        y = (mt[n - m:n - 1] & um) | (mt[n - m + 1:n] & lm)
+        mt[n - m:n - 1] = mt[0:m - 1] ^ (y >> one) ^ np.where((y & one) != 0, a, zero)
+        y = (mt[n - 1] & um) | (mt[0] & lm)
+        mt[n - 1] = mt[m - 1] ^ (y >> one) ^ (a if (y & one) else zero)
+        out[b * n:(b + 1) * n] = mt
+    y = out[:count]
+    y = y ^ ((y >> u64(29)) & u64(0x5555555555555555))
+    y = y ^ ((y << u64(17)) & u64(0x71D67FFFEDA60000))
+    y = y ^ ((y << u64(37)) & u64(0xFFF7EEE000000000))
+    return y ^ (y >> u64(43))
+
+
+def mt19937_64_uniform(seed: int, n: int, bounds) -> list[np.ndarray]:
+    """Rows i = 0..n-1 of ``std::uniform_real_distribution<double>(lo, hi)`` draws from one
+    std::mt19937_64(seed), one draw per (lo, hi) in ``bounds`` per row, in order -- the C++ loop
+    ``for i: for (lo, hi): v = dist(lo, hi)(g)`` under libstdc++ (generate_canonical<double, 53>
+    takes one 64-bit draw: u = double(x) / 2^64, 1 -> nextafter(1, 0); v = u * (hi - lo) + lo).
+    Golden rows from g++ in tests/golden/mt19937_64_golden.json."""
+    k = len(bounds)
+    u = _mt19937_64_raw(seed, n * k).astype(np.float64) / 18446744073709551616.0
+    u = np.where(u >= 1.0, np.nextafter(1.0, 0.0), u).reshape(n, k)
+    return [u[:, j] * (hi - lo) + lo for j, (lo, hi) in enumerate(bounds)]
+
+
 def cfg3_queries(n: int, seed: int = 12345):
     """BASELINE cfg3: TxH~U(3001,1e5) m, D~U(0,5e4) m, depth~-U(0,300) m, ice 3000 m
-    (SURVEY.md §8(d)); mt19937_64 stream is replaced by numpy's PCG64 with the stated seed."""
-    rng = np.random.default_rng(seed)
-    txh = rng.uniform(3001.0, 100000.0, n)
-    dist = rng.uniform(0.0, 50000.0, n)
-    depth = -rng.uniform(0.0, 300.0, n)
-    return txh, dist, depth
+    (SURVEY.md §8(d)), from std::mt19937_64(seed): per query TxH, D, then depth."""
+    txh, dist, d = mt19937_64_uniform(seed, n, [(3001.0, 100000.0), (0.0, 50000.0), (0.0, 300.0)])
+    return txh, dist, -d
 
 
 def cfg5_queries(n: int, seed: int = 777):
-    """BASELINE cfg5 (Py_TraceIceToAir): depth~-U(1,300), TxH~U(3001,20000), D~U(0,30000)."""
-    rng = np.random.default_rng(seed)
-    depth = -rng.uniform(1.0, 300.0, n)
-    txh = rng.uniform(3001.0, 20000.0, n)
-    dist = rng.uniform(0.0, 30000.0, n)
+    """BASELINE cfg5 (Py_TraceIceToAir): depth~-U(1,300), TxH~U(3001,20000), D~U(0,30000), from
+    std::mt19937_64(seed): per query depth, TxH, then D."""
+    d, txh, dist = mt19937_64_uniform(seed, n, [(1.0, 300.0), (3001.0, 20000.0), (0.0, 30000.0)])
     ice = np.full(n, 3000.0)
-    return depth, ice, txh, dist
+    return -d, ice, txh, dist
 
 
 def lookup_queries(table: np.ndarray, n: int, seed: int = 4242, max_dist: float = 60000.0):

@@ -81,8 +81,32 @@ def test_grid_init_matches_oracle(args):
     g = make_grid(*args)
     og = oracle.grid_init(*args)
     for f in ("start_height", "stop_height", "height_step", "height_steps", "start_angle",
-              "stop_angle", "angle_step", "angle_steps", "depth_m", "ice_m", "in_ice"):
+              "stop_angle", "angle_step", "angle_steps", "depth_m", "ice_m", "in_ice",
+              "table_rows"):
         assert getattr(g, f) == getattr(og, f), f
+
+
+@pytest.mark.parametrize("depth_cm,ice_cm,step,rows,kept", [
+    (-20000.0, 300000.0, 20.0, 4851, 4851),  # cfg2: every Tx height > 0
+    (-20000.0, 0.0, 20.0, 5001, 5000),       # sea-level ice: the Tx = 0 row is skipped
+    (+5000.0, 0.0, 10.0, 9996, 9996),        # Rx 50 m in the air above sea-level ice: stop 50 m
+    (-100.0, -150000.0, 1000.0, 102, 100),   # ice 1.5 km below sea level: Tx 0 and -1000 skipped
+    (-100.0, -100.0, 3.0, 33334, 33334),     # last row kept (unforced Tx 1 m) and forced to -1 m
+])
+def test_grid_skips_nonpositive_tx_rows(depth_cm, ice_cm, step, rows, kept):
+    """MakeRayTracingTable pushes no entries for rows whose Tx height is not > 0 (.cc:2082):
+    the table holds the leading table_rows rows while TotalHeightSteps keeps its value."""
+    from airiceraytracing_amd import make_grid
+    g = make_grid(depth_cm, ice_cm, step, 92.0, 180.0, 0.5)
+    og = oracle.grid_init(depth_cm, ice_cm, step, 92.0, 180.0, 0.5)
+    assert (g.height_steps, g.table_rows) == (rows, kept)
+    assert (og.height_steps, og.table_rows) == (rows, kept)
+    assert g.n_rays == og.n_rays == kept * g.angle_steps
+    # the oracle's table is the reference's shorter table
+    m = oracle.load_atmosphere(os.path.join(ROOT, "airiceraytracing_amd", "data",
+                                            "Atmosphere.dat.gz"))
+    t = oracle.table_rows(m, og, max(0, rows - 3), rows)
+    assert t.shape == (11, max(0, kept - max(0, rows - 3)) * og.angle_steps)
 
 
 def test_error_codes():
@@ -123,3 +147,65 @@ def test_product_does_not_import_oracle():
             if f.endswith((".py", ".cpp", ".hip", ".hpp", ".h")):
                 src = open(os.path.join(dirpath, f)).read()
                 assert "import oracle" not in src and "airice_oracle" not in src, f
+
+
+# The MultiRayAirIceRefraction.h surface of the reference (its .h:26-204), as demangled
+# signatures: every function a caller of the reference can link against, bar the GSL-typed
+# FindFunctionRoot and the deprecated MakeTable / GetInterpolatedValue (.cc:1618-1794).
+MULTIRAY_FUNCTIONS = [
+    "readATMpar()", "readnhFromFile()", "GetB_ice(double)", "GetC_ice(double)",
+    "Getnz_ice(double)", "FillInAirRefractiveIndex()", "GetB_air(double)", "GetC_air(double)",
+    "Getnz_air(double)", "Refl_S(double, double)", "Trans_S(double, double)",
+    "Refl_P(double, double)", "Trans_P(double, double)", "fDnfR(double, void*)",
+    "ftimeD(double, void*)", "fpathD(double, void*)",
+    "GetRayHorizontalPath(double, double, double, double, int)",
+    "GetRayPropagationTime(double, double, double, double, int)",
+    "GetRayGeometricPath(double, double, double, double, int)",
+    "GetLayerHitPointPar(double, double, double, double, int)", "MakeAtmosphere()",
+    "GetAirPropagationPar(double, double, double)",
+    "GetIcePropagationPar(double, double, double, double)",
+    "MinimizeforLaunchAngle(double, void*)",
+    "GetHorizontalDistanceToIntersectionPoint(double, double, double, double, double&, double&, "
+    "double&, double&, double&, double&, double&, double&, double&)",
+    "oneDLinearInterpolation(double, double, double, double, double)",
+    "Extrapolate(int, int, double, int)", "FindExtrapolationLimit(int, double, int)",
+    "FindClosestAirTxHeight(double, int&, int&, double&, int&, int&, double&, int)",
+    "FindClosestTHD(double, int, int, int&, int&, double&, int)",
+    "GetParValues(double, double, double, double, double&, double*, double&, double*)",
+    "GetHorizontalDistanceToIntersectionPoint_Table(double, double, double, double, int, double&, "
+    "double&, double&, double&, double&, double&, double&, double&, double&)",
+    "Air2IceRayTracing(double, double, double, double, double, double*)",
+    "GetRayTracingSolutions(double, double, double, double, double*, bool&)",
+    "MakeRayTracingTable(double, double, int)",
+]
+MULTIRAY_DATA = ["nh_data", "lognh_data", "h_data", "GridPositionH", "GridPositionTh",
+                 "GridZValue", "GridStartTh", "GridStopTh", "GridStepSizeH_O", "GridStepSizeTh_O",
+                 "GridWidthH", "GridWidthTh", "GridPoints", "TotalStepsH_O", "TotalStepsTh_O",
+                 "GridStartH", "GridStopH", "ATMLAY", "abc", "C_air", "B_air", "A_ice", "B_ice",
+                 "C_ice", "MaxLayers"]
+GLOBAL_DATA = ["MaxAirTxHeight", "MinAirTxHeight", "AllTableAllAntData", "AngleStepSize",
+               "LoopStartAngle", "LoopStopAngle", "TotalAngleSteps", "HeightStepSize",
+               "LoopStartHeight", "LoopStopHeight", "TotalHeightSteps"]
+
+
+def test_multiray_dropin_exports_the_reference_surface():
+    """nm -D of libairice.so holds every function and namespace variable of the reference's
+    MultiRayAirIceRefraction.h under its mangled name; the caller-owned AntennaDepths /
+    AntennaTableAlreadyMade are weak references (the library loads without them)."""
+    from airiceraytracing_amd import _lib
+    out = subprocess.run(["nm", "-DC", _lib.LIB_PATH], capture_output=True, text=True,
+                         check=True).stdout
+    defined, weak = set(), set()
+    for ln in out.splitlines():
+        parts = ln.split(None, 2)
+        if len(parts) == 3 and parts[1] in "TDBR":
+            defined.add(parts[2].strip())
+        elif len(parts) == 2 and parts[0] == "w":
+            weak.add(parts[1].strip())
+    ns = "MultiRayAirIceRefraction::"
+    missing = [f for f in MULTIRAY_FUNCTIONS if ns + f not in defined]
+    assert not missing, missing
+    assert any(s.startswith(ns + "flatten(std::vector<std::vector<double") for s in defined)
+    assert not [v for v in MULTIRAY_DATA if ns + v not in defined]
+    assert not [v for v in GLOBAL_DATA if v not in defined]
+    assert {"AntennaDepths", "AntennaTableAlreadyMade"} <= weak

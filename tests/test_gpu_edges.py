@@ -54,6 +54,26 @@ def test_degenerate_and_ragged_grids(solver, oracle_medium, depth_cm, hstep, a0,
     assert parity.float_ulp_diff(table, ot) <= 1
 
 
+@pytest.mark.parametrize("depth_cm,ice_cm,hstep", [
+    (-20000.0, 0.0, 500.0),      # sea-level ice: the Tx = 0 row is skipped (.cc:2082)
+    (+5000.0, 0.0, 500.0),       # Rx in the air over sea-level ice
+    (-100.0, -150000.0, 1000.0),  # ice below sea level: two rows skipped
+    (-100.0, -100.0, 3.0),       # last row kept, forced to Tx = -1 m
+])
+def test_tables_skip_nonpositive_tx_rows(solver, oracle_medium, depth_cm, ice_cm, hstep):
+    from airiceraytracing_amd import make_grid
+    g = make_grid(depth_cm, ice_cm, hstep, 92.0, 180.0, 0.5)
+    og = oracle.grid_init(depth_cm, ice_cm, hstep, 92.0, 180.0, 0.5)
+    assert g.table_rows == og.table_rows
+    r0 = max(0, g.table_rows - 40)  # the rows next to the skipped ones (and the forced last row)
+    table, full = solver.table_host(g, row_begin=r0, full=True)
+    ot, of = oracle.table_rows(oracle_medium, og, r0, og.height_steps, full=True, nthreads=16)
+    assert table.shape == ot.shape
+    rep = parity.compare_columns(full, of, parity.RAY_FLOORS)
+    assert rep["ok"], rep
+    assert parity.float_ulp_diff(table, ot) <= 1
+
+
 def test_single_query_batches(solver, oracle_medium):
     """n = 1 through the batched minimizer (one lane in a 1024-query sort block)."""
     for txh, dist, depth in ((5000.0, 1000.0, -200.0), (99999.0, 49999.0, -300.0),

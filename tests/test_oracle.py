@@ -207,3 +207,19 @@ def test_cfg3_statistics(oracle_medium):
     assert unpinned.mean() < 0.02
     ok = np.abs(out[1] - dist) < 1
     assert ok.mean() > 0.97
+
+
+def test_mt19937_64_known_answer_and_libstdcxx_golden():
+    """The cfg3/cfg5 generators are std::mt19937_64 + std::uniform_real_distribution (BASELINE.md
+    §3): the C++ standard's known answer, then rows printed by g++ (tests/golden/make_mt_golden.cpp)."""
+    import json
+    from tests import parity
+    assert int(parity._mt19937_64_raw(5489, 10000)[-1]) == 9981545732273789042
+    with open(os.path.join(os.path.dirname(__file__), "golden", "mt19937_64_golden.json")) as f:
+        gold = json.load(f)
+    g3 = np.array(gold["cfg3_seed12345"])
+    np.testing.assert_array_equal(np.stack(parity.cfg3_queries(len(g3)), axis=1), g3)
+    g5 = np.array(gold["cfg5_seed777"])
+    d, ice, txh, dist = parity.cfg5_queries(len(g5))
+    np.testing.assert_array_equal(np.stack([d, txh, dist], axis=1), g5)
+    assert np.all(ice == 3000.0)
