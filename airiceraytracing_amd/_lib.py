@@ -128,6 +128,7 @@ RTF_ICE_PROPAGATION, RTF_FDNFR, RTF_FTIMED, RTF_MIN_LAUNCH = 4, 5, 6, 7
 EXPORTED_SYMBOLS = (
     "airice_last_error", "airice_version", "airice_atmosphere_load", "airice_atmosphere_parse",
     "airice_nz_air", "airice_nz_ice", "airice_grid_init", "airice_table_launch",
+    "airice_table_launch_multi",
     "airice_table_host", "airice_rays_launch", "airice_solve_launch", "airice_solve_host",
     "airice_hdtip_launch", "airice_table_lookup_launch", "airice_lookup_pack", "airice_single_ray_plan",
     "airice_single_ray_launch", "airice_single_ray_host", "airice_trace_ice_to_air_launch",
@@ -181,6 +182,7 @@ def lib() -> ctypes.CDLL:
         "airice_grid_init": ([G, D, D, D, D, D, D], I),
         "airice_table_launch": ([M, G, ctypes.c_int32, ctypes.c_int32, P, P, S, P], I),
         "airice_table_host": ([M, G, ctypes.c_int32, ctypes.c_int32, P, P, S], I),
+        "airice_table_launch_multi": ([M, G, ctypes.c_int32, P, P, P], I),
         "airice_rays_launch": ([M, P, P, D, D, ctypes.c_int32, S, P, S, P], I),
         "airice_solve_launch": ([M, I, D, P, P, P, P, S, P, S, P, P], I),
         "airice_solve_host": ([M, I, D, P, P, P, P, S, P, S, P], I),

@@ -21,6 +21,7 @@
 #include <cstdio>
 #include <algorithm>
 #include <cstdlib>
+#include <cstring>
 #include <mutex>
 #include <vector>
 
@@ -378,27 +379,26 @@ __device__ __forceinline__ void table_ray(const DevMedium& M, const IceConsts& I
 // (Persistent grid-stride and atomic-chunk schedules were measured and rejected: the loop around
 // the inlined ray body raises register pressure to 160 VGPRs, or 330 B/lane of scratch when capped
 // at 64, and runs 2.7x / 7x slower; the R copies here are straight-line code.)
-template <int BS, int R, bool TRACE = false>
-// waves_per_eu(8) at R = 1: 64 VGPRs (12 B/lane spilled) at 8 waves/SIMD measured on par or
-// slightly ahead of 67 VGPRs at 7 (bench 42.0 vs 42.9 us for cfg2).  R = 2 needs <= 7 waves/SIMD.
-__global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(R == 1 ? AIRICE_TABLE_WAVES : AIRICE_TABLE_WAVES2, R == 1 ? AIRICE_TABLE_WAVES : AIRICE_TABLE_WAVES2))) void table_kernel(
-                                                   DevMedium M, IceConsts I, TableArgs G,
-                                                   float* __restrict__ table,
-                                                   double* __restrict__ full,
-                                                   WaveTrace* __restrict__ trace) {
+// The work of one table block (BS rays of one antenna's grid), shared by the single- and the
+// multi-antenna kernels.
+template <int BS, int R, bool TRACE>
+__device__ __forceinline__ void table_block(const DevMedium& M, const IceConsts& I,
+                                            const TableArgs& G, float* __restrict__ table,
+                                            double* __restrict__ full,
+                                            WaveTrace* __restrict__ trace, unsigned block) {
   extern __shared__ __align__(16) unsigned char smem[];
   RowConst* rows = reinterpret_cast<RowConst*>(smem);
-  // the log table (4 KB) staged in LDS: one 16-byte entry per thread
+  // the log table (4 KB) staged in LDS: 16-byte entries, (1 << kLogTableBits) / BS per thread
   __shared__ __align__(16) double s_logtab[1 << kLogTableBits][2];
-  static_assert(BS >= (1 << kLogTableBits), "one table entry per thread");
-  if (threadIdx.x < (1u << kLogTableBits)) {
-    s_logtab[threadIdx.x][0] = kLogTable[threadIdx.x][0];
-    s_logtab[threadIdx.x][1] = kLogTable[threadIdx.x][1];
+#pragma unroll
+  for (unsigned t = threadIdx.x; t < (1u << kLogTableBits); t += BS) {
+    s_logtab[t][0] = kLogTable[t][0];
+    s_logtab[t][1] = kLogTable[t][1];
   }
-  const unsigned wave = blockIdx.x * (BS / 64) + (threadIdx.x >> 6);
+  const unsigned wave = block * (BS / 64) + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   if (TRACE && lane == 0) trace[wave].t0 = __builtin_amdgcn_s_memrealtime();
-  const int k0 = (int)blockIdx.x * BS;
+  const int k0 = (int)block * BS;
   int r0[R];
 #pragma unroll
   for (int j = 0; j < R; ++j) {
@@ -432,6 +432,38 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(R == 1 ? AIR
     trace[wave].hw_id = __builtin_amdgcn_s_getreg((4 << 0) | (0 << 6) | (31 << 11));  // HW_ID
     trace[wave].xcc_id = __builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (31 << 11));
   }
+}
+
+template <int BS, int R, bool TRACE = false>
+// waves_per_eu(8) at R = 1: 64 VGPRs (12 B/lane spilled) at 8 waves/SIMD measured on par or
+// slightly ahead of 67 VGPRs at 7 (bench 42.0 vs 42.9 us for cfg2).  R = 2 needs <= 7 waves/SIMD.
+__global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(R == 1 ? AIRICE_TABLE_WAVES : AIRICE_TABLE_WAVES2, R == 1 ? AIRICE_TABLE_WAVES : AIRICE_TABLE_WAVES2))) void table_kernel(
+                                                   DevMedium M, IceConsts I, TableArgs G,
+                                                   float* __restrict__ table,
+                                                   double* __restrict__ full,
+                                                   WaveTrace* __restrict__ trace) {
+  table_block<BS, R, TRACE>(M, I, G, table, full, trace, blockIdx.x);
+}
+
+// Several antennas' tables in one grid (airice_table_launch_multi): the blocks of antenna a are
+// [begin[a], begin[a+1]); its per-antenna constants (IceConsts, TableArgs: antenna depth, stop
+// height) come from global memory, read with scalar loads since the index is block-uniform.
+// One launch ramp and one drain for all antennas instead of one per table.
+constexpr int kMaxAntennas = 32;
+struct MultiMap {
+  int n_ant;
+  int begin[kMaxAntennas + 1];
+  float* table[kMaxAntennas];
+};
+
+template <int BS>
+__global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(AIRICE_TABLE_WAVES, AIRICE_TABLE_WAVES))) void table_multi_kernel(
+    DevMedium M, const IceConsts* __restrict__ Iv, const TableArgs* __restrict__ Gv, MultiMap map) {
+  int a = 0;
+  for (int j = 1; j < map.n_ant; ++j) a += (int)blockIdx.x >= map.begin[j];
+  a = __builtin_amdgcn_readfirstlane(a);
+  table_block<BS, 1, false>(M, Iv[a], Gv[a], map.table[a], nullptr, nullptr,
+                            blockIdx.x - (unsigned)map.begin[a]);
 }
 
 __global__ __launch_bounds__(kBlock) void rays_kernel(DevMedium M, IceConsts I,
@@ -1600,6 +1632,106 @@ int launch_table(const DevMedium& M, const IceConsts& I, const airice_grid* g, i
       fclose(f);
     }
   }
+  return launch_ok();
+}
+
+// Several antennas' whole tables in one launch of table_multi_kernel.  Ih[a], grids[a]: antenna
+// a's constants and grid (the rows it holds: grids[a].table_rows); tables[a] its output, column
+// stride lds[a].  The per-antenna constants are uploaded to a device buffer that is kept and
+// reused while the same set is launched again (bench steps, repeated builds).
+int launch_table_multi(const DevMedium& M, const IceConsts* Ih, const airice_grid* grids, int n,
+                       float* const* tables, const size_t* lds, hipStream_t st) {
+  if (n <= 0) return AIRICE_OK;
+  if (n > kMaxAntennas) {
+    set_error("at most %d antennas per multi-antenna launch", kMaxAntennas);
+    return AIRICE_EINVAL;
+  }
+  std::vector<TableArgs> Ah(n);
+  MultiMap map;
+  std::memset(&map, 0, sizeof(map));
+  map.n_ant = n;
+  long long blocks = 0;
+  const int rpb = [&] {
+    int r = 2;
+    for (int a = 0; a < n; ++a)
+      r = std::max(r, std::min(kTableBlock, (kTableBlock - 1) / grids[a].angle_steps + 2));
+    return r;
+  }();
+  for (int a = 0; a < n; ++a) {
+    const airice_grid* g = &grids[a];
+    TableArgs& A = Ah[a];
+    std::memset(&A, 0, sizeof(A));
+    A.start_h = g->start_height;
+    A.stop_h = g->stop_height;
+    A.step_h = g->height_step;
+    A.start_a = g->start_angle;
+    A.stop_a = g->stop_angle;
+    A.step_a = g->angle_step;
+    A.hsteps = g->height_steps;
+    A.asteps = g->angle_steps;
+    A.in_ice = g->in_ice;
+    A.ld = lds[a];
+    A.inv_asteps = 1.0 / (double)g->angle_steps;
+    A.rows_per_block = rpb;
+    A.row0 = 0;
+    const long long rays = (long long)g->table_rows * g->angle_steps;
+    if (rays >= (1LL << 31) - 2 * kTableBlock || lds[a] < (size_t)rays) {
+      set_error("antenna %d: %lld rays (ld %zu) do not fit one multi-antenna launch", a, rays,
+                lds[a]);
+      return AIRICE_EINVAL;
+    }
+    A.n = (int)rays;
+    A.half = A.n;
+    map.begin[a] = (int)blocks;
+    map.table[a] = tables[a];
+    blocks += (rays + kTableBlock - 1) / kTableBlock;
+  }
+  map.begin[n] = (int)blocks;
+  if (blocks == 0) return AIRICE_OK;
+  // device copy of the per-antenna constants, reused while unchanged (per device)
+  struct Cache {
+    std::vector<unsigned char> host;
+    void* dev = nullptr;
+    size_t cap = 0;
+  };
+  static std::mutex mu;
+  static std::vector<Cache> caches;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return AIRICE_EHIP;
+  const size_t bytes_i = sizeof(IceConsts) * n, bytes = bytes_i + sizeof(TableArgs) * n;
+  std::vector<unsigned char> packed(bytes);
+  std::memcpy(packed.data(), Ih, bytes_i);
+  std::memcpy(packed.data() + bytes_i, Ah.data(), sizeof(TableArgs) * n);
+  void* dconst = nullptr;
+  {
+    std::lock_guard<std::mutex> lock(mu);
+    if (caches.size() <= (size_t)dev) caches.resize(dev + 1);
+    Cache& c = caches[dev];
+    if (c.host != packed) {
+      if (c.cap < bytes) {
+        if (c.dev != nullptr) (void)hipFree(c.dev);
+        c.dev = nullptr;
+        c.cap = 0;
+        if (hipMalloc(&c.dev, bytes) != hipSuccess) return AIRICE_EHIP;
+        c.cap = bytes;
+      }
+      // ordered before this launch on st; the previous launches reading the old contents have
+      // completed when a synchronous copy returns
+      if (hipStreamSynchronize(st) != hipSuccess ||
+          hipMemcpy(c.dev, packed.data(), bytes, hipMemcpyHostToDevice) != hipSuccess)
+        return AIRICE_EHIP;
+      c.host = packed;
+    }
+    dconst = c.dev;
+  }
+  const size_t lds_bytes = sizeof(RowConst) * (size_t)rpb;
+  ktimer_begin(KT_TABLE, st);
+  hipLaunchKernelGGL(table_multi_kernel<kTableBlock>, dim3((unsigned)blocks), dim3(kTableBlock),
+                     lds_bytes, st, M, static_cast<const IceConsts*>(dconst),
+                     reinterpret_cast<const TableArgs*>(static_cast<unsigned char*>(dconst) +
+                                                        bytes_i),
+                     map);
+  ktimer_end(KT_TABLE, st);
   return launch_ok();
 }
 

@@ -554,6 +554,31 @@ int airice_table_launch(const airice_medium* m, const airice_grid* g, int32_t ro
   return rc;
 }
 
+int airice_table_launch_multi(const airice_medium* m, const airice_grid* grids, int32_t n_grids,
+                              float* const* d_tables, const size_t* lds, void* stream) {
+  if (n_grids < 0 || (n_grids > 0 && (grids == nullptr || d_tables == nullptr || lds == nullptr))) {
+    set_error("null argument");
+    return AIRICE_EINVAL;
+  }
+  if (n_grids == 0) return AIRICE_OK;
+  DevMedium M;
+  int rc = build_dev_medium(m, AIRICE_VARIANT_MULTIRAY, &M);
+  if (rc) return rc;
+  std::vector<IceConsts> I(n_grids);
+  for (int a = 0; a < n_grids; ++a) {
+    const airice_grid& g = grids[a];
+    if (g.angle_steps != grids[0].angle_steps || g.angle_steps < 1 || d_tables[a] == nullptr) {
+      set_error("multi-antenna launch: antenna %d has another angle grid or no table", a);
+      return AIRICE_EINVAL;
+    }
+    build_ice_consts(M, g.stop_height, -g.depth_m, &I[a]);
+  }
+  rc = launch_table_multi(M, I.data(), grids, n_grids, d_tables, lds, (hipStream_t)stream);
+  if (rc && rc != AIRICE_EINVAL)
+    set_error("multi-antenna table launch failed: %s", hipGetErrorString(hipGetLastError()));
+  return rc;
+}
+
 int airice_table_host(const airice_medium* m, const airice_grid* g, int32_t row_begin,
                       int32_t row_count, float* h_table, double* h_full, size_t ld) {
   DevMedium M;

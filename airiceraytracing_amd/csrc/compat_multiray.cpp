@@ -11,6 +11,7 @@
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
+#include <algorithm>
 #include <cstring>
 #include <initializer_list>
 #include <mutex>
@@ -462,6 +463,64 @@ int MakeRayTracingTable(double AntennaDepth, double IceLayerHeight, int AntennaN
     g_tables[index].n = n;
     g_tables[index].fp = table_fingerprint(AllTableAllAntData[index]);
   }
+  return 0;
+}
+
+int MakeRayTracingTables(const std::vector<double>& AntennaDepth, double IceLayerHeight) {
+  const size_t na = AntennaDepth.size();
+  if (na == 0) return 0;
+  MakeAtmosphere();
+  const airice_medium m = medium();
+  std::vector<airice_grid> grids(na);
+  std::vector<float*> dev(na, nullptr);
+  std::vector<size_t> n(na);
+  for (size_t a = 0; a < na; ++a) {
+    airice_grid& g = grids[a];
+    if (airice_grid_init(&g, AntennaDepth[a], IceLayerHeight, HeightStepSize, LoopStartAngle,
+                         LoopStopAngle, AngleStepSize) != AIRICE_OK)
+      die("MakeRayTracingTables grid");
+    g.angle_steps = TotalAngleSteps;  // the global, computed at static init (.cc:15)
+    n[a] = (size_t)g.table_rows * (size_t)g.angle_steps;
+    if (n[a] > 0 && hipMalloc(&dev[a], sizeof(float) * 11 * n[a]) != hipSuccess)
+      die("hipMalloc table");
+  }
+  // antennas whose table is empty (every Tx row skipped) take no part in the launch
+  std::vector<airice_grid> lg;
+  std::vector<float*> lt;
+  std::vector<size_t> ll;
+  for (size_t a = 0; a < na; ++a)
+    if (n[a] > 0) {
+      lg.push_back(grids[a]);
+      lt.push_back(dev[a]);
+      ll.push_back(n[a]);
+    }
+  for (size_t s = 0; s < lg.size(); s += 32) {
+    const int cnt = (int)std::min<size_t>(32, lg.size() - s);
+    if (airice_table_launch_multi(&m, lg.data() + s, cnt, lt.data() + s, ll.data() + s, nullptr) !=
+        AIRICE_OK)
+      die("MakeRayTracingTables");
+  }
+  for (size_t a = 0; a < na; ++a) {
+    std::vector<std::vector<float>> cols(11, std::vector<float>(n[a]));
+    for (int c = 0; c < 11 && n[a] > 0; ++c)
+      if (hipMemcpy(cols[c].data(), dev[a] + (size_t)c * n[a], sizeof(float) * n[a],
+                    hipMemcpyDeviceToHost) != hipSuccess)
+        die("hipMemcpy table");
+    AllTableAllAntData.push_back(std::move(cols));
+    std::lock_guard<std::mutex> lock(g_mu);
+    const size_t index = AllTableAllAntData.size() - 1;
+    if (g_tables.size() <= index) g_tables.resize(index + 1);
+    drop(g_tables[index]);
+    if (n[a] > 0) {
+      g_tables[index].dev = dev[a];
+      g_tables[index].n = n[a];
+      g_tables[index].fp = table_fingerprint(AllTableAllAntData[index]);
+    }
+  }
+  const airice_grid& g = grids[na - 1];
+  LoopStartHeight = g.start_height;
+  LoopStopHeight = g.stop_height;
+  TotalHeightSteps = g.height_steps;
   return 0;
 }
 

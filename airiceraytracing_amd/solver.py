@@ -57,6 +57,17 @@ class AirIceSolver:
                                         row_count, ptr(table), ptr(full), ld,
                                         _stream_handle(stream)), "airice_table_launch")
 
+    def tables_device(self, grids, tables, stream=None) -> None:
+        """Several antennas' whole tables in one launch (airice_table_launch_multi): grids[a] and
+        tables[a] (11 x >= grids[a].n_rays float32 device tensors, one per antenna)."""
+        n = len(grids)
+        garr = (Grid * n)(*grids)
+        ptrs = (ctypes.c_void_p * n)(*[ptr(t).value for t in tables])
+        lds = (ctypes.c_size_t * n)(*[int(t.shape[-1]) for t in tables])
+        check(lib().airice_table_launch_multi(ctypes.byref(self.medium), garr, n, ptrs, lds,
+                                              _stream_handle(stream)),
+              "airice_table_launch_multi")
+
     def table_host(self, grid: Grid, row_begin: int = 0, row_count: int | None = None,
                    full: bool = False):
         if row_count is None:

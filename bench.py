@@ -459,10 +459,25 @@ def main():
                 build_all()
             torch.cuda.synchronize()
             sec = time.perf_counter() - t1
-            multi[f"{n_ant}_antennas"] = {"rays_per_s": rays * reps / sec,
-                                          "ms_per_round": sec / reps * 1e3}
+            # the same tables in ONE launch (airice_table_launch_multi, table_multi_kernel)
+            solver.tables_device(grids, tabs, stream=stream)
+            torch.cuda.synchronize()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
+            for _ in range(reps):
+                solver.tables_device(grids, tabs, stream=stream)
+            e1.record(stream)
+            torch.cuda.synchronize()
+            one_ms = e0.elapsed_time(e1) / reps
+            multi[f"{n_ant}_antennas"] = {
+                "streams_rays_per_s": rays * reps / sec, "streams_ms_per_round": sec / reps * 1e3,
+                "one_launch_rays_per_s": rays / (one_ms * 1e-3), "one_launch_ms": one_ms,
+                "one_launch_vs_single_table": rays / (one_ms * 1e-3) / value if world == 1
+                else None}
         extra["multi_antenna_tables"] = {
-            "metric": "cfg2 tables of several antennas on concurrent HIP streams (rays/s)",
+            "metric": "cfg2 tables of several antennas (MakeRayTracingTable per antenna, "
+                      "RunMultiRayCode.C:29-52): concurrent HIP streams, and one "
+                      "airice_table_launch_multi launch (rays/s)",
             **multi}
     if not args.no_pcie and not sharded:
         # host-buffer callers (AllTableAllAntData is host memory): table build + D2H copy of the

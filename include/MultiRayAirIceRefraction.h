@@ -177,6 +177,11 @@ bool GetHorizontalDistanceToIntersectionPoint_Table(
     double& transmissionCoefficientP, double& RecievedAngleInIce);
 
 /* Extensions (no reference counterpart). */
+/* MakeRayTracingTable for several antennas in ONE GPU launch (airice_table_launch_multi): appends
+ * one table per entry of AntennaDepth (cm, in order) to AllTableAllAntData, exactly as the
+ * reference's per-antenna loop of MakeRayTracingTable calls would (RunMultiRayCode.C:29-52), with
+ * one launch ramp and drain for all of them.  The grid globals are those of the last antenna. */
+int MakeRayTracingTables(const std::vector<double>& AntennaDepth, double IceLayerHeight);
 /* The same lookup on an already-resolved table index (AllTableAllAntData[TableIndex]). */
 bool TableLookup(double SrcHeightASL, double HorizontalDistanceToRx,
                  double RxDepthBelowIceBoundary, double IceLayerHeight, int TableIndex,

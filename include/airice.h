@@ -129,6 +129,13 @@ int airice_grid_init(airice_grid *g, double antenna_depth_cm, double ice_height_
 int airice_table_launch(const airice_medium *m, const airice_grid *g, int32_t row_begin,
                         int32_t row_count, float *d_table, double *d_full, size_t ld,
                         void *stream);
+/* Several antennas' tables in ONE launch (one grid over every antenna's rows; the reference's
+ * per-antenna loop RunMultiRayCode.C:29-52 calls MakeRayTracingTable once per antenna): grids[a]
+ * from airice_grid_init for antenna a (same angle grid for all), d_tables[a] its 11 float columns
+ * with column stride lds[a] >= grids[a].table_rows * angle_steps.  Bit-identical to one
+ * airice_table_launch per antenna; at most 32 antennas. */
+int airice_table_launch_multi(const airice_medium *m, const airice_grid *grids, int32_t n_grids,
+                              float *const *d_tables, const size_t *lds, void *stream);
 int airice_table_host(const airice_medium *m, const airice_grid *g, int32_t row_begin,
                       int32_t row_count, float *h_table, double *h_full, size_t ld);
 

@@ -4,6 +4,7 @@
 // tests/test_gpu_compat.py compares with the oracle.
 #include <cmath>
 #include <cstdio>
+#include <cstring>
 #include <string>
 #include <vector>
 
@@ -109,6 +110,29 @@ int main() {
       M::MakeRayTracingTable(AntennaDepths[i], 3000 * 100., (int)i);
       AntennaTableAlreadyMade.push_back((int)i);
     }
+  }
+  // MakeRayTracingTables (one launch) against the per-antenna tables just made, plus an
+  // antenna in the air made both ways
+  {
+    const size_t before = AllTableAllAntData.size();
+    M::MakeRayTracingTables({-200 * 100., -100 * 100., 50 * 100.}, 3000 * 100.);
+    M::MakeRayTracingTable(50 * 100., 3000 * 100., 3);
+    auto bits_equal = [](const std::vector<std::vector<float>>& x,
+                         const std::vector<std::vector<float>>& y) {  // NaN entries included
+      if (x.size() != y.size()) return 0;
+      for (size_t c = 0; c < x.size(); ++c)
+        if (x[c].size() != y[c].size() ||
+            std::memcmp(x[c].data(), y[c].data(), sizeof(float) * x[c].size()) != 0)
+          return 0;
+      return 1;
+    };
+    const int same[3] = {bits_equal(AllTableAllAntData[before], AllTableAllAntData[0]),
+                         bits_equal(AllTableAllAntData[before + 1], AllTableAllAntData[1]),
+                         bits_equal(AllTableAllAntData[before + 2], AllTableAllAntData[before + 3])};
+    std::printf("\"multi_tables_equal\": [%d, %d, %d],\n", same[0], same[1], same[2]);
+    AllTableAllAntData.resize(before);  // drop them again: the remap below sees tables 0 and 1
+    M::MakeRayTracingTable(-100 * 100., 3000 * 100., 1);  // restores the last-table globals
+    AllTableAllAntData.pop_back();
   }
   std::printf("\"grid\": [%.17g, %.17g, %d, %d],\n", LoopStopHeight, HeightStepSize,
               TotalHeightSteps, TotalAngleSteps);

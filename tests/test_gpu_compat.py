@@ -167,6 +167,8 @@ def test_cpp_inner_api_against_oracle(tmp_path, oracle_medium):
     m2.A_ice = 1.775
     _close(r["a_ice_1775"], [oracle.getnz_ice(m2, -100), oracle.rtf_eval(m2, 13,
                                                                           [30.0, 3000, -200, 0.9])[0]])
+    # MakeRayTracingTables (one launch for three antennas) == one MakeRayTracingTable each
+    assert r["multi_tables_equal"] == [1, 1, 1]
     # table walks on table 0, bit for bit against the oracle's restatement on the same floats
     stop, step, hsteps, asteps = r["grid"]
     og = oracle.grid_init(-20000.0, 300000.0, 2000.0, 92.0, 180.0, 5.0)
