@@ -540,6 +540,29 @@ __device__ __forceinline__ Slim stop_slim(const DevMedium& M, int l) {
   return r;
 }
 
+// Start endpoint of air layer l (scalar reads when l is wave-uniform, as start_slim below).
+__device__ __forceinline__ Endpoint start_endpoint(const DevMedium& M, int l) {
+  const int lu = __builtin_amdgcn_readfirstlane(l);
+  if (__ballot(l != lu) == 0) return M.start[lu];
+  Endpoint r = M.start[0];
+  r = pick(l == 1, M.start[1], r);
+  r = pick(l == 2, M.start[2], r);
+  r = pick(l == 3, M.start[3], r);
+  return r;
+}
+
+// Start end of air layer l: a scalar read when l is the same on every lane of the wave (a batch
+// with one ice height), per-lane selects otherwise.
+__device__ __forceinline__ Slim start_slim(const DevMedium& M, int l) {
+  const int lu = __builtin_amdgcn_readfirstlane(l);
+  if (__ballot(l != lu) == 0) return slim(M.start[lu]);
+  Slim r = slim(M.start[0]);
+  r = pick(l == 1, slim(M.start[1]), r);
+  r = pick(l == 2, slim(M.start[2]), r);
+  r = pick(l == 3, slim(M.start[3]), r);
+  return r;
+}
+
 __device__ __forceinline__ double stop_n(const DevMedium& M, int l) {
   double r = M.stop[0].n;
   r = (l == 1) ? M.stop[1].n : r;
@@ -582,13 +605,26 @@ __device__ __forceinline__ double air_thd(const DevMedium& M, const Query& q, do
   const double L = q.n_rtop * sin_asin(q.ratio * sin_asin(v1));
   L0 = L;
   const RayL RL = ray_L(M.A_air * M.A_air, L);
+  // The reference's layer loop (top -> bot) in three parts with the same summation order: the
+  // Tx layer (both ends per query), the layers strictly between (both ends layer bounds: uniform
+  // across the wave, read as scalars, no per-lane selects; at most layers 2 and 1), the ice layer
+  // (start bound of the lowest layer -> the query's ice endpoint).
   double thd = 0.0;
-#pragma unroll 1
-  for (int il = kMaxLayers - 1; il >= 0; --il) {
-    if (il > q.top || il < q.bot) continue;
-    const Slim T = pick(il == q.top, q.tx, slim(M.start[il]));
-    const Slim R = pick(il == q.top, q.rtop, pick(il == q.bot, q.iceair, slim(M.stop[il])));
-    double x1 = delta_D(T, R, RL, tab);
+  {
+    double x1 = delta_D(q.tx, q.rtop, RL, tab);
+    x1 *= -1;
+    thd += x1;
+  }
+#pragma unroll
+  for (int il = kMaxLayers - 2; il >= 1; --il) {
+    if (il < q.top && il > q.bot) {
+      double x1 = delta_D(slim(M.start[il]), slim(M.stop[il]), RL, tab);
+      x1 *= -1;
+      thd += x1;
+    }
+  }
+  if (q.top > q.bot) {
+    double x1 = delta_D(start_slim(M, q.bot), q.iceair, RL, tab);
     x1 *= -1;
     thd += x1;
   }
@@ -961,14 +997,18 @@ __device__ __forceinline__ Solved evaluate_root(const DevMedium& M, const IceCon
     L0 = P.rtop.n * v2;
     const double A2 = M.A_air * M.A_air;
     const RayL RL = ray_L(A2, L0);
-    for (int il = P.top; il > P.bot - 1; --il) {
-      const Endpoint T = (il == P.top) ? P.tx : M.start[il];
-      const Endpoint R = (il == P.top) ? P.rtop : ((il == P.bot) ? P.iceair : M.stop[il]);
-      const Segment sg = segment(T, R, M.A_air, A2, RL, true, tab);
+    // the layer loop top -> bot as in air_thd: Tx layer, layers strictly between (uniform ends),
+    // ice layer; same summation order
+    auto add = [&](const Segment& sg) {
       S.thd_air += sg.thd;
       S.t_air += sg.t;
       S.geo_air += sg.geo;
-    }
+    };
+    add(segment(P.tx, P.rtop, M.A_air, A2, RL, true, tab));
+#pragma unroll
+    for (int il = kMaxLayers - 2; il >= 1; --il)
+      if (il < P.top && il > P.bot) add(segment(M.start[il], M.stop[il], M.A_air, A2, RL, true, tab));
+    if (P.top > P.bot) add(segment(start_endpoint(M, P.bot), P.iceair, M.A_air, A2, RL, true, tab));
     // receive angle of the last layer: asin(v2) for the first layer, asin(L0/n(Stop)) below
     S.inc = k_asin(P.top == P.bot ? v2 : L0 / P.iceair.n) * M.r2d;
   }

@@ -9,7 +9,7 @@ export TMPDIR=/tmp
 cd /tmp
 C="SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_BRANCH SQ_WAVES"
 C2="SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU_TRANS_F64"
-for mode in fast exact; do
+for mode in ${SPMC_MODES:-fast exact}; do
   for p in a b; do
     [ $p = a ] && ctr="$C" || ctr="$C2"
     if [ $mode = exact ]; then export AIRICE_BISECT_EXACT=1; else unset AIRICE_BISECT_EXACT; fi
