@@ -103,7 +103,7 @@ class LookupTable(ctypes.Structure):
     ]
 
 
-LOOKUP_ENTRY_FLOATS = 12  # AIRICE_LOOKUP_ENTRY_FLOATS
+LOOKUP_ENTRY_FLOATS = 32  # AIRICE_LOOKUP_ENTRY_FLOATS
 
 
 class SingleRayInfo(ctypes.Structure):

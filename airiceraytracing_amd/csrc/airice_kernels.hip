@@ -832,7 +832,9 @@ __device__ __forceinline__ SolveResult solve_root(const DevMedium& M, const IceC
     } else if (phase == PH_BISECT) {
       x = (lo + hi) / 2.0;
     } else if (phase == PH_EST) {
-      x = (est == 0) ? x2 : x2 - f2 * ((x2 - x1) / (f2 - f1));
+      // the secant point only steers the search (the root comes from GSL's bisection replay), so
+      // its quotient takes v_rcp_f64 (~2^-24 relative) instead of the IEEE division
+      x = (est == 0) ? x2 : x2 - f2 * ((x2 - x1) * __builtin_amdgcn_rcp(f2 - f1));
 #if AIRICE_OVERSHOOT
       // near convergence (the step is under a quarter of GSL's final bracket width W and x2 is
       // a guard), aim W/8 past the predicted root: the new point and x2 then straddle the root
@@ -924,7 +926,7 @@ __device__ __forceinline__ SolveResult solve_root(const DevMedium& M, const IceC
       } else if (fabs(f) < tau) {
         // at the root: guards a few tau either side, scaled by the local secant slope; a side
         // whose guard already lies within W/4 of the root needs none
-        dlt = 4.0 * tau * fabs((x2 - x1) / (f2 - f1));
+        dlt = 4.0 * tau * fabs((x2 - x1) * __builtin_amdgcn_rcp(f2 - f1));
         xg = x;
         const double Wq = AIRICE_GUARD_SKIP ? 0.25e-9 * gL : 0.0;
         const bool needL = !(xg - gL <= Wq), needR = !(gR - xg <= Wq);

@@ -7,8 +7,8 @@
 //                                                            valid-THD span of that row,
 //                    FindClosestTHD         (.cc:1128-1169)  8 bisection steps + linear scan,
 //                    GetParValues           (.cc:1172-1302)  10 columns at 2 heights
-//                                                            (one 48-byte packed record per
-//                                                            entry when the table is packed),
+//                                                            (one 128-byte packed record per
+//                                                            interpolation pair when packed),
 //                    _Table                 (.cc:1305-1462)  interpolation in height, checks.
 //                  Lanes that hit the one-sided extrapolation case (.cc:1418) are flagged and
 //                  finished by the masked minimizer pass (launch_lookup_fallback,
@@ -54,21 +54,28 @@ __global__ __launch_bounds__(kLkBlock) void lookup_kernel(LkTable T, const doubl
   flags[k] = (uint8_t)fl;
 }
 
-// airice_lookup_pack: one lane per entry; each column read is coalesced across the wave and each
-// wave writes one contiguous 3 KB run of records.
+// airice_lookup_pack: one lane per record (entries i and i + 1); each column read is coalesced
+// across the wave and each wave writes one contiguous 8 KB run of records.
 __global__ __launch_bounds__(kLkBlock) void lookup_pack_kernel(const float* __restrict__ t,
                                                                long long ld, long long n,
                                                                float* __restrict__ e) {
   const long long i = (long long)blockIdx.x * kLkBlock + threadIdx.x;
   if (i >= n) return;
+  const bool last = i + 1 >= n;
   float c[AIRICE_LOOKUP_ENTRY_FLOATS];
 #pragma unroll
-  for (int k = 0; k < 11; ++k) c[k] = t[(long long)k * ld + i];
+  for (int k = 0; k < 11; ++k) {
+    c[k] = t[(long long)k * ld + i];
+    c[12 + k] = last ? __builtin_nanf("") : t[(long long)k * ld + i + 1];
+  }
   c[11] = 0.0f;
+  c[23] = 0.0f;
+#pragma unroll
+  for (int k = 24; k < AIRICE_LOOKUP_ENTRY_FLOATS; ++k) c[k] = 0.0f;
   float4* p = reinterpret_cast<float4*>(e + (long long)AIRICE_LOOKUP_ENTRY_FLOATS * i);
-  p[0] = make_float4(c[0], c[1], c[2], c[3]);
-  p[1] = make_float4(c[4], c[5], c[6], c[7]);
-  p[2] = make_float4(c[8], c[9], c[10], c[11]);
+#pragma unroll
+  for (int q = 0; q < AIRICE_LOOKUP_ENTRY_FLOATS / 4; ++q)
+    p[q] = make_float4(c[4 * q], c[4 * q + 1], c[4 * q + 2], c[4 * q + 3]);
 }
 
 }  // namespace

@@ -145,8 +145,9 @@ class AirIceSolver:
 
     @staticmethod
     def lookup_pack(lt: LookupTable, stream=None):
-        """airice_lookup_pack: a packed copy of the table (12 floats per entry, torch tensor on
-        the table's device) that ``lt`` then reads; the tensor is kept on ``lt``."""
+        """airice_lookup_pack: a packed copy of the table (one 128-byte record per entry, holding
+        it and the next entry; torch tensor on the table's device) that ``lt`` then reads; the
+        tensor is kept on ``lt``."""
         import torch
         packed = torch.empty(int(lt.n_entries) * _lib.LOOKUP_ENTRY_FLOATS, dtype=torch.float32,
                              device=torch.device("cuda", torch.cuda.current_device()))

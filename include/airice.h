@@ -186,13 +186,17 @@ typedef struct airice_lookup_table {
                                  reads the columns only); same values, fewer cache lines */
 } airice_lookup_table;
 
-/* Floats per packed entry: the 11 columns of one table entry, then one 0 (48 B, 16 B aligned). */
-#define AIRICE_LOOKUP_ENTRY_FLOATS 12
+/* Floats per packed record: record i holds the 11 columns of entry i (floats 0-10, float 11 = 0)
+ * and of entry i + 1 (floats 12-22, float 23 = 0; NaN for the last entry), then 8 zeros: 128 B,
+ * one L2 line when the array is 128-byte aligned.  The lookup interpolates between entries i and
+ * i + 1 (FindClosestTHD's index1, index2), so each table row costs it one line. */
+#define AIRICE_LOOKUP_ENTRY_FLOATS 32
 
-/* Pack one antenna's table for the lookup: d_entries[12*i + c] = column c of entry i (c < 11),
- * n_entries * 12 floats, 16-byte aligned.  The lookup reads the 10 interpolated parameters of a
- * table entry from 48 contiguous bytes instead of 10 columns ld floats apart; results are
- * identical.  Stream-ordered; run once per table, then set t->entries = d_entries. */
+/* Pack one antenna's table for the lookup: n_entries records of AIRICE_LOOKUP_ENTRY_FLOATS floats
+ * (above), 16-byte aligned (128-byte for one line per record).  The lookup reads the 10
+ * interpolated parameters of both entries of a pair from one record instead of 10 columns ld
+ * floats apart; results are identical.  Stream-ordered; run once per table, then set
+ * t->entries = d_entries. */
 int airice_lookup_pack(const airice_lookup_table *t, float *d_entries, void *stream);
 
 #define AIRICE_LOOKUP_FALLBACK 1 /* the minimizer fallback ran (.cc:1418-1420) */

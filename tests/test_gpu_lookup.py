@@ -55,7 +55,7 @@ def _run_case(solver, oracle_medium, depth_cm, hstep, a0, a1, astep, nq, seed):
                                stream=torch.cuda.current_stream())
     torch.cuda.synchronize()
     out, ok, fl = out.cpu().numpy(), ok.cpu().numpy(), fl.cpu().numpy()
-    # the packed table (airice_lookup_pack): the same floats from 48-byte records -> identical
+    # the packed table (airice_lookup_pack): the same floats from 128-byte pair records -> identical
     lp = solver.lookup_table(table, g)
     solver.lookup_pack(lp, stream=torch.cuda.current_stream())
     out_p = torch.empty_like(torch.from_numpy(out)).to(dev)
@@ -66,8 +66,10 @@ def _run_case(solver, oracle_medium, depth_cm, hstep, a0, a1, astep, nq, seed):
     torch.cuda.synchronize()
     assert np.array_equal(out_p.cpu().numpy(), out, equal_nan=True)
     assert np.array_equal(ok_p.cpu().numpy(), ok) and np.array_equal(fl_p.cpu().numpy(), fl)
-    packed = lp._packed.cpu().numpy().reshape(-1, 12)
+    packed = lp._packed.cpu().numpy().reshape(-1, 32)  # record i: entries i and i + 1
     assert np.array_equal(packed[:, :11].T, host, equal_nan=True) and not packed[:, 11].any()
+    assert np.array_equal(packed[:-1, 12:23].T, host[:, 1:], equal_nan=True)
+    assert np.isnan(packed[-1, 12:23]).all() and not packed[:, 23:].any()
     rout, rok, rfl = oracle.table_lookup_batch(oracle_medium, oracle.lookup_table(host, og),
                                                src, dist, dep, ICE_CM, nthreads=NTHREADS)
     assert np.array_equal(fl, rfl), np.flatnonzero(fl != rfl)[:10]
