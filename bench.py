@@ -396,9 +396,14 @@ def main():
         solver.lookup_pack(lt, stream=stream)
         torch.cuda.synchronize()
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        # re-pack into the same buffer (the kernel alone; lookup_pack also allocates)
+        import ctypes
+        from airiceraytracing_amd import _lib
+        from airiceraytracing_amd.solver import _stream_handle
         e0.record(stream)
         for _ in range(10):
-            solver.lookup_pack(lt, stream=stream)
+            _lib.check(_lib.lib().airice_lookup_pack(ctypes.byref(lt), _lib.ptr(lt._packed),
+                                                     _stream_handle(stream)), "airice_lookup_pack")
         e1.record(stream)
         torch.cuda.synchronize()
         pack_ms = e0.elapsed_time(e1) / 10
