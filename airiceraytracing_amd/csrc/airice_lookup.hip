@@ -54,8 +54,8 @@ __global__ __launch_bounds__(kLkBlock) void lookup_kernel(LkTable T, const doubl
   flags[k] = (uint8_t)fl;
 }
 
-// airice_lookup_pack: one lane per record (entries i and i + 1); each column read is coalesced
-// across the wave and each wave writes one contiguous 8 KB run of records.
+// airice_lookup_pack: one lane per record (entries i and i + 1, columns 1-10 each); the column
+// reads are coalesced across the wave and each wave writes one contiguous 8 KB run of records.
 __global__ __launch_bounds__(kLkBlock) void lookup_pack_kernel(const float* __restrict__ t,
                                                                long long ld, long long n,
                                                                float* __restrict__ e) {
@@ -64,14 +64,12 @@ __global__ __launch_bounds__(kLkBlock) void lookup_pack_kernel(const float* __re
   const bool last = i + 1 >= n;
   float c[AIRICE_LOOKUP_ENTRY_FLOATS];
 #pragma unroll
-  for (int k = 0; k < 11; ++k) {
-    c[k] = t[(long long)k * ld + i];
-    c[12 + k] = last ? __builtin_nanf("") : t[(long long)k * ld + i + 1];
+  for (int k = 0; k < 10; ++k) {
+    c[k] = t[(long long)(1 + k) * ld + i];
+    c[10 + k] = last ? __builtin_nanf("") : t[(long long)(1 + k) * ld + i + 1];
   }
-  c[11] = 0.0f;
-  c[23] = 0.0f;
 #pragma unroll
-  for (int k = 24; k < AIRICE_LOOKUP_ENTRY_FLOATS; ++k) c[k] = 0.0f;
+  for (int k = 20; k < AIRICE_LOOKUP_ENTRY_FLOATS; ++k) c[k] = 0.0f;
   float4* p = reinterpret_cast<float4*>(e + (long long)AIRICE_LOOKUP_ENTRY_FLOATS * i);
 #pragma unroll
   for (int q = 0; q < AIRICE_LOOKUP_ENTRY_FLOATS / 4; ++q)

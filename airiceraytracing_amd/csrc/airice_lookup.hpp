@@ -30,53 +30,39 @@ struct LkThdBins {
   double c;
 };
 
-// One table entry's 11 columns, from the packed copy when there is one (the first three 16-byte
-// loads of its record) or else column by column.  Out-of-range entries: NaN, flagged, as lk_at.
+// The 10 interpolated parameters of one table entry (columns 1-10: THD first).
 struct LkRec {
-  float c[12];
+  float c[10];
 };
-
-// (Non-temporal loads for the records, to keep the THD column in L2, measured 33 % slower.)
-__host__ __device__ __forceinline__ float4 lk_ld4(const float* p) {
-  return *reinterpret_cast<const float4*>(p);
-}
-
-__host__ __device__ __forceinline__ void lk_unpack(const float* p, LkRec& r) {
-  const float4 a = lk_ld4(p), b = lk_ld4(p + 4), d = lk_ld4(p + 8);
-  r.c[0] = a.x, r.c[1] = a.y, r.c[2] = a.z, r.c[3] = a.w;
-  r.c[4] = b.x, r.c[5] = b.y, r.c[6] = b.z, r.c[7] = b.w;
-  r.c[8] = d.x, r.c[9] = d.y, r.c[10] = d.z, r.c[11] = d.w;
-}
 
 __host__ __device__ __forceinline__ LkRec lk_rec(const LkTable& T, long long i, int& fl) {
   LkRec r;
   if (i < 0 || i >= T.n) {
     fl |= AIRICE_LOOKUP_UNPINNED;
 #pragma unroll
-    for (int c = 0; c < 12; ++c) r.c[c] = __builtin_nanf("");
-    return r;
-  }
-  if (T.e != nullptr) {
-    lk_unpack(T.e + (long long)AIRICE_LOOKUP_ENTRY_FLOATS * i, r);
+    for (int c = 0; c < 10; ++c) r.c[c] = __builtin_nanf("");
     return r;
   }
 #pragma unroll
-  for (int c = 0; c < 11; ++c) r.c[c] = T.col[c][i];
-  r.c[11] = 0.0f;
+  for (int c = 0; c < 10; ++c) r.c[c] = T.col[1 + c][i];
   return r;
 }
 
-// Entries i and i + 1 (an interpolation pair): one 128-byte packed record holds both.
-__host__ __device__ __forceinline__ void lk_rec_pair(const LkTable& T, long long i, LkRec& r0,
-                                                     LkRec& r1, int& fl) {
-  if (T.e != nullptr && i >= 0 && i + 1 < T.n) {
-    const float* p = T.e + (long long)AIRICE_LOOKUP_ENTRY_FLOATS * i;
-    lk_unpack(p, r0);
-    lk_unpack(p + 12, r1);
-    return;
+// Entries i and i + 1 (an interpolation pair) from one 128-byte packed record -- five 16-byte
+// loads of one L2 line -- when there is a packed copy and both entries exist; false otherwise.
+__host__ __device__ __forceinline__ bool lk_pair(const LkTable& T, long long i, LkRec& r0,
+                                                 LkRec& r1) {
+  if (T.e == nullptr || i < 0 || i + 1 >= T.n) return false;
+  const float4* p = reinterpret_cast<const float4*>(T.e + (long long)AIRICE_LOOKUP_ENTRY_FLOATS * i);
+  const float4 a = p[0], b = p[1], c = p[2], d = p[3], e = p[4];
+  const float v[20] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w, c.x, c.y,
+                       c.z, c.w, d.x, d.y, d.z, d.w, e.x, e.y, e.z, e.w};
+#pragma unroll
+  for (int k = 0; k < 10; ++k) {
+    r0.c[k] = v[k];
+    r1.c[k] = v[10 + k];
   }
-  r0 = lk_rec(T, i, fl);
-  r1 = lk_rec(T, i + 1, fl);
+  return true;
 }
 
 __host__ __device__ __forceinline__ double lk_at(const LkTable& T, int c, long long i, int& fl) {
@@ -137,9 +123,14 @@ __host__ __device__ __forceinline__ LkTxhBins lk_closest_txh(const LkTable& T, d
   return b;
 }
 
-// FindClosestTHD (.cc:1128-1169)
+// FindClosestTHD (.cc:1128-1169).  With a packed table the THD values at the final pair come
+// from the pair's record, which also carries the parameters lk_row_params interpolates (have_pair).
+struct LkThdPair {
+  LkRec r1, r2;  // entries index1, index2
+  bool have_pair = false;
+};
 __host__ __device__ __forceinline__ LkThdBins lk_closest_thd(const LkTable& T, double P, long long s, long long e,
-                                            int& fl) {
+                                            int& fl, LkThdPair& pr) {
 #pragma unroll 1
   for (int i = 0; i < 8; ++i) {
     if (e - s >= 3) {
@@ -163,8 +154,9 @@ __host__ __device__ __forceinline__ LkThdBins lk_closest_thd(const LkTable& T, d
     }
   }
   const long long index1 = index2 - 1;
-  const double v2 = lk_at(T, 1, index2, fl);
-  const double v1 = lk_at(T, 1, index1, fl);
+  pr.have_pair = lk_pair(T, index1, pr.r1, pr.r2);
+  const double v2 = pr.have_pair ? (double)pr.r2.c[0] : lk_at(T, 1, index2, fl);
+  const double v1 = pr.have_pair ? (double)pr.r1.c[0] : lk_at(T, 1, index1, fl);
   minimum = fabs(P - v2);
   if (minimum > fabs(P - v1)) minimum = fabs(P - v1);
   return LkThdBins{index1, index2, minimum};
@@ -175,19 +167,22 @@ __host__ __device__ __forceinline__ void lk_row_params(const LkTable& T, double 
                                               double par[10], double* closest, int& fl) {
   const double max_thd = lk_at(T, 1, s, fl);
   if (D <= max_thd) {
-    const LkThdBins b = lk_closest_thd(T, D, s, e, fl);
+    LkThdPair pr;
+    const LkThdBins b = lk_closest_thd(T, D, s, e, fl, pr);
     *closest = b.c;
     if (b.c != 0) {
-      const double x1 = lk_at(T, 1, b.s, fl), x2 = lk_at(T, 1, b.e, fl);
-      LkRec rs, re;  // b.e == b.s + 1 (FindClosestTHD's index1 = index2 - 1)
-      lk_rec_pair(T, b.s, rs, re, fl);
+      // b.e == b.s + 1 (index1 = index2 - 1)
+      const LkRec rs = pr.have_pair ? pr.r1 : lk_rec(T, b.s, fl);
+      const LkRec re = pr.have_pair ? pr.r2 : lk_rec(T, b.e, fl);
+      const double x1 = pr.have_pair ? (double)pr.r1.c[0] : lk_at(T, 1, b.s, fl);
+      const double x2 = pr.have_pair ? (double)pr.r2.c[0] : lk_at(T, 1, b.e, fl);
 #pragma unroll
       for (int ip = 0; ip < 10; ++ip)
-        par[ip] = lk_interp(D, x1, (double)rs.c[1 + ip], x2, (double)re.c[1 + ip]);
+        par[ip] = lk_interp(D, x1, (double)rs.c[ip], x2, (double)re.c[ip]);
     } else {
-      const LkRec r = lk_rec(T, b.s + 1, fl);
+      const LkRec r = pr.have_pair ? pr.r2 : lk_rec(T, b.s + 1, fl);
 #pragma unroll
-      for (int ip = 0; ip < 10; ++ip) par[ip] = (double)r.c[1 + ip];
+      for (int ip = 0; ip < 10; ++ip) par[ip] = (double)r.c[ip];
     }
   } else {
 #pragma unroll

@@ -562,7 +562,8 @@ int FindClosestTHD(double ParValue, int StartIndex, int EndIndex, int& RStartInd
                    int& REndIndex, double& ClosestVal, int AntennaNumber) {
   const airice::LkTable T = host_lk(host_table(AntennaNumber));
   int fl = 0;
-  const airice::LkThdBins b = airice::lk_closest_thd(T, ParValue, StartIndex, EndIndex, fl);
+  airice::LkThdPair pr;  // host tables are not packed: the column path
+  const airice::LkThdBins b = airice::lk_closest_thd(T, ParValue, StartIndex, EndIndex, fl, pr);
   RStartIndex = (int)b.s;
   REndIndex = (int)b.e;
   ClosestVal = b.c;

@@ -186,10 +186,11 @@ typedef struct airice_lookup_table {
                                  reads the columns only); same values, fewer cache lines */
 } airice_lookup_table;
 
-/* Floats per packed record: record i holds the 11 columns of entry i (floats 0-10, float 11 = 0)
- * and of entry i + 1 (floats 12-22, float 23 = 0; NaN for the last entry), then 8 zeros: 128 B,
- * one L2 line when the array is 128-byte aligned.  The lookup interpolates between entries i and
- * i + 1 (FindClosestTHD's index1, index2), so each table row costs it one line. */
+/* Floats per packed record: record i holds columns 1-10 of entry i (floats 0-9) and of entry
+ * i + 1 (floats 10-19; NaN for the last entry), then 12 zeros: 128 B, one L2 line when the array
+ * is 128-byte aligned.  The lookup interpolates between entries i and i + 1 (FindClosestTHD's
+ * index1, index2), so each table row it visits costs it one record line, which also supplies the
+ * THD values at the pair. */
 #define AIRICE_LOOKUP_ENTRY_FLOATS 32
 
 /* Pack one antenna's table for the lookup: n_entries records of AIRICE_LOOKUP_ENTRY_FLOATS floats
