@@ -631,6 +631,49 @@ __device__ __forceinline__ double air_thd(const DevMedium& M, const Query& q, do
   return thd;
 }
 
+// One evaluation of f spread over a wave, for one-query calls (roots_wave_kernel): lanes 0-4 take
+// the Tx layer, layers 2 and 1 (when strictly between), the ice layer and the segment in the ice,
+// each with the same delta_D as air_thd, and the sums are formed in air_thd's order from the
+// lanes' values -- the same bits as the one-lane evaluation, with ~1/4 of its dependent chain.
+// Every lane holds the same query, so everything else stays wave-uniform.
+__device__ __forceinline__ void eval_thd_wave(const DevMedium& M, const IceConsts& I,
+                                              const Query& q, double theta, const double* tab,
+                                              double& thd_air, double& thd_ice) {
+  const int lane = (int)(threadIdx.x & 63);
+  const bool air = q.top >= q.bot;
+  double L = __builtin_nan("");
+  if (air) {
+    const double v1 = sin_start((180 - theta) * M.d2r);
+    L = q.n_rtop * sin_asin(q.ratio * sin_asin(v1));
+  }
+  const bool ice = lane == 4;
+  const RayL RL = ray_L(ice ? M.A_ice * M.A_ice : M.A_air * M.A_air, L);
+  Slim T = q.tx, R = q.rtop;  // lane 0 (and the lanes past 4, whose value is unused)
+  T = pick(lane == 1, slim(M.start[2]), T);
+  R = pick(lane == 1, slim(M.stop[2]), R);
+  T = pick(lane == 2, slim(M.start[1]), T);
+  R = pick(lane == 2, slim(M.stop[1]), R);
+  T = pick(lane == 3, slim(M.start[0]), T);
+  T = pick(lane == 3 && q.bot >= 1, slim(M.start[1]), T);
+  T = pick(lane == 3 && q.bot >= 2, slim(M.start[2]), T);
+  T = pick(lane == 3 && q.bot >= 3, slim(M.start[3]), T);
+  R = pick(lane == 3, q.iceair, R);
+  T = pick(ice, slim(I.ice0), T);
+  R = pick(ice, q.rx, R);
+  const double x = delta_D(T, R, RL, tab);
+  const double d0 = __shfl(x, 0), d1 = __shfl(x, 1), d2 = __shfl(x, 2), d3 = __shfl(x, 3),
+               d4 = __shfl(x, 4);
+  thd_air = 0.0;
+  if (air) {
+    thd_air += -d0;
+    if (2 < q.top && 2 > q.bot) thd_air += -d1;
+    if (1 < q.top && 1 > q.bot) thd_air += -d2;
+    if (q.top > q.bot) thd_air += -d3;
+  }
+  thd_ice = 0;
+  if (q.depth_pos != 0) thd_ice += d4;
+}
+
 // ---------------------------------------------------------------------------
 // Air2IceRayTracing (.cc:1464-1616) in two launches: stage 1 finds the launch angle
 // (bracket, probe, bisection) keeping only the slim per-query state live; stage 2 rebuilds
@@ -674,6 +717,7 @@ struct SolveResult {
 enum { PH_PROBE = 0, PH_FLO = 1, PH_FHI = 2, PH_EST = 3, PH_G1 = 4, PH_G2 = 5, PH_BISECT = 6,
        PH_DONE = 7 };
 
+template <bool WAVE = false>
 __device__ __forceinline__ SolveResult solve_root(const DevMedium& M, const IceConsts& I,
                                                   const Geometry& g, double thR, bool exact,
                                                   const double* tab) {
@@ -855,12 +899,17 @@ __device__ __forceinline__ SolveResult solve_root(const DevMedium& M, const IceC
     // the single evaluation site: MinimizeforLaunchAngle (.cc:873-917)
     ++n_eval;
     n_inside += (phase == PH_BISECT);
-    double L;
-    const double thd_air = air_thd(M, q, x, L, tab);
-    double thd_ice = 0;
-    if (q.depth_pos != 0) {
-      const RayL RL = ray_L(M.A_ice * M.A_ice, L);
-      thd_ice += delta_D(slim(I.ice0), q.rx, RL, tab);
+    double thd_air, thd_ice;
+    if constexpr (WAVE) {
+      eval_thd_wave(M, I, q, x, tab, thd_air, thd_ice);
+    } else {
+      double L;
+      thd_air = air_thd(M, q, x, L, tab);
+      thd_ice = 0;
+      if (q.depth_pos != 0) {
+        const RayL RL = ray_L(M.A_ice * M.A_ice, L);
+        thd_ice += delta_D(slim(I.ice0), q.rx, RL, tab);
+      }
     }
     const double f = (q.dist - (thd_ice + thd_air));
     if (phase == PH_PROBE) {
@@ -1354,6 +1403,27 @@ __global__ __launch_bounds__(kSortedBlock, AIRICE_SORTED_WAVES) void roots_sorte
   park.status[k * park.stride] = (double)r.status;
 }
 
+// One-query root finding (the scalar C++ / ctypes entry points): one wave solves query 0 with the
+// evaluation spread over its lanes (eval_thd_wave); same roots and status bits as roots_kernel.
+template <int IN>
+__global__ __launch_bounds__(64) void roots_wave_kernel(DevMedium M, IceConsts I, QueryArgs Q,
+                                                        Park park) {
+  __shared__ __align__(16) double s_logtab[1 << kLogTableBits][2];
+  for (int t = threadIdx.x; t < (1 << kLogTableBits); t += 64) {
+    s_logtab[t][0] = kLogTable[t][0];
+    s_logtab[t][1] = kLogTable[t][1];
+  }
+  __syncthreads();
+  if (IN == IN_CM100 && !(Q.mask[0] & AIRICE_LOOKUP_FALLBACK)) return;
+  double thR;
+  const Geometry g = load_query<IN>(M, Q, 0, thR);
+  const SolveResult r = solve_root<true>(M, I, g, thR, park.exact != 0, &s_logtab[0][0]);
+  if (threadIdx.x == 0) {
+    park.root[0] = r.root;
+    park.status[0] = (double)r.status;
+  }
+}
+
 __device__ __forceinline__ bool check_solution(double thd, double D) {
   // CheckSolution (.cc:978-983, AirIceRayTracing.cc:916-921)
   bool good = false;
@@ -1372,19 +1442,18 @@ __device__ __forceinline__ void stage_log_table(double (*s)[2]) {
 
 // Stage 2 of Air2IceRayTracing: dummy[0..16] (MultiRay, .cc:1597-1614) or dummy[0..14]
 // (pythonwrapper, AirIceRayTracing.cc:1070-1084), SoA with stride ld.
+// Stage-2 bodies (one query k, parked root in its output slots), shared by the batch out kernels
+// and the one-query fused kernel (scalar_solve_kernel).
 template <int VARIANT>
-__global__ __launch_bounds__(kBlock) void solve_out_kernel(DevMedium M, IceConsts I, QueryArgs Q,
-                                                           double* __restrict__ out, size_t ld,
-                                                           uint8_t* __restrict__ status) {
-  const long long k = (long long)blockIdx.x * kBlock + threadIdx.x;
-  __shared__ __align__(16) double s_logtab[1 << kLogTableBits][2];
-  stage_log_table(s_logtab);
-  if (k >= Q.n) return;
+__device__ __forceinline__ void solve_out_body(const DevMedium& M, const IceConsts& I,
+                                               const QueryArgs& Q, double* __restrict__ out,
+                                               size_t ld, uint8_t* __restrict__ status,
+                                               long long k, const double* tab) {
   double thR;
   const Geometry g = load_query<IN_M>(M, Q, k, thR);
   const double x = out[10 * ld + k];
   const int st = (int)out[0 * ld + k];
-  const Solved S = evaluate_root(M, I, g, x, st, &s_logtab[0][0]);
+  const Solved S = evaluate_root(M, I, g, x, st, tab);
   const double thd = S.thd_ice + S.thd_air;
   const double tt = S.t_ice + S.t_air;
   out[0 * ld + k] = g.H;
@@ -1416,19 +1485,27 @@ __global__ __launch_bounds__(kBlock) void solve_out_kernel(DevMedium M, IceConst
   if (status != nullptr) status[k] = (uint8_t)S.status;
 }
 
-// Stage 2 of GetHorizontalDistanceToIntersectionPoint (.cc:945-989): 9 outputs (cm, rad) + bool.
-__global__ __launch_bounds__(kBlock) void hdtip_out_kernel(DevMedium M, IceConsts I, QueryArgs Q,
+template <int VARIANT>
+__global__ __launch_bounds__(kBlock) void solve_out_kernel(DevMedium M, IceConsts I, QueryArgs Q,
                                                            double* __restrict__ out, size_t ld,
-                                                           uint8_t* __restrict__ ok) {
+                                                           uint8_t* __restrict__ status) {
   const long long k = (long long)blockIdx.x * kBlock + threadIdx.x;
   __shared__ __align__(16) double s_logtab[1 << kLogTableBits][2];
   stage_log_table(s_logtab);
   if (k >= Q.n) return;
+  solve_out_body<VARIANT>(M, I, Q, out, ld, status, k, &s_logtab[0][0]);
+}
+
+// Stage 2 of GetHorizontalDistanceToIntersectionPoint (.cc:945-989): 9 outputs (cm, rad) + bool.
+__device__ __forceinline__ void hdtip_out_body(const DevMedium& M, const IceConsts& I,
+                                               const QueryArgs& Q, double* __restrict__ out,
+                                               size_t ld, uint8_t* __restrict__ ok, long long k,
+                                               const double* tab) {
   double thR;
   const Geometry g = load_query<IN_CM>(M, Q, k, thR);
   const double x = out[4 * ld + k];
   const int st = (int)out[0 * ld + k];
-  const Solved S = evaluate_root(M, I, g, x, st, &s_logtab[0][0]);
+  const Solved S = evaluate_root(M, I, g, x, st, tab);
   const double thd = S.thd_ice + S.thd_air;
   double tS, tP;
   fresnel_from_sine(S.ice_n, I.ice0.n, S.ice_n / I.ice0.n, sin_start(S.inc * M.d2r), tS, tP);
@@ -1444,24 +1521,32 @@ __global__ __launch_bounds__(kBlock) void hdtip_out_kernel(DevMedium M, IceConst
   ok[k] = check_solution(thd, g.D) ? 1 : 0;
 }
 
+__global__ __launch_bounds__(kBlock) void hdtip_out_kernel(DevMedium M, IceConsts I, QueryArgs Q,
+                                                           double* __restrict__ out, size_t ld,
+                                                           uint8_t* __restrict__ ok) {
+  const long long k = (long long)blockIdx.x * kBlock + threadIdx.x;
+  __shared__ __align__(16) double s_logtab[1 << kLogTableBits][2];
+  stage_log_table(s_logtab);
+  if (k >= Q.n) return;
+  hdtip_out_body(M, I, Q, out, ld, ok, k, &s_logtab[0][0]);
+}
+
 // Stage 2 of the table lookup's minimizer fallback (.cc:1417-1456): the reference passes its
 // own output references to GetHorizontalDistanceToIntersectionPoint in the order
 // (geoIce, geoAir, optIce, optAir, ...), so the optical and geometric slots trade places;
 // `ok` arrives holding the lookup's checks and is completed with CheckSolBool and
 // launchAngle < 0, then the four zeroed slots of .cc:1451-1456.
-__global__ __launch_bounds__(kBlock) void lookup_fallback_out_kernel(
-    DevMedium M, IceConsts I, QueryArgs Q, double* __restrict__ out, size_t ld,
-    uint8_t* __restrict__ ok) {
-  const long long k = (long long)blockIdx.x * kBlock + threadIdx.x;
-  __shared__ __align__(16) double s_logtab[1 << kLogTableBits][2];
-  stage_log_table(s_logtab);
-  if (k >= Q.n) return;
+__device__ __forceinline__ void lookup_fallback_out_body(const DevMedium& M, const IceConsts& I,
+                                                         const QueryArgs& Q,
+                                                         double* __restrict__ out, size_t ld,
+                                                         uint8_t* __restrict__ ok, long long k,
+                                                         const double* tab) {
   if (!(Q.mask[k] & AIRICE_LOOKUP_FALLBACK)) return;
   double thR;
   const Geometry g = load_query<IN_CM100>(M, Q, k, thR);
   const double x = out[4 * ld + k];
   const int st = (int)out[0 * ld + k];
-  const Solved S = evaluate_root(M, I, g, x, st, &s_logtab[0][0]);
+  const Solved S = evaluate_root(M, I, g, x, st, tab);
   const double thd = S.thd_ice + S.thd_air;
   double tS, tP;
   fresnel_from_sine(S.ice_n, I.ice0.n, S.ice_n / I.ice0.n, sin_start(S.inc * M.d2r), tS, tP);
@@ -1479,19 +1564,26 @@ __global__ __launch_bounds__(kBlock) void lookup_fallback_out_kernel(
   ok[k] = good ? 1 : 0;
 }
 
-// Stage 2 of the pythonwrapper TraceIceToAir (TraceIceToAir.C:5-73), rows of 10.
-__global__ __launch_bounds__(kBlock) void trace_out_kernel(DevMedium M, IceConsts I, QueryArgs Q,
-                                                           double* __restrict__ out10) {
+__global__ __launch_bounds__(kBlock) void lookup_fallback_out_kernel(
+    DevMedium M, IceConsts I, QueryArgs Q, double* __restrict__ out, size_t ld,
+    uint8_t* __restrict__ ok) {
   const long long k = (long long)blockIdx.x * kBlock + threadIdx.x;
   __shared__ __align__(16) double s_logtab[1 << kLogTableBits][2];
   stage_log_table(s_logtab);
   if (k >= Q.n) return;
+  lookup_fallback_out_body(M, I, Q, out, ld, ok, k, &s_logtab[0][0]);
+}
+
+// Stage 2 of the pythonwrapper TraceIceToAir (TraceIceToAir.C:5-73), rows of 10.
+__device__ __forceinline__ void trace_out_body(const DevMedium& M, const IceConsts& I,
+                                               const QueryArgs& Q, double* __restrict__ out10,
+                                               long long k, const double* tab) {
   double thR;
   const Geometry g = load_query<IN_TRACE>(M, Q, k, thR);
   double* o = out10 + 10 * k;
   const double x = o[5];
   const int st = (int)o[9];
-  const Solved S = evaluate_root(M, I, g, x, st, &s_logtab[0][0]);
+  const Solved S = evaluate_root(M, I, g, x, st, tab);
   const double thd = S.thd_ice + S.thd_air;
   const double aoi = k_asin((S.ice_n / I.ice0.n) * sin_start(S.inc * M.d2r)) * M.r2d;
   if (check_solution(thd, g.D)) {
@@ -1510,6 +1602,45 @@ __global__ __launch_bounds__(kBlock) void trace_out_kernel(DevMedium M, IceConst
 #pragma unroll
     for (int c = 0; c < 10; ++c) o[c] = -1000;
   }
+}
+
+__global__ __launch_bounds__(kBlock) void trace_out_kernel(DevMedium M, IceConsts I, QueryArgs Q,
+                                                           double* __restrict__ out10) {
+  const long long k = (long long)blockIdx.x * kBlock + threadIdx.x;
+  __shared__ __align__(16) double s_logtab[1 << kLogTableBits][2];
+  stage_log_table(s_logtab);
+  if (k >= Q.n) return;
+  trace_out_body(M, I, Q, out10, k, &s_logtab[0][0]);
+}
+
+// One query, both stages in one launch (the scalar C++ / ctypes entry points): one wave finds the
+// root with the evaluation spread over its lanes, lane 0 parks it and runs the stage-2 body of
+// the entry point (OUT).  Bit-identical to the two batch kernels.
+enum { OUT_SOLVE_MR = 0, OUT_SOLVE_PY = 1, OUT_HDTIP = 2, OUT_FALLBACK = 3, OUT_TRACE = 4 };
+template <int IN, int OUT>
+// (out is not __restrict__: park's slots lie inside it, written here and read by the body)
+__global__ __launch_bounds__(64) void scalar_solve_kernel(DevMedium M, IceConsts I, QueryArgs Q,
+                                                          Park park, double* out, size_t ld,
+                                                          uint8_t* flag) {
+  __shared__ __align__(16) double s_logtab[1 << kLogTableBits][2];
+  for (int t = threadIdx.x; t < (1 << kLogTableBits); t += 64) {
+    s_logtab[t][0] = kLogTable[t][0];
+    s_logtab[t][1] = kLogTable[t][1];
+  }
+  __syncthreads();
+  if (IN == IN_CM100 && !(Q.mask[0] & AIRICE_LOOKUP_FALLBACK)) return;
+  double thR;
+  const Geometry g = load_query<IN>(M, Q, 0, thR);
+  const SolveResult r = solve_root<true>(M, I, g, thR, park.exact != 0, &s_logtab[0][0]);
+  if (threadIdx.x != 0) return;
+  park.root[0] = r.root;
+  park.status[0] = (double)r.status;
+  const double* tab = &s_logtab[0][0];
+  if (OUT == OUT_SOLVE_MR) solve_out_body<AIRICE_VARIANT_MULTIRAY>(M, I, Q, out, ld, flag, 0, tab);
+  if (OUT == OUT_SOLVE_PY) solve_out_body<AIRICE_VARIANT_PYWRAPPER>(M, I, Q, out, ld, flag, 0, tab);
+  if (OUT == OUT_HDTIP) hdtip_out_body(M, I, Q, out, ld, flag, 0, tab);
+  if (OUT == OUT_FALLBACK) lookup_fallback_out_body(M, I, Q, out, ld, flag, 0, tab);
+  if (OUT == OUT_TRACE) trace_out_body(M, I, Q, out, 0, tab);
 }
 
 // ---------------------------------------------------------------------------
@@ -1559,6 +1690,12 @@ size_t group_min_batch() {
 template <int IN>
 static int launch_roots(const DevMedium& M, const IceConsts& I, const QueryArgs& Q,
                         const Park& park, size_t n, hipStream_t st) {
+  if (n == 1 && park.stats == nullptr) {  // one query: the wave-parallel evaluation
+    ktimer_begin(KT_ROOTS, st);
+    hipLaunchKernelGGL(roots_wave_kernel<IN>, dim3(1), dim3(64), 0, st, M, I, Q, park);
+    ktimer_end(KT_ROOTS, st);
+    return launch_ok();
+  }
   const size_t group_min = group_min_batch();
   // (the table lookup's fallback pass stays block-local: its batch is the whole lookup batch,
   // of which typically well under 1 % of lanes are fallback lanes)
@@ -1795,6 +1932,15 @@ int launch_solve(const DevMedium& M, const IceConsts& I, int variant, const doub
   if (stats_path != nullptr && hipMalloc(&park.stats, sizeof(int) * 3 * n) != hipSuccess)
     return AIRICE_EHIP;
   const dim3 grid(grid_for((long long)n)), block(kBlock);
+  if (n == 1 && park.stats == nullptr) {
+    if (variant == AIRICE_VARIANT_MULTIRAY)
+      hipLaunchKernelGGL((scalar_solve_kernel<IN_M, OUT_SOLVE_MR>), dim3(1), dim3(64), 0, st, M, I,
+                         Q, park, out, ld, status);
+    else
+      hipLaunchKernelGGL((scalar_solve_kernel<IN_M, OUT_SOLVE_PY>), dim3(1), dim3(64), 0, st, M, I,
+                         Q, park, out, ld, status);
+    return launch_ok();
+  }
   if (int rc = launch_roots<IN_M>(M, I, Q, park, n, st)) return rc;
   if (park.stats != nullptr) {  // debug: append the per-query counts (synchronous)
     std::vector<int> h(3 * n);
@@ -1825,6 +1971,11 @@ int launch_hdtip(const DevMedium& M, const IceConsts& I, const double* src, cons
   const QueryArgs Q{src, dist, depth, nullptr, ice_cm, (long long)n};
   const Park park{out + 4 * ld, out, 1, bisect_exact(), nullptr};
   const dim3 grid(grid_for((long long)n)), block(kBlock);
+  if (n == 1) {
+    hipLaunchKernelGGL((scalar_solve_kernel<IN_CM, OUT_HDTIP>), dim3(1), dim3(64), 0, st, M, I, Q,
+                       park, out, ld, ok);
+    return launch_ok();
+  }
   if (int rc = launch_roots<IN_CM>(M, I, Q, park, n, st)) return rc;
   ktimer_begin(KT_OUT, st);
   hipLaunchKernelGGL(hdtip_out_kernel, grid, block, 0, st, M, I, Q, out, ld, ok);
@@ -1842,6 +1993,11 @@ int launch_lookup_fallback(const DevMedium& M, const IceConsts& I, const double*
   const QueryArgs Q{src, dist, depth, nullptr, ice_arg, (long long)n, flags};
   const Park park{out + 4 * ld, out, 1, bisect_exact(), nullptr};
   const dim3 grid(grid_for((long long)n)), block(kBlock);
+  if (n == 1) {
+    hipLaunchKernelGGL((scalar_solve_kernel<IN_CM100, OUT_FALLBACK>), dim3(1), dim3(64), 0, st, M,
+                       I, Q, park, out, ld, ok);
+    return launch_ok();
+  }
   if (int rc = launch_roots<IN_CM100>(M, I, Q, park, n, st)) return rc;
   hipLaunchKernelGGL(lookup_fallback_out_kernel, grid, block, 0, st, M, I, Q, out, ld, ok);
   return launch_ok();
@@ -1853,6 +2009,11 @@ int launch_trace(const DevMedium& M, const IceConsts& I, const double* depth, co
   const QueryArgs Q{depth, ice, txh, dist, 0.0, (long long)n};
   const Park park{out10 + 5, out10 + 9, 10, bisect_exact(), nullptr};
   const dim3 grid(grid_for((long long)n)), block(kBlock);
+  if (n == 1) {
+    hipLaunchKernelGGL((scalar_solve_kernel<IN_TRACE, OUT_TRACE>), dim3(1), dim3(64), 0, st, M, I, Q,
+                       park, out10, 0, nullptr);
+    return launch_ok();
+  }
   if (int rc = launch_roots<IN_TRACE>(M, I, Q, park, n, st)) return rc;
   ktimer_begin(KT_OUT, st);
   hipLaunchKernelGGL(trace_out_kernel, grid, block, 0, st, M, I, Q, out10);
