@@ -631,7 +631,7 @@ __device__ __forceinline__ double air_thd(const DevMedium& M, const Query& q, do
   return thd;
 }
 
-// One evaluation of f spread over a wave, for one-query calls (roots_wave_kernel): lanes 0-4 take
+// One evaluation of f spread over a wave, for one-query calls (scalar_solve_kernel): lanes 0-4 take
 // the Tx layer, layers 2 and 1 (when strictly between), the ice layer and the segment in the ice,
 // each with the same delta_D as air_thd, and the sums are formed in air_thd's order from the
 // lanes' values -- the same bits as the one-lane evaluation, with ~1/4 of its dependent chain.
@@ -1403,27 +1403,6 @@ __global__ __launch_bounds__(kSortedBlock, AIRICE_SORTED_WAVES) void roots_sorte
   park.status[k * park.stride] = (double)r.status;
 }
 
-// One-query root finding (the scalar C++ / ctypes entry points): one wave solves query 0 with the
-// evaluation spread over its lanes (eval_thd_wave); same roots and status bits as roots_kernel.
-template <int IN>
-__global__ __launch_bounds__(64) void roots_wave_kernel(DevMedium M, IceConsts I, QueryArgs Q,
-                                                        Park park) {
-  __shared__ __align__(16) double s_logtab[1 << kLogTableBits][2];
-  for (int t = threadIdx.x; t < (1 << kLogTableBits); t += 64) {
-    s_logtab[t][0] = kLogTable[t][0];
-    s_logtab[t][1] = kLogTable[t][1];
-  }
-  __syncthreads();
-  if (IN == IN_CM100 && !(Q.mask[0] & AIRICE_LOOKUP_FALLBACK)) return;
-  double thR;
-  const Geometry g = load_query<IN>(M, Q, 0, thR);
-  const SolveResult r = solve_root<true>(M, I, g, thR, park.exact != 0, &s_logtab[0][0]);
-  if (threadIdx.x == 0) {
-    park.root[0] = r.root;
-    park.status[0] = (double)r.status;
-  }
-}
-
 __device__ __forceinline__ bool check_solution(double thd, double D) {
   // CheckSolution (.cc:978-983, AirIceRayTracing.cc:916-921)
   bool good = false;
@@ -1690,12 +1669,6 @@ size_t group_min_batch() {
 template <int IN>
 static int launch_roots(const DevMedium& M, const IceConsts& I, const QueryArgs& Q,
                         const Park& park, size_t n, hipStream_t st) {
-  if (n == 1 && park.stats == nullptr) {  // one query: the wave-parallel evaluation
-    ktimer_begin(KT_ROOTS, st);
-    hipLaunchKernelGGL(roots_wave_kernel<IN>, dim3(1), dim3(64), 0, st, M, I, Q, park);
-    ktimer_end(KT_ROOTS, st);
-    return launch_ok();
-  }
   const size_t group_min = group_min_batch();
   // (the table lookup's fallback pass stays block-local: its batch is the whole lookup batch,
   // of which typically well under 1 % of lanes are fallback lanes)

@@ -1,4 +1,4 @@
-"""One-query calls take the wave-parallel root finder (roots_wave_kernel: the lanes of one wave
+"""One-query calls take the fused wave-parallel kernel (scalar_solve_kernel: the lanes of one wave
 share each f evaluation); batches take the per-lane kernels.  The two must agree bit for bit --
 roots, status bits and every output column -- for Air2IceRayTracing, the CoREAS entry and
 Py_TraceIceToAir, over the cfg3/cfg5 distributions and the edge geometries of
