@@ -76,20 +76,19 @@ __global__ __launch_bounds__(kLkBlock) void lookup_pack_kernel(const float* __re
     p[q] = make_float4(c[4 * q], c[4 * q + 1], c[4 * q + 2], c[4 * q + 3]);
 }
 
-}  // namespace
-
-int launch_lookup_pack(const airice_lookup_table* t, float* e, hipStream_t st) {
-  const long long n = (long long)t->n_entries;
-  if (n == 0) return AIRICE_OK;
-  hipLaunchKernelGGL(lookup_pack_kernel, dim3((unsigned)((n + kLkBlock - 1) / kLkBlock)),
-                     dim3(kLkBlock), 0, st, t->table, (long long)t->ld, n, e);
-  return hipGetLastError() == hipSuccess ? AIRICE_OK : AIRICE_EHIP;
+// Row records after the entry records: one lane per full table row (lk_row_fold).
+__global__ __launch_bounds__(kLkBlock) void lookup_rows_kernel(LkTable T, float* __restrict__ e) {
+  const long long r = (long long)blockIdx.x * kLkBlock + threadIdx.x;
+  if (r >= T.rows) return;
+  float rec[AIRICE_LOOKUP_ROW_FLOATS];
+  lk_row_fold(T, r, rec);
+  float4* p = reinterpret_cast<float4*>(e + T.n * AIRICE_LOOKUP_ENTRY_FLOATS +
+                                        r * AIRICE_LOOKUP_ROW_FLOATS);
+  p[0] = make_float4(rec[0], rec[1], rec[2], rec[3]);
+  p[1] = make_float4(rec[4], rec[5], rec[6], rec[7]);
 }
 
-int launch_lookup(const DevMedium& M, const IceConsts& I, const airice_lookup_table* t,
-                  const double* src, const double* dist, const double* depth, double ice_cm,
-                  size_t n, double* out, size_t ld, uint8_t* ok, uint8_t* flags, hipStream_t st) {
-  if (n == 0) return AIRICE_OK;
+LkTable lk_table(const airice_lookup_table* t) {
   LkTable T;
   for (int c = 0; c < AIRICE_TABLE_COLUMNS; ++c) T.col[c] = t->table + (size_t)c * t->ld;
   T.e = t->entries;
@@ -98,6 +97,31 @@ int launch_lookup(const DevMedium& M, const IceConsts& I, const airice_lookup_ta
   T.step_h = t->height_step;
   T.hsteps = t->total_height_steps;
   T.asteps = t->total_angle_steps;
+  T.rows = T.e != nullptr ? T.n / T.asteps : 0;
+  return T;
+}
+
+}  // namespace
+
+int launch_lookup_pack(const airice_lookup_table* t, float* e, hipStream_t st) {
+  const long long n = (long long)t->n_entries;
+  if (n == 0) return AIRICE_OK;
+  hipLaunchKernelGGL(lookup_pack_kernel, dim3((unsigned)((n + kLkBlock - 1) / kLkBlock)),
+                     dim3(kLkBlock), 0, st, t->table, (long long)t->ld, n, e);
+  LkTable T = lk_table(t);
+  T.e = e;
+  T.rows = n / T.asteps;
+  if (T.rows > 0)
+    hipLaunchKernelGGL(lookup_rows_kernel, dim3((unsigned)((T.rows + kLkBlock - 1) / kLkBlock)),
+                       dim3(kLkBlock), 0, st, T, e);
+  return hipGetLastError() == hipSuccess ? AIRICE_OK : AIRICE_EHIP;
+}
+
+int launch_lookup(const DevMedium& M, const IceConsts& I, const airice_lookup_table* t,
+                  const double* src, const double* dist, const double* depth, double ice_cm,
+                  size_t n, double* out, size_t ld, uint8_t* ok, uint8_t* flags, hipStream_t st) {
+  if (n == 0) return AIRICE_OK;
+  const LkTable T = lk_table(t);
   const unsigned grid = (unsigned)((n + kLkBlock - 1) / kLkBlock);
   ktimer_begin(KT_LOOKUP, st);
   hipLaunchKernelGGL(lookup_kernel, dim3(grid), dim3(kLkBlock), 0, st, T, src, dist, ice_cm,

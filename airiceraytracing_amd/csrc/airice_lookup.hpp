@@ -9,6 +9,7 @@
 
 #include <cmath>
 #include <cstdint>
+#include <cstring>
 
 #include "airice.h"
 
@@ -20,6 +21,7 @@ struct LkTable {
   long long n;
   double stop_h, step_h;  // LoopStopHeight, HeightStepSize of the last table made
   int hsteps, asteps;     // TotalHeightSteps, TotalAngleSteps
+  long long rows;         // row records after the entry records in e (n / asteps), 0: none
 };
 struct LkTxhBins {
   long long s1, e1, s2, e2;
@@ -80,9 +82,13 @@ __host__ __device__ __forceinline__ double lk_interp(double x, double xa, double
 
 // FindClosestAirTxHeight (.cc:1033-1126): the row of height P and the span of entries with a
 // usable THD (not NaN, not in (-inf, 0.01) except exactly 0), scanned inwards from both ends.
-__host__ __device__ __forceinline__ LkTxhBins lk_closest_txh(const LkTable& T, double P, int& fl) {
+__host__ __device__ __forceinline__ long long lk_txh_index(const LkTable& T, double P) {
   const long long step = (long long)floor((P - T.stop_h) / T.step_h);
-  const long long index = T.hsteps - step - 1;
+  return T.hsteps - step - 1;
+}
+
+// The span of row `index` (everything of FindClosestAirTxHeight but ClosestVal).
+__host__ __device__ __forceinline__ LkTxhBins lk_txh_span(const LkTable& T, long long index, int& fl) {
   const long long max_bin = index * T.asteps + T.asteps - 1;
   const long long min_bin = index * T.asteps;
   double val = -0.001;
@@ -114,13 +120,77 @@ __host__ __device__ __forceinline__ LkTxhBins lk_closest_txh(const LkTable& T, d
   LkTxhBins b;
   b.s1 = end_bin;
   b.e1 = start_bin;
-  b.c1 = fabs(lk_at(T, 0, index, fl) - P);  // sic (.cc:1076): row index used as an entry index
   b.s2 = b.s1 - T.asteps;
   b.e2 = b.e1 - T.asteps;
   if (b.s2 < 0) b.s2 = b.s1 + T.asteps;
   if (b.e2 < 0) b.e2 = b.e1 + T.asteps;
+  b.c1 = 0;
+  b.c2 = 0;
+  return b;
+}
+
+__host__ __device__ __forceinline__ LkTxhBins lk_closest_txh(const LkTable& T, double P, int& fl) {
+  const long long index = lk_txh_index(T, P);
+  LkTxhBins b = lk_txh_span(T, index, fl);
+  b.c1 = fabs(lk_at(T, 0, index, fl) - P);  // sic (.cc:1076): row index used as an entry index
   b.c2 = b.c1;  // ClosestVal2 (.cc:1123) is the same expression
   return b;
+}
+
+// Row record (packed copy, after the entry records): the span of row `index` and the table values
+// the lookup reads at its ends, folded by airice_lookup_pack from the same code as above.  Used
+// only for rows whose scans stay inside the table (ok), so the flags are unchanged.
+struct LkRow {
+  LkTxhBins b;
+  double c1v;      // column 0 at entry `index` (ClosestVal's operand)
+  double h1, h2;   // column 0 at s1, at s2 (s2 < n - 1)
+  double mt1, mt2; // column 1 (THD) at s1, at s2
+};
+__host__ __device__ __forceinline__ float lk_bits_f(int32_t i) {
+  float f;
+  std::memcpy(&f, &i, sizeof(f));
+  return f;
+}
+__host__ __device__ __forceinline__ int32_t lk_bits_i(float f) {
+  int32_t i;
+  std::memcpy(&i, &f, sizeof(i));
+  return i;
+}
+// Fold row r (pack time): 8 floats {s1, e1 (int bits), col0[r], col0[s1], col0[s2], col1[s1],
+// col1[s2], ok (int bits)}.
+__host__ __device__ __forceinline__ void lk_row_fold(const LkTable& T, long long r, float rec[8]) {
+  int fl = 0;
+  const LkTxhBins b = lk_txh_span(T, r, fl);
+  const bool s2_used = b.s2 < T.n - 1;
+  const bool ok = fl == 0 && b.s1 >= 0 && b.s1 < T.n && r < T.n && b.s1 < (1LL << 31) &&
+                  b.e1 >= -(1LL << 31) && b.e1 < (1LL << 31) && b.s2 >= 0;
+  rec[0] = lk_bits_f((int32_t)(ok ? b.s1 : 0));
+  rec[1] = lk_bits_f((int32_t)(ok ? b.e1 : 0));
+  rec[2] = ok ? T.col[0][r] : 0.0f;
+  rec[3] = ok ? T.col[0][b.s1] : 0.0f;
+  rec[4] = ok && s2_used ? T.col[0][b.s2] : 0.0f;
+  rec[5] = ok ? T.col[1][b.s1] : 0.0f;
+  rec[6] = ok && s2_used ? T.col[1][b.s2] : 0.0f;
+  rec[7] = lk_bits_f(ok ? 1 : 0);
+}
+__host__ __device__ __forceinline__ bool lk_row(const LkTable& T, long long index, LkRow& R) {
+  if (T.e == nullptr || index < 0 || index >= T.rows) return false;
+  const float4* p = reinterpret_cast<const float4*>(T.e + T.n * AIRICE_LOOKUP_ENTRY_FLOATS +
+                                                    index * AIRICE_LOOKUP_ROW_FLOATS);
+  const float4 a = p[0], c = p[1];
+  if (lk_bits_i(c.w) == 0) return false;
+  R.b.s1 = lk_bits_i(a.x);
+  R.b.e1 = lk_bits_i(a.y);
+  R.b.s2 = R.b.s1 - T.asteps;
+  R.b.e2 = R.b.e1 - T.asteps;
+  if (R.b.s2 < 0) R.b.s2 = R.b.s1 + T.asteps;
+  if (R.b.e2 < 0) R.b.e2 = R.b.e1 + T.asteps;
+  R.c1v = a.z;
+  R.h1 = a.w;
+  R.h2 = c.x;
+  R.mt1 = c.y;
+  R.mt2 = c.z;
+  return true;
 }
 
 // FindClosestTHD (.cc:1128-1169).  With a packed table the THD values at the final pair come
@@ -164,8 +234,9 @@ __host__ __device__ __forceinline__ LkThdBins lk_closest_thd(const LkTable& T, d
 
 // The 10 parameters of one table row at horizontal distance D (.cc:1199-1240 / 1250-1289).
 __host__ __device__ __forceinline__ void lk_row_params(const LkTable& T, double D, long long s, long long e,
-                                              double par[10], double* closest, int& fl) {
-  const double max_thd = lk_at(T, 1, s, fl);
+                                              double par[10], double* closest, int& fl,
+                                              const double* max_thd_row = nullptr) {
+  const double max_thd = max_thd_row != nullptr ? *max_thd_row : lk_at(T, 1, s, fl);
   if (D <= max_thd) {
     LkThdPair pr;
     const LkThdBins b = lk_closest_thd(T, D, s, e, fl, pr);
@@ -194,15 +265,24 @@ __host__ __device__ __forceinline__ void lk_row_params(const LkTable& T, double 
 __host__ __device__ __forceinline__ void lk_par_values(const LkTable& T, double H, double D, double* h1,
                                        double par1[10], double* h2, double par2[10], int& fl) {
   const double min_h = lk_at(T, 0, T.n - 1, fl);
-  const LkTxhBins b = lk_closest_txh(T, H, fl);
+  LkRow R;  // packed row record: the span and its end values without the scans
+  const bool fast = lk_row(T, lk_txh_index(T, H), R);
+  LkTxhBins b;
+  if (fast) {
+    b = R.b;
+    b.c1 = fabs(R.c1v - H);
+    b.c2 = b.c1;
+  } else {
+    b = lk_closest_txh(T, H, fl);
+  }
   double c1 = 0;
-  *h1 = lk_at(T, 0, b.s1, fl);
-  lk_row_params(T, D, b.s1, b.e1, par1, &c1, fl);
+  *h1 = fast ? R.h1 : lk_at(T, 0, b.s1, fl);
+  lk_row_params(T, D, b.s1, b.e1, par1, &c1, fl, fast ? &R.mt1 : nullptr);
   *h2 = *h1;
   if (b.c1 != 0 && H > min_h && b.s2 < T.n - 1) {
-    *h2 = lk_at(T, 0, b.s2, fl);
+    *h2 = fast ? R.h2 : lk_at(T, 0, b.s2, fl);
     double c2 = 0;
-    lk_row_params(T, D, b.s2, b.e2, par2, &c2, fl);
+    lk_row_params(T, D, b.s2, b.e2, par2, &c2, fl, fast ? &R.mt2 : nullptr);
   } else {
 #pragma unroll
     for (int ip = 0; ip < 10; ++ip) par2[ip] = par1[ip];

@@ -136,6 +136,7 @@ airice::LkTable host_lk(const std::vector<std::vector<float>>& cols) {
   airice::LkTable T;
   for (int c = 0; c < AIRICE_TABLE_COLUMNS; ++c) T.col[c] = cols[c].data();
   T.e = nullptr;
+  T.rows = 0;
   T.n = (long long)cols[0].size();
   T.stop_h = LoopStopHeight;
   T.step_h = HeightStepSize;
@@ -659,7 +660,7 @@ void TableLookupBatch(const double* SrcHeightASL, const double* HorizontalDistan
   t.total_angle_steps = TotalAngleSteps;
   t.entries = nullptr;
   if (dt.packed == nullptr) {
-    if (hipMalloc(&dt.packed, sizeof(float) * AIRICE_LOOKUP_ENTRY_FLOATS * entries) != hipSuccess ||
+    if (hipMalloc(&dt.packed, sizeof(float) * AIRICE_LOOKUP_PACK_FLOATS(entries, t.total_angle_steps)) != hipSuccess ||
         airice_lookup_pack(&t, dt.packed, nullptr) != AIRICE_OK)
       die("airice_lookup_pack");
   }

@@ -146,10 +146,12 @@ class AirIceSolver:
     @staticmethod
     def lookup_pack(lt: LookupTable, stream=None):
         """airice_lookup_pack: a packed copy of the table (one 128-byte record per entry, holding
-        it and the next entry; torch tensor on the table's device) that ``lt`` then reads; the
-        tensor is kept on ``lt``."""
+        it and the next entry, then one 32-byte record per table row; torch tensor on the table's
+        device) that ``lt`` then reads; the tensor is kept on ``lt``."""
         import torch
-        packed = torch.empty(int(lt.n_entries) * _lib.LOOKUP_ENTRY_FLOATS, dtype=torch.float32,
+        n = int(lt.n_entries)
+        floats = n * _lib.LOOKUP_ENTRY_FLOATS + (n // int(lt.total_angle_steps)) * _lib.LOOKUP_ROW_FLOATS
+        packed = torch.empty(floats, dtype=torch.float32,
                              device=torch.device("cuda", torch.cuda.current_device()))
         check(lib().airice_lookup_pack(ctypes.byref(lt), ptr(packed), _stream_handle(stream)),
               "airice_lookup_pack")

@@ -192,9 +192,18 @@ typedef struct airice_lookup_table {
  * index1, index2), so each table row it visits costs it one record line, which also supplies the
  * THD values at the pair. */
 #define AIRICE_LOOKUP_ENTRY_FLOATS 32
+/* Floats per row record, after the n_entries entry records, one per full table row
+ * (n_entries / total_angle_steps rows): the row's FindClosestAirTxHeight span and the table
+ * values the lookup reads at its ends (32 B), folded once by the pack. */
+#define AIRICE_LOOKUP_ROW_FLOATS 8
+/* Floats of the whole packed copy. */
+#define AIRICE_LOOKUP_PACK_FLOATS(n_entries, angle_steps)                 \
+  ((size_t)(n_entries) * AIRICE_LOOKUP_ENTRY_FLOATS +                    \
+   ((size_t)(n_entries) / (size_t)(angle_steps)) * AIRICE_LOOKUP_ROW_FLOATS)
 
-/* Pack one antenna's table for the lookup: n_entries records of AIRICE_LOOKUP_ENTRY_FLOATS floats
- * (above), 16-byte aligned (128-byte for one line per record).  The lookup reads the 10
+/* Pack one antenna's table for the lookup: AIRICE_LOOKUP_PACK_FLOATS(n_entries, total_angle_steps)
+ * floats -- the entry records, then the row records (above) -- 16-byte aligned (128-byte for one
+ * line per record).  The lookup reads the 10
  * interpolated parameters of both entries of a pair from one record instead of 10 columns ld
  * floats apart; results are identical.  Stream-ordered; run once per table, then set
  * t->entries = d_entries. */

@@ -66,10 +66,22 @@ def _run_case(solver, oracle_medium, depth_cm, hstep, a0, a1, astep, nq, seed):
     torch.cuda.synchronize()
     assert np.array_equal(out_p.cpu().numpy(), out, equal_nan=True)
     assert np.array_equal(ok_p.cpu().numpy(), ok) and np.array_equal(fl_p.cpu().numpy(), fl)
-    packed = lp._packed.cpu().numpy().reshape(-1, 32)  # record i: columns 1-10 of entries i, i+1
+    flat = lp._packed.cpu().numpy()
+    ne, asteps = host.shape[1], g.angle_steps
+    packed = flat[:ne * 32].reshape(-1, 32)  # record i: columns 1-10 of entries i, i+1
     assert np.array_equal(packed[:, :10].T, host[1:11], equal_nan=True)
     assert np.array_equal(packed[:-1, 10:20].T, host[1:11, 1:], equal_nan=True)
     assert np.isnan(packed[-1, 10:20]).all() and not packed[:, 20:].any()
+    # row records: the row's usable-THD span inside the row and the values at its ends
+    rows = flat[ne * 32:].reshape(ne // asteps, 8)
+    ri = rows.view(np.int32)
+    r = np.arange(rows.shape[0])
+    okr = ri[:, 7] == 1
+    assert okr.mean() > 0.9
+    s1, e1 = ri[okr, 0], ri[okr, 1]
+    assert (s1 >= r[okr] * asteps).all() and (e1 <= r[okr] * asteps + asteps - 1).all()
+    assert np.array_equal(rows[okr, 2], host[0][r[okr]])
+    assert np.array_equal(rows[okr, 3], host[0][s1]) and np.array_equal(rows[okr, 5], host[1][s1])
     rout, rok, rfl = oracle.table_lookup_batch(oracle_medium, oracle.lookup_table(host, og),
                                                src, dist, dep, ICE_CM, nthreads=NTHREADS)
     assert np.array_equal(fl, rfl), np.flatnonzero(fl != rfl)[:10]
