@@ -320,6 +320,7 @@ struct TableArgs {
 // s_memrealtime at entry and exit plus HW_ID / XCC_ID.  Not part of the API.
 struct WaveTrace {
   unsigned long long t0, t1;
+  unsigned long long c0, c1;  // s_memtime (shader clock) at entry and exit: the in-kernel clock
   unsigned hw_id, xcc_id;
 };
 
@@ -397,7 +398,10 @@ __device__ __forceinline__ void table_block(const DevMedium& M, const IceConsts&
   }
   const unsigned wave = block * (BS / 64) + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
-  if (TRACE && lane == 0) trace[wave].t0 = __builtin_amdgcn_s_memrealtime();
+  if (TRACE && lane == 0) {
+    trace[wave].t0 = __builtin_amdgcn_s_memrealtime();
+    trace[wave].c0 = __builtin_amdgcn_s_memtime();
+  }
   const int k0 = (int)block * BS;
   int r0[R];
 #pragma unroll
@@ -429,6 +433,7 @@ __device__ __forceinline__ void table_block(const DevMedium& M, const IceConsts&
   }
   if (TRACE && lane == 0) {
     trace[wave].t1 = __builtin_amdgcn_s_memrealtime();
+    trace[wave].c1 = __builtin_amdgcn_s_memtime();
     trace[wave].hw_id = __builtin_amdgcn_s_getreg((4 << 0) | (0 << 6) | (31 << 11));  // HW_ID
     trace[wave].xcc_id = __builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (31 << 11));
   }

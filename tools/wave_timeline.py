@@ -25,7 +25,8 @@ def run(hstep):
             os.remove(path)
         s.table_device(g, t)
     torch.cuda.synchronize()
-    dt = np.dtype([("t0", "<u8"), ("t1", "<u8"), ("hw", "<u4"), ("xcc", "<u4")])
+    dt = np.dtype([("t0", "<u8"), ("t1", "<u8"), ("c0", "<u8"), ("c1", "<u8"), ("hw", "<u4"),
+                   ("xcc", "<u4")])
     return np.fromfile(path, dtype=dt), g
 
 
@@ -49,6 +50,11 @@ def main():
         np.savez_compressed(out, start=start, end=end, key=key)
     print(f"waves={len(w)} simds={nsimd} waves/simd={len(w) / nsimd:.2f} "
           f"kernel span={end.max():.2f}us first-start spread={np.percentile(start, 99):.2f}us")
+    # in-kernel shader clock (s_memtime ticks per 100 MHz s_memrealtime tick), long waves only
+    dt_real = (w["t1"] - w["t0"]).astype(np.float64)
+    dt_core = (w["c1"] - w["c0"]).astype(np.float64)
+    long = dt_real > np.percentile(dt_real, 50)
+    print(f"in-kernel clock GHz: median {np.median(dt_core[long] / dt_real[long]) * 0.1:.3f}")
     print(f"wave duration us: min {dur.min():.2f} p10 {np.percentile(dur, 10):.2f} "
           f"median {np.median(dur):.2f} p90 {np.percentile(dur, 90):.2f} max {dur.max():.2f}")
     # resident waves per SIMD over time, averaged over SIMDs
