@@ -240,7 +240,8 @@ __device__ __forceinline__ void ray_solution_row(const DevMedium& M, const IceCo
 #pragma clang loop unroll(disable)
     for (int il = top_hi - 1; il >= bot; --il) {
       if (il < top) {
-        const Segment s = segment_const(I.lower[il], M.A_air, A2, sin_asin(v), true, v, tab);
+        // v is a segment's output sine here (already sin_asin'd: sin_asin is idempotent)
+        const Segment s = segment_const(I.lower[il], M.A_air, A2, v, true, v, tab);
         thd_air += s.thd;
         t_air += s.t;
         geo_air += s.geo;
@@ -251,7 +252,7 @@ __device__ __forceinline__ void ray_solution_row(const DevMedium& M, const IceCo
 #pragma unroll
     for (int il = kMaxLayers - 2; il >= 0; --il) {
       if (il >= top || il < bot) continue;
-      const Segment s = segment_const(I.lower[il], M.A_air, A2, sin_asin(v), true, v, tab);
+      const Segment s = segment_const(I.lower[il], M.A_air, A2, v, true, v, tab);
       thd_air += s.thd;
       t_air += s.t;
       geo_air += s.geo;
