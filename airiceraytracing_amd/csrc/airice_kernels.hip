@@ -792,7 +792,10 @@ __device__ __forceinline__ SolveResult solve_root(const DevMedium& M, const IceC
       phase = PH_DONE;
     }
   }
-  double root = probe_bad ? 0.0 : 0.5 * (lo + hi);
+  // GSL's reported root is 0.5 (lo + hi) of the final bracket on every path (each iterate sets it
+  // so, and the exact-zero exits make lo == hi), except the failed probe, which reports 0: the
+  // root is formed once at the end instead of being carried through the loop
+  bool root_zero = probe_bad;
   double f_lower = 0.0, f_upper = 0.0;
   const double tol = 0.000000001;
   int iter = 0;
@@ -811,7 +814,9 @@ __device__ __forceinline__ SolveResult solve_root(const DevMedium& M, const IceC
   // linear (a straight ray's is exactly H u; single precision is plenty for a first guess), then
   // secant steps in theta on the last two points (x1, f1), (x2, f2)
   double x1 = 0.0, f1 = 0.0, x2 = 0.0, f2 = 0.0;
-  double xg = 0.0, dlt = 0.0;  // PH_G1/G2: guards at xg -/+ dlt
+  // PH_G1/G2: guards at x2 -/+ dlt, where x2 is the secant search's last point (it stays put after
+  // the search) and dlt lives in x1 (dead once the search ends)
+  double& dlt = x1;
   int est = 0, n_eval = 0, n_inside = 0;
   auto guard = [&](double x, double f) {
     if (!(fabs(f) >= tau) || !(x > gL && x < gR)) return;
@@ -845,9 +850,9 @@ __device__ __forceinline__ SolveResult solve_root(const DevMedium& M, const IceC
       // (right) moves to it, as gsl_root_fsolver_iterate would
       if (f_lower == 0.0 || f_upper == 0.0) {
         ++iter;
-        root = (f_lower == 0.0) ? lo : hi;
-        lo = root;
-        hi = root;
+        const double r0 = (f_lower == 0.0) ? lo : hi;
+        lo = r0;
+        hi = r0;
         finish(false);
         break;  // lo == hi: gsl_root_test_interval converges
       }
@@ -872,7 +877,6 @@ __device__ __forceinline__ SolveResult solve_root(const DevMedium& M, const IceC
         }
         if (lo != lo0) f_lower = fL;
         if (hi != hi0) f_upper = fR;
-        if (lo != lo0 || hi != hi0) root = 0.5 * (lo + hi);
         if (done) break;
       }
     }
@@ -896,9 +900,9 @@ __device__ __forceinline__ SolveResult solve_root(const DevMedium& M, const IceC
 #endif
       if (!(x > gL && x < gR)) x = 0.5 * (gL + gR);  // safeguard: the guards' midpoint
     } else if (phase == PH_G1) {
-      x = xg - dlt;
+      x = x2 - dlt;
     } else if (phase == PH_G2) {
-      x = xg + dlt;
+      x = x2 + dlt;
     } else {
       x = lo;
     }
@@ -921,11 +925,10 @@ __device__ __forceinline__ SolveResult solve_root(const DevMedium& M, const IceC
     if (phase == PH_PROBE) {
       if ((!isnan(thd_air) && thd_air > 0) || lo > hi - 0.1) {
         if (hi < 90.001 && hi > 90.00) hi = 90.05;
-        root = 0.5 * (lo + hi);
         phase = PH_FLO;
         if (lo > hi) {
           status |= AIRICE_SOLVE_BAD_BRACKET;
-          root = 0.0;
+          root_zero = true;
           phase = PH_DONE;
         }
       } else {
@@ -982,9 +985,8 @@ __device__ __forceinline__ SolveResult solve_root(const DevMedium& M, const IceC
         // at the root: guards a few tau either side, scaled by the local secant slope; a side
         // whose guard already lies within W/4 of the root needs none
         dlt = 4.0 * tau * fabs((x2 - x1) * __builtin_amdgcn_rcp(f2 - f1));
-        xg = x;
         const double Wq = AIRICE_GUARD_SKIP ? 0.25e-9 * gL : 0.0;
-        const bool needL = !(xg - gL <= Wq), needR = !(gR - xg <= Wq);
+        const bool needL = !(x2 - gL <= Wq), needR = !(gR - x2 <= Wq);
         phase = (dlt > 0.0 && dlt < (gR - gL)) ? (needL ? PH_G1 : (needR ? PH_G2 : PH_BISECT))
                                                : PH_BISECT;
       } else {
@@ -997,7 +999,7 @@ __device__ __forceinline__ SolveResult solve_root(const DevMedium& M, const IceC
       }
     } else if (phase == PH_G1 || phase == PH_G2) {
       if (isfinite(f)) guard(x, f);
-      phase = (phase == PH_G1 && !(AIRICE_GUARD_SKIP && gR - xg <= 0.25e-9 * gL)) ? PH_G2
+      phase = (phase == PH_G1 && !(AIRICE_GUARD_SKIP && gR - x2 <= 0.25e-9 * gL)) ? PH_G2
                                                                                : PH_BISECT;
     } else {  // PH_BISECT: gsl_root_fsolver_iterate at a midpoint between the guards
       if (!exact && isfinite(f)) guard(x, f);
@@ -1009,22 +1011,19 @@ __device__ __forceinline__ SolveResult solve_root(const DevMedium& M, const IceC
         status |= AIRICE_SOLVE_STALE_MID | AIRICE_SOLVE_MAXITER;
         frozen = true;
       } else if (f == 0.0) {
-        root = x;
         lo = x;
         hi = x;
       } else if ((f_lower > 0.0 && f < 0.0) || (f_lower < 0.0 && f > 0.0)) {
-        root = 0.5 * (lo + x);
         hi = x;
         f_upper = f;
       } else {
-        root = 0.5 * (x + hi);
         lo = x;
         f_lower = f;
       }
       finish(frozen);
     }
   }
-  return SolveResult{root, status, n_eval, est, n_inside};
+  return SolveResult{root_zero ? 0.0 : 0.5 * (lo + hi), status, n_eval, est, n_inside};
 }
 
 struct Solved {
