@@ -10,8 +10,10 @@
  *
  * Parity status: the reference needs GNU GSL (absent from this image), so it is
  * unbuildable here; the oracle is a restatement pinned by (a) scipy's natural
- * cubic spline for the atmosphere N0, and (b) the known-answer values recorded in
- * SURVEY.md §4 (see tests/golden/README.md for their provenance).
+ * cubic spline for the atmosphere N0, (b) the known-answer values recorded in
+ * SURVEY.md §4 (see tests/golden/README.md for their provenance), and (c) numerical
+ * integration of the ray equations in its own n(z) (tests/test_oracle_physics.py:
+ * segment closed forms, whole forward rays, Air2Ice roots).
  *
  * Every function cites the reference file:line it restates.  Faithful mode: the
  * call structure mirrors the reference (per-call layer scans, repeated libm calls),

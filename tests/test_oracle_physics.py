@@ -1,0 +1,161 @@
+"""Independent check of the oracle's closed forms: the antiderivatives the reference evaluates
+(fDnfR, ftimeD, fpathD, MultiRayAirIceRefraction.cc:377-447, through GetRayHorizontalPath /
+GetRayPropagationTime / GetRayGeometricPath, .cc:449-513) against direct numerical integration of
+the ray equations in the oracle's own n(z) (scipy quad, relative tolerance 1e-13):
+
+    horizontal distance  dX/dz = L / sqrt(n^2 - L^2)
+    travel time          dt/dz = n^2 / (c sqrt(n^2 - L^2))
+    geometric path       ds/dz = n / sqrt(n^2 - L^2)
+
+for segments in every air layer of the GDAS atmosphere and in the ice, and for whole forward rays
+(GetRayTracingSolutions, .cc:1796-2017) integrated layer by layer with the reference's convention
+at layer boundaries (the incidence sine carries over, each layer re-derives its ray parameter from
+its start: L = n(start) sin) and Snell's law into the ice.  The reference itself cannot be built
+here (GNU GSL is absent); this pins the formulas the oracle restates -- and hence
+every GPU path checked against the oracle -- to the physics they integrate, independently of the
+survey's known-answer points."""
+import os
+
+import numpy as np
+import pytest
+from scipy.integrate import quad
+
+import oracle
+
+C_LIGHT = 299792458.0
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.fixture(scope="module")
+def medium():
+    return oracle.load_atmosphere(os.path.join(ROOT, "airiceraytracing_amd", "data",
+                                               "Atmosphere.dat.gz"))
+
+
+def _integrals(n, L, z1, z2):
+    def q(f):
+        return quad(f, z1, z2, epsabs=0.0, epsrel=1e-13, limit=400)[0]
+    return (q(lambda z: L / np.sqrt(n(z) ** 2 - L * L)),
+            q(lambda z: n(z) ** 2 / (C_LIGHT * np.sqrt(n(z) ** 2 - L * L))),
+            q(lambda z: n(z) / np.sqrt(n(z) ** 2 - L * L)))
+
+
+def _rel(a, b):
+    return abs(a - b) / max(abs(b), 1e-300)
+
+
+def test_segment_closed_forms_match_integration(medium):
+    m = medium
+    atm = [m.atmlay[i] / 100 for i in range(5)]
+    rng = np.random.default_rng(3)
+    worst = 0.0
+    cases = 0
+    for layer in range(m.max_layers):
+        lo, hi = atm[layer], atm[layer + 1]
+        for _ in range(6):
+            z1, z2 = np.sort(rng.uniform(lo + 1.0, hi - 1.0, 2))
+            def n(z):
+                return oracle.getnz_air(m, z)
+            L = min(n(z1), n(z2)) * np.sin(np.radians(rng.uniform(5.0, 88.0)))
+            thd, t, s = _integrals(n, L, z1, z2)
+            # Rx the lower end, Tx the upper (the air sign convention, .cc:464-466)
+            got = (oracle.rtf_eval(m, 1, [m.A_air, z1, z2, L, 1])[0],
+                   oracle.rtf_eval(m, 2, [m.A_air, z1, z2, L, 1])[0],
+                   oracle.rtf_eval(m, 10, [m.A_air, z1, z2, L, 1])[0])
+            for g, e in zip(got, (thd, t, s)):
+                worst = max(worst, _rel(g, e))
+            # swapping the ends flips every sign
+            assert oracle.rtf_eval(m, 1, [m.A_air, z2, z1, L, 1])[0] == -got[0]
+            cases += 1
+    # ice: depths below the surface, Rx the deeper end
+    for _ in range(12):
+        d1, d2 = np.sort(rng.uniform(0.5, 2000.0, 2))
+        def n(z):
+            return oracle.getnz_ice(m, z)
+        L = n(d1) * np.sin(np.radians(rng.uniform(5.0, 85.0)))
+        thd, t, s = _integrals(n, L, d1, d2)
+        got = (oracle.rtf_eval(m, 1, [m.A_ice, d2, d1, L, 0])[0],
+               oracle.rtf_eval(m, 2, [m.A_ice, d2, d1, L, 0])[0],
+               oracle.rtf_eval(m, 10, [m.A_ice, d2, d1, L, 0])[0])
+        for g, e in zip(got, (thd, t, s)):
+            worst = max(worst, _rel(g, e))
+        cases += 1
+    assert cases == 6 * m.max_layers + 12
+    assert worst < 1e-10, worst
+
+
+def _ray_by_integration(m, launch_deg, txh, ice_h, depth):
+    """Layer walk of GetRayTracingSolutions (.cc:1796-1922) with the integrals above."""
+    atm = [m.atmlay[i] / 100 for i in range(5)]
+    d2r = m.pi / 180.0
+    v = np.sin((180.0 - launch_deg) * d2r)
+
+    def n_air(z):
+        return oracle.getnz_air(m, z)
+
+    def layer_of(z):
+        for il in range(m.max_layers):
+            if atm[il] <= z < atm[il + 1]:
+                return il
+        return m.max_layers - 1
+
+    top, bot = layer_of(txh), layer_of(ice_h)
+    thd_air = t_air = s_air = 0.0
+    for il in range(top, bot - 1, -1):
+        start = txh if il == top else atm[il + 1] - 1e-5
+        stop = ice_h if il == bot else atm[il]
+        L = n_air(start) * v
+        thd, t, s = _integrals(n_air, L, stop, start)
+        thd_air, t_air, s_air = thd_air + thd, t_air + t, s_air + s
+        v = L / n_air(stop)
+    # Snell into the ice, then down to the antenna
+    L = n_air(ice_h) * v
+    thd_ice, t_ice, s_ice = _integrals(lambda z: oracle.getnz_ice(m, z), L, 0.0, -depth)
+    return thd_air, thd_ice, t_air, t_ice, s_air, s_ice
+
+
+@pytest.mark.parametrize("launch_deg,txh", [(170.0, 20000.0), (150.0, 60000.0), (135.0, 5000.0),
+                                            (179.0, 3500.0), (120.0, 95000.0), (160.0, 9000.0)])
+def test_forward_ray_matches_layer_walk_integration(medium, launch_deg, txh):
+    ice_h, depth = 3000.0, -200.0
+    d = oracle.ray_solution(medium, launch_deg, txh, ice_h, depth)
+    thd_air, thd_ice, t_air, t_ice, s_air, s_ice = _ray_by_integration(medium, launch_deg, txh,
+                                                                       ice_h, depth)
+    # dummy[3], [4]: THD in air / ice; [6], [7]: c x time; [16], [17]: geometric paths
+    pairs = ((d[3], thd_air), (d[4], thd_ice), (d[6], t_air * C_LIGHT), (d[7], t_ice * C_LIGHT),
+             (d[16], s_air), (d[17], s_ice))
+    for got, exp in pairs:
+        assert _rel(got, exp) < 1e-9, (got, exp, [p for p in pairs])
+
+
+def test_air2ice_root_solves_the_integrated_ray(medium):
+    """Air2IceRayTracing (.cc:1464-1616): at the oracle's root the integrated ray -- one ray
+    parameter from the Tx layer down through every air layer and into the ice (GetAirPropagationPar
+    .cc:757-771 reuses the first layer's L) -- has the closed forms' THD in air and in ice, and
+    their sum meets the horizontal distance D to within the root's bracket."""
+    from tests import parity
+    m = medium
+    atm = [m.atmlay[i] / 100 for i in range(5)]
+    d2r = m.pi / 180.0
+    txh, dist, dep = parity.cfg3_queries(40)
+    checked = solved = 0
+    for H, D, depth in zip(txh, dist, dep):
+        out, st = oracle.air2ice(m, H, D, 3000.0, depth)
+        if st & oracle.SOLVE_UNPINNED or not np.isfinite(out[10]):
+            continue
+        L = oracle.getnz_air(m, H) * np.sin((180.0 - out[10]) * d2r)
+        # layer spans: the Tx layer from its lower bound (or the ice) up to H; each layer below
+        # from its lower bound (or the ice) up to 1e-5 m under its upper bound (.cc:1846)
+        cuts = [a for a in atm if 3000.0 < a < H]
+        spans = [(lo, hi - (1e-5 if hi != H else 0.0))
+                 for lo, hi in zip([3000.0] + cuts, cuts + [H])]
+        thd_air = sum(_integrals(lambda z: oracle.getnz_air(m, z), L, a, b)[0] for a, b in spans)
+        thd_ice = _integrals(lambda z: oracle.getnz_ice(m, z), L, 0.0, -depth)[0]
+        assert _rel(out[2], thd_air) < 1e-9 and _rel(out[3], thd_ice) < 1e-9, (H, D, depth)
+        checked += 1
+        # rows the reference counts as solved (CheckSolution, .cc:978-983): the root meets D far
+        # inside that 1 m / 1 % check (queries beyond the reachable distance stay unsolved)
+        if abs(out[1] - D) < 1.0:
+            assert abs(out[1] - D) < 1e-6 * D + 0.01, (H, D, out[1])
+            solved += 1
+    assert checked >= 35 and solved >= 30, (checked, solved)
