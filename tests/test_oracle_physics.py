@@ -159,3 +159,29 @@ def test_air2ice_root_solves_the_integrated_ray(medium):
             assert abs(out[1] - D) < 1e-6 * D + 0.01, (H, D, out[1])
             solved += 1
     assert checked >= 35 and solved >= 30, (checked, solved)
+
+
+def test_pythonwrapper_root_matches_the_integrated_ray():
+    """The pythonwrapper's Air2IceRayTracing (AirIceRayTracing.cc, exact pi) at its roots: the same
+    integrated-ray check as above."""
+    from tests import parity
+    m = oracle.load_atmosphere(os.path.join(ROOT, "airiceraytracing_amd", "data",
+                                            "Atmosphere.dat.gz"), pi=oracle.PI_EXACT)
+    atm = [m.atmlay[i] / 100 for i in range(5)]
+    d2r = m.pi / 180.0
+    txh, dist, dep = parity.cfg3_queries(20, seed=99)
+    checked = 0
+    for H, D, depth in zip(txh, dist, dep):
+        thr = oracle.straight_angle_of(m, H, D, 3000.0, depth)
+        out, st = oracle.py_air2ice(m, H, D, 3000.0, depth, thr)
+        if st & oracle.SOLVE_UNPINNED or not np.isfinite(out[10]):
+            continue
+        L = oracle.getnz_air(m, H) * np.sin((180.0 - out[10]) * d2r)
+        cuts = [a for a in atm if 3000.0 < a < H]
+        spans = [(lo, hi - (1e-5 if hi != H else 0.0))
+                 for lo, hi in zip([3000.0] + cuts, cuts + [H])]
+        thd_air = sum(_integrals(lambda z: oracle.getnz_air(m, z), L, a, b)[0] for a, b in spans)
+        thd_ice = _integrals(lambda z: oracle.getnz_ice(m, z), L, 0.0, -depth)[0]
+        assert _rel(out[2], thd_air) < 1e-9 and _rel(out[3], thd_ice) < 1e-9, (H, D, depth)
+        checked += 1
+    assert checked >= 15
