@@ -463,4 +463,17 @@ __device__ __forceinline__ void fresnel_trans(double n1, double n2, double theta
   if (isnan(tP)) tP = 0;
 }
 
+// Completion signal of a one-query launch (ScalarCall::arm, airice_runtime.cpp): the thread that
+// wrote the call's last output makes its stores visible to the host, then stores seq into the
+// pinned, device-mapped flag the calling host thread spins on.  flag == nullptr: no signal.
+struct Signal {
+  unsigned* flag;
+  unsigned seq;
+};
+__device__ __forceinline__ void signal_done(const Signal& s) {
+  if (s.flag == nullptr) return;
+  __threadfence_system();
+  *static_cast<volatile unsigned*>(s.flag) = s.seq;
+}
+
 }  // namespace airice

@@ -62,12 +62,19 @@ void set_error(const char* fmt, ...);
 // One-query calls of the scalar drop-ins (the C++ MultiRayAirIceRefraction:: / RayTracingFunctions::
 // functions, Py_TraceIceToAir, airice_rtf_eval): a pinned, device-mapped staging block per device
 // that the host fills with the inputs and the kernels read and write in place (no copies), and a
-// library-owned non-blocking stream; a call is its launches plus one stream synchronisation.
+// library-owned non-blocking stream; a call is its launches plus one wait.
 // The slot of the current device (hipGetDevice) is created on first use and locked for the call.
+// A call made of ONE kernel launch arms the slot's completion flag first (arm()); the launcher
+// of that kernel takes the signal (take_scalar_signal) and passes it to the kernel, which stores
+// the sequence number after its outputs (signal_done); sync() then spins on the pinned flag
+// instead of synchronising the stream (launch + wait 7.8 us instead of 11-12 us).
 struct ScalarSlot {
   double* h = nullptr;  // host view
   double* d = nullptr;  // device view of the same memory
   hipStream_t st = nullptr;
+  unsigned* flag_h = nullptr;  // completion flag: host view
+  unsigned* flag_d = nullptr;  //                  device view
+  unsigned seq = 0;
 };
 constexpr size_t kScalarSlotDoubles = 512;
 class ScalarCall {
@@ -76,11 +83,18 @@ class ScalarCall {
   ~ScalarCall();
   bool ok() const { return slot_ != nullptr; }
   ScalarSlot& slot() { return *slot_; }
-  int sync();  // waits for the slot's stream; AIRICE_OK or AIRICE_EHIP
+  // Arms the completion signal for the next launch on this thread (the call's only kernel).
+  void arm();
+  // Waits for the call: on the flag when the armed signal was taken by a launcher (falling back
+  // to the stream after a bounded spin), else on the slot's stream; AIRICE_OK or AIRICE_EHIP.
+  int sync();
  private:
   ScalarSlot* slot_ = nullptr;
   void* lock_ = nullptr;
+  bool armed_ = false;
 };
+// The armed signal of this thread (cleared by taking it); {nullptr, 0} when none is armed.
+Signal take_scalar_signal();
 // The table lookup's minimizer fallback for one query that lk_query flagged one-sided
 // (.cc:1418-1420), on the device through the scalar slot: out9 / *ok as the batch lookup.
 int lookup_fallback_one(const airice_medium* m, double src_cm, double dist_cm, double depth_cm,

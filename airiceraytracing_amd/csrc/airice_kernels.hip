@@ -476,13 +476,14 @@ __global__ __launch_bounds__(kBlock) void rays_kernel(DevMedium M, IceConsts I,
                                                       const double* __restrict__ launch,
                                                       const double* __restrict__ txh, int in_ice,
                                                       long long n, double* __restrict__ out,
-                                                      size_t ld) {
+                                                      size_t ld, Signal sig) {
   const long long k = (long long)blockIdx.x * kBlock + threadIdx.x;
   if (k >= n) return;
   double d[18];
   ray_solution(M, I, launch[k], txh[k], in_ice != 0, d);
 #pragma unroll
   for (int c = 0; c < 18; ++c) out[c * ld + k] = d[c];
+  if (k == 0) signal_done(sig);  // armed for one-ray calls only
 }
 
 // ---------------------------------------------------------------------------
@@ -1605,14 +1606,17 @@ template <int IN, int OUT>
 // (out is not __restrict__: park's slots lie inside it, written here and read by the body)
 __global__ __launch_bounds__(64) void scalar_solve_kernel(DevMedium M, IceConsts I, QueryArgs Q,
                                                           Park park, double* out, size_t ld,
-                                                          uint8_t* flag) {
+                                                          uint8_t* flag, Signal sig) {
   __shared__ __align__(16) double s_logtab[1 << kLogTableBits][2];
   for (int t = threadIdx.x; t < (1 << kLogTableBits); t += 64) {
     s_logtab[t][0] = kLogTable[t][0];
     s_logtab[t][1] = kLogTable[t][1];
   }
   __syncthreads();
-  if (IN == IN_CM100 && !(Q.mask[0] & AIRICE_LOOKUP_FALLBACK)) return;
+  if (IN == IN_CM100 && !(Q.mask[0] & AIRICE_LOOKUP_FALLBACK)) {
+    if (threadIdx.x == 0) signal_done(sig);
+    return;
+  }
   double thR;
   const Geometry g = load_query<IN>(M, Q, 0, thR);
   const SolveResult r = solve_root<true>(M, I, g, thR, park.exact != 0, &s_logtab[0][0]);
@@ -1625,6 +1629,7 @@ __global__ __launch_bounds__(64) void scalar_solve_kernel(DevMedium M, IceConsts
   if (OUT == OUT_HDTIP) hdtip_out_body(M, I, Q, out, ld, flag, 0, tab);
   if (OUT == OUT_FALLBACK) lookup_fallback_out_body(M, I, Q, out, ld, flag, 0, tab);
   if (OUT == OUT_TRACE) trace_out_body(M, I, Q, out, 0, tab);
+  signal_done(sig);
 }
 
 // ---------------------------------------------------------------------------
@@ -1895,8 +1900,9 @@ int launch_table_multi(const DevMedium& M, const IceConsts* Ih, const airice_gri
 int launch_rays(const DevMedium& M, const IceConsts& I, const double* launch, const double* txh,
                 int in_ice, size_t n, double* out, size_t ld, hipStream_t st) {
   if (n == 0) return AIRICE_OK;
+  const Signal sig = n == 1 ? take_scalar_signal() : Signal{nullptr, 0};
   hipLaunchKernelGGL(rays_kernel, dim3(grid_for((long long)n)), dim3(kBlock), 0, st, M, I, launch,
-                     txh, in_ice, (long long)n, out, ld);
+                     txh, in_ice, (long long)n, out, ld, sig);
   return launch_ok();
 }
 
@@ -1911,12 +1917,13 @@ int launch_solve(const DevMedium& M, const IceConsts& I, int variant, const doub
     return AIRICE_EHIP;
   const dim3 grid(grid_for((long long)n)), block(kBlock);
   if (n == 1 && park.stats == nullptr) {
+    const Signal sig = take_scalar_signal();
     if (variant == AIRICE_VARIANT_MULTIRAY)
       hipLaunchKernelGGL((scalar_solve_kernel<IN_M, OUT_SOLVE_MR>), dim3(1), dim3(64), 0, st, M, I,
-                         Q, park, out, ld, status);
+                         Q, park, out, ld, status, sig);
     else
       hipLaunchKernelGGL((scalar_solve_kernel<IN_M, OUT_SOLVE_PY>), dim3(1), dim3(64), 0, st, M, I,
-                         Q, park, out, ld, status);
+                         Q, park, out, ld, status, sig);
     return launch_ok();
   }
   if (int rc = launch_roots<IN_M>(M, I, Q, park, n, st)) return rc;
@@ -1951,7 +1958,7 @@ int launch_hdtip(const DevMedium& M, const IceConsts& I, const double* src, cons
   const dim3 grid(grid_for((long long)n)), block(kBlock);
   if (n == 1) {
     hipLaunchKernelGGL((scalar_solve_kernel<IN_CM, OUT_HDTIP>), dim3(1), dim3(64), 0, st, M, I, Q,
-                       park, out, ld, ok);
+                       park, out, ld, ok, take_scalar_signal());
     return launch_ok();
   }
   if (int rc = launch_roots<IN_CM>(M, I, Q, park, n, st)) return rc;
@@ -1973,7 +1980,7 @@ int launch_lookup_fallback(const DevMedium& M, const IceConsts& I, const double*
   const dim3 grid(grid_for((long long)n)), block(kBlock);
   if (n == 1) {
     hipLaunchKernelGGL((scalar_solve_kernel<IN_CM100, OUT_FALLBACK>), dim3(1), dim3(64), 0, st, M,
-                       I, Q, park, out, ld, ok);
+                       I, Q, park, out, ld, ok, take_scalar_signal());
     return launch_ok();
   }
   if (int rc = launch_roots<IN_CM100>(M, I, Q, park, n, st)) return rc;
@@ -1989,7 +1996,7 @@ int launch_trace(const DevMedium& M, const IceConsts& I, const double* depth, co
   const dim3 grid(grid_for((long long)n)), block(kBlock);
   if (n == 1) {
     hipLaunchKernelGGL((scalar_solve_kernel<IN_TRACE, OUT_TRACE>), dim3(1), dim3(64), 0, st, M, I, Q,
-                       park, out10, 0, nullptr);
+                       park, out10, 0, nullptr, take_scalar_signal());
     return launch_ok();
   }
   if (int rc = launch_roots<IN_TRACE>(M, I, Q, park, n, st)) return rc;

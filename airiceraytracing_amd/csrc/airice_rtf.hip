@@ -503,7 +503,7 @@ struct RtfCall {
   double a[8];
 };
 
-__global__ void rtf_kernel(DevMedium M, RtfCall c, double* __restrict__ out) {
+__global__ void rtf_kernel(DevMedium M, RtfCall c, double* __restrict__ out, Signal sig) {
   if (threadIdx.x != 0 || blockIdx.x != 0) return;
   double r[AIRICE_RTF_AIR2ICE_FIELDS > 5 * kMaxLayers + 2 ? AIRICE_RTF_AIR2ICE_FIELDS
                                                          : 5 * kMaxLayers + 2];
@@ -558,6 +558,7 @@ __global__ void rtf_kernel(DevMedium M, RtfCall c, double* __restrict__ out) {
       break;
   }
   for (int i = 0; i < c.n_out; i++) out[i] = r[i];
+  signal_done(sig);
 }
 
 }  // namespace
@@ -597,7 +598,7 @@ int launch_rtf(const DevMedium& M, int op, const double* args, size_t n_args, do
   c.op = op;
   c.n_out = rtf_outputs(op, M.ml);
   for (int i = 0; i < 8; i++) c.a[i] = (size_t)i < n_args ? args[i] : 0.0;
-  hipLaunchKernelGGL(rtf_kernel, dim3(1), dim3(64), 0, st, M, c, d_out);
+  hipLaunchKernelGGL(rtf_kernel, dim3(1), dim3(64), 0, st, M, c, d_out, take_scalar_signal());
   return hipGetLastError() == hipSuccess ? AIRICE_OK : AIRICE_EHIP;
 }
 

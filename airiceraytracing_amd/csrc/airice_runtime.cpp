@@ -7,6 +7,7 @@
 #include <algorithm>
 #include <cstdio>
 #include <cstdlib>
+#include <chrono>
 #include <cstring>
 #include <fstream>
 #include <mutex>
@@ -284,7 +285,14 @@ struct SlotEntry {
 };
 std::mutex g_slots_mu;
 std::vector<SlotEntry*> g_slots;  // by device ordinal; never freed (process lifetime)
+thread_local Signal t_signal{nullptr, 0};
 }  // namespace
+
+Signal take_scalar_signal() {
+  const Signal s = t_signal;
+  t_signal = Signal{nullptr, 0};
+  return s;
+}
 
 ScalarCall::ScalarCall() {
   int dev = 0;
@@ -306,7 +314,8 @@ ScalarCall::ScalarCall() {
     void* h = nullptr;
     void* d = nullptr;
     hipStream_t st = nullptr;
-    if ((e = hipHostMalloc(&h, sizeof(double) * kScalarSlotDoubles, hipHostMallocMapped)) !=
+    // the flag sits in the slot's last 128-byte line, away from the inputs and outputs
+    if ((e = hipHostMalloc(&h, sizeof(double) * (kScalarSlotDoubles + 16), hipHostMallocMapped)) !=
             hipSuccess ||
         (e = hipHostGetDevicePointer(&d, h, 0)) != hipSuccess ||
         (e = hipStreamCreateWithFlags(&st, hipStreamNonBlocking)) != hipSuccess) {
@@ -318,14 +327,43 @@ ScalarCall::ScalarCall() {
     sl.h = static_cast<double*>(h);
     sl.d = static_cast<double*>(d);
     sl.st = st;
+    sl.flag_h = reinterpret_cast<unsigned*>(sl.h + kScalarSlotDoubles);
+    sl.flag_d = reinterpret_cast<unsigned*>(sl.d + kScalarSlotDoubles);
+    __atomic_store_n(sl.flag_h, 0u, __ATOMIC_RELEASE);
   }
   slot_ = &sl;
   lock_ = lk;
 }
 
-ScalarCall::~ScalarCall() { delete static_cast<std::unique_lock<std::mutex>*>(lock_); }
+ScalarCall::~ScalarCall() {
+  if (armed_) t_signal = Signal{nullptr, 0};  // never leave a signal armed past the call
+  delete static_cast<std::unique_lock<std::mutex>*>(lock_);
+}
+
+void ScalarCall::arm() {
+  if (++slot_->seq == 0) slot_->seq = 1;  // 0 is the flag's initial value
+  t_signal = Signal{slot_->flag_d, slot_->seq};
+  armed_ = true;
+}
 
 int ScalarCall::sync() {
+  if (armed_) {
+    armed_ = false;
+    const bool taken = t_signal.flag == nullptr;
+    t_signal = Signal{nullptr, 0};
+    if (taken) {
+      // the kernel's outputs are visible once the flag holds seq; a launch that has not
+      // signalled after ~2 ms (first-use code loading, a fault) is waited for on its stream
+      const unsigned want = slot_->seq;
+      const auto t0 = std::chrono::steady_clock::now();
+      for (unsigned spins = 0;; ++spins) {
+        if (__atomic_load_n(slot_->flag_h, __ATOMIC_ACQUIRE) == want) return AIRICE_OK;
+        if ((spins & 255) == 255 &&
+            std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(2000))
+          break;
+      }
+    }
+  }
   const hipError_t e = hipStreamSynchronize(slot_->st);
   if (e != hipSuccess) {
     set_error("scalar call: %s", hipGetErrorString(e));
@@ -351,6 +389,7 @@ int lookup_fallback_one(const airice_medium* m, double src_cm, double dist_cm, d
   hb[0] = good ? 1 : 0;
   hb[1] = (uint8_t)flags;
   uint8_t* db = reinterpret_cast<uint8_t*>(sl.d + 12);
+  call.arm();
   rc = launch_lookup_fallback(M, I, sl.d, sl.d + 1, sl.d + 2, ice_cm, 1, sl.d + 3, 1, db, db + 1,
                               sl.st);
   if (rc == AIRICE_OK) rc = call.sync();
@@ -776,6 +815,7 @@ int airice_rtf_eval(const airice_medium* m, int op, const double* args, size_t n
   }
   ScalarCall call;  // the kernel writes its outputs straight into the pinned slot
   if (!call.ok()) return AIRICE_EHIP;
+  call.arm();
   rc = airice::launch_rtf(M, op, args, n_args, call.slot().d, call.slot().st);
   if (rc) {
     set_error("rtf launch failed: %s", hipGetErrorString(hipGetLastError()));
@@ -878,6 +918,7 @@ void Py_TraceIceToAir(double AntennaDepth, double IceLayerHeight, double AirTxHe
   sl.h[1] = IceLayerHeight;
   sl.h[2] = AirTxHeight;
   sl.h[3] = HorizontalDistance;
+  call.arm();
   if (airice_trace_ice_to_air_launch(&g_py_medium, sl.d, sl.d + 1, sl.d + 2, sl.d + 3, 1,
                                      sl.d + 4, sl.st) != AIRICE_OK ||
       call.sync() != AIRICE_OK) {
