@@ -51,6 +51,9 @@ constexpr int kTableBlock = AIRICE_TABLE_BS;
 // with e.g. -DAIRICE_TWO_RAY_MIN=524288 -DAIRICE_TWO_RAY_MAX=917504.
 // AIRICE_TABLE_R2=0 leaves the R = 2 kernel out of the build (co-compiled template variants can
 // perturb each other's register allocation)
+#ifndef AIRICE_SCALAR_STAMP
+#define AIRICE_SCALAR_STAMP 0
+#endif
 #ifndef AIRICE_OVERSHOOT
 #define AIRICE_OVERSHOOT 0
 #endif
@@ -638,15 +641,19 @@ __device__ __forceinline__ double air_thd(const DevMedium& M, const Query& q, do
   return thd;
 }
 
-// One evaluation of f spread over a wave, for one-query calls (scalar_solve_kernel): lanes 0-4 take
-// the Tx layer, layers 2 and 1 (when strictly between), the ice layer and the segment in the ice,
-// each with the same delta_D as air_thd, and the sums are formed in air_thd's order from the
-// lanes' values -- the same bits as the one-lane evaluation, with ~1/4 of its dependent chain.
-// Every lane holds the same query, so everything else stays wave-uniform.
+// Two evaluations of f spread over a wave, for one-query calls (scalar_solve_kernel): lanes 0-4
+// take the Tx layer, layers 2 and 1 (when strictly between), the ice layer and the segment in the
+// ice at theta_a, lanes 32-36 the same at theta_b, each with the same delta_D as air_thd, and the
+// sums are formed in air_thd's order from the lanes' values -- the same bits as the one-lane
+// evaluation, with ~1/4 of its dependent chain.  Every lane holds the same query, so everything
+// else stays wave-uniform.
 __device__ __forceinline__ void eval_thd_wave(const DevMedium& M, const IceConsts& I,
-                                              const Query& q, double theta, const double* tab,
-                                              double& thd_air, double& thd_ice) {
-  const int lane = (int)(threadIdx.x & 63);
+                                              const Query& q, double theta_a, double theta_b,
+                                              const double* tab, double& thd_air_a,
+                                              double& thd_ice_a, double& thd_air_b,
+                                              double& thd_ice_b) {
+  const int lane = (int)(threadIdx.x & 31);
+  const double theta = (threadIdx.x & 32) ? theta_b : theta_a;
   const bool air = q.top >= q.bot;
   double L = __builtin_nan("");
   if (air) {
@@ -668,17 +675,21 @@ __device__ __forceinline__ void eval_thd_wave(const DevMedium& M, const IceConst
   T = pick(ice, slim(I.ice0), T);
   R = pick(ice, q.rx, R);
   const double x = delta_D(T, R, RL, tab);
-  const double d0 = __shfl(x, 0), d1 = __shfl(x, 1), d2 = __shfl(x, 2), d3 = __shfl(x, 3),
-               d4 = __shfl(x, 4);
-  thd_air = 0.0;
-  if (air) {
-    thd_air += -d0;
-    if (2 < q.top && 2 > q.bot) thd_air += -d1;
-    if (1 < q.top && 1 > q.bot) thd_air += -d2;
-    if (q.top > q.bot) thd_air += -d3;
-  }
-  thd_ice = 0;
-  if (q.depth_pos != 0) thd_ice += d4;
+  auto sums = [&](int l0, double& thd_air, double& thd_ice) {
+    const double d0 = __shfl(x, l0), d1 = __shfl(x, l0 + 1), d2 = __shfl(x, l0 + 2),
+                 d3 = __shfl(x, l0 + 3), d4 = __shfl(x, l0 + 4);
+    thd_air = 0.0;
+    if (air) {
+      thd_air += -d0;
+      if (2 < q.top && 2 > q.bot) thd_air += -d1;
+      if (1 < q.top && 1 > q.bot) thd_air += -d2;
+      if (q.top > q.bot) thd_air += -d3;
+    }
+    thd_ice = 0;
+    if (q.depth_pos != 0) thd_ice += d4;
+  };
+  sums(0, thd_air_a, thd_ice_a);
+  sums(32, thd_air_b, thd_ice_b);
 }
 
 // ---------------------------------------------------------------------------
@@ -719,6 +730,9 @@ struct SolveResult {
   double root;
   int status;
   int n_eval, n_est, n_inside;  // evaluations: all, secant search, bisection midpoints (stats)
+#if AIRICE_SCALAR_STAMP
+  int t_setup = 0, t_lean = 0;  // debug: shader clocks of the set-up and of the lean bisection runs
+#endif
 };
 
 enum { PH_PROBE = 0, PH_FLO = 1, PH_FHI = 2, PH_EST = 3, PH_G1 = 4, PH_G2 = 5, PH_BISECT = 6,
@@ -728,6 +742,10 @@ template <bool WAVE = false>
 __device__ __forceinline__ SolveResult solve_root(const DevMedium& M, const IceConsts& I,
                                                   const Geometry& g, double thR, bool exact,
                                                   const double* tab) {
+#if AIRICE_SCALAR_STAMP
+  const unsigned long long ts0 = __builtin_amdgcn_s_memtime();
+  int t_lean = 0;
+#endif
   int status = 0;
   Query q;
   q.depth_pos = g.depth_pos;
@@ -819,6 +837,11 @@ __device__ __forceinline__ SolveResult solve_root(const DevMedium& M, const IceC
   // the search) and dlt lives in x1 (dead once the search ends)
   double& dlt = x1;
   int est = 0, n_eval = 0, n_inside = 0;
+  // WAVE: f(lo) and f(hi), and the two guards, are independent pairs of points; the wave evaluates
+  // each pair at once and keeps the second value for the next trip (the same points, the same
+  // bits, two sequential evaluations fewer)
+  bool have_next = false;
+  double next_air = 0.0, next_ice = 0.0;
   auto guard = [&](double x, double f) {
     if (!(fabs(f) >= tau) || !(x > gL && x < gR)) return;
     if ((f < 0.0) == (fL < 0.0)) {
@@ -844,6 +867,9 @@ __device__ __forceinline__ SolveResult solve_root(const DevMedium& M, const IceC
     if (cont && iter == 40) status |= AIRICE_SOLVE_MAXITER;
     if (frozen || !cont || iter == 40) phase = PH_DONE;
   };
+#if AIRICE_SCALAR_STAMP
+  const int t_setup = (int)(__builtin_amdgcn_s_memtime() - ts0) + (int)(0.0 * (lo + hi));
+#endif
   while (phase != PH_DONE) {
     if (phase == PH_BISECT) {
       // steps that need no evaluation: an exact zero at a bracket end (GSL returns that end),
@@ -858,26 +884,54 @@ __device__ __forceinline__ SolveResult solve_root(const DevMedium& M, const IceC
         break;  // lo == hi: gsl_root_test_interval converges
       }
       if ((okL || okR) && lo > 0.0) {
+#if AIRICE_SCALAR_STAMP
+        const unsigned long long tl0 = __builtin_amdgcn_s_memtime();
+#endif
         // lean run (0 < lo < hi here): the root GSL reports after a step is 0.5 (lo + hi) of the
         // new bracket either way; the interval test reduces to hi - lo < tol lo
         const double gl = okL ? gL : -1.0, gr = okR ? gR : __builtin_inf();
         const double lo0 = lo, hi0 = hi;
         bool done = false;
-        for (;;) {
-          const double xm = (lo + hi) / 2.0;
-          if (xm <= gl) lo = xm;
-          else if (xm >= gr) hi = xm;
-          else break;
-          ++iter;
-          const bool cont = !(fabs(hi - lo) < 0 + tol * lo);
-          if (!cont || iter == 40) {
-            if (cont) status |= AIRICE_SOLVE_MAXITER;
-            done = true;
-            break;
+        if constexpr (WAVE) {
+          // one query per wave: the same steps as selects, four per trip, so that the chain is
+          // midpoint -> compare -> select without a branch per step
+          bool stop = false;
+          while (!stop) {
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+              const double xm = (lo + hi) / 2.0;
+              const bool inL = xm <= gl, inR = !inL && xm >= gr;
+              const bool mv = !stop && (inL || inR);  // otherwise: evaluate this midpoint
+              lo = (mv && inL) ? xm : lo;
+              hi = (mv && inR) ? xm : hi;
+              iter += mv ? 1 : 0;
+              const bool cont = !(fabs(hi - lo) < 0 + tol * lo);
+              const bool fin = mv && (!cont || iter == 40);
+              status = (fin && cont) ? (status | AIRICE_SOLVE_MAXITER) : status;
+              done = done || fin;
+              stop = stop || !mv || fin;
+            }
+          }
+        } else {
+          for (;;) {
+            const double xm = (lo + hi) / 2.0;
+            if (xm <= gl) lo = xm;
+            else if (xm >= gr) hi = xm;
+            else break;
+            ++iter;
+            const bool cont = !(fabs(hi - lo) < 0 + tol * lo);
+            if (!cont || iter == 40) {
+              if (cont) status |= AIRICE_SOLVE_MAXITER;
+              done = true;
+              break;
+            }
           }
         }
         if (lo != lo0) f_lower = fL;
         if (hi != hi0) f_upper = fR;
+#if AIRICE_SCALAR_STAMP
+        t_lean += (int)(__builtin_amdgcn_s_memtime() - tl0) + (int)(0.0 * (lo + hi));
+#endif
         if (done) break;
       }
     }
@@ -912,7 +966,25 @@ __device__ __forceinline__ SolveResult solve_root(const DevMedium& M, const IceC
     n_inside += (phase == PH_BISECT);
     double thd_air, thd_ice;
     if constexpr (WAVE) {
-      eval_thd_wave(M, I, q, x, tab, thd_air, thd_ice);
+      if (have_next) {
+        thd_air = next_air;
+        thd_ice = next_ice;
+        have_next = false;
+      } else {
+        // the point the next trip evaluates when this one is f(lo) (then f(hi)) or the first guard
+        // (then always the second: PH_G1 -> PH_G2)
+        const bool pair = phase == PH_FLO || (phase == PH_G1 && !AIRICE_GUARD_SKIP);
+        const double xb = phase == PH_FLO ? hi : x2 + dlt;
+#if AIRICE_SCALAR_STAMP
+        const unsigned long long e0 = __builtin_amdgcn_s_memtime();
+#endif
+        eval_thd_wave(M, I, q, x, pair ? xb : x, tab, thd_air, thd_ice, next_air, next_ice);
+#if AIRICE_SCALAR_STAMP
+        // debug: evaluation ticks in n_inside (the wave form does not count midpoints)
+        n_inside += (int)(__builtin_amdgcn_s_memtime() - e0) + (int)(0.0 * (thd_air + thd_ice));
+#endif
+        have_next = pair;
+      }
     } else {
       double L;
       thd_air = air_thd(M, q, x, L, tab);
@@ -940,6 +1012,7 @@ __device__ __forceinline__ SolveResult solve_root(const DevMedium& M, const IceC
       if (!isfinite(f)) {
         status |= AIRICE_SOLVE_NONFINITE_END;
         phase = PH_BISECT;
+        have_next = false;  // f(hi) is not wanted after all
       } else {
         fL = f;
         phase = PH_FHI;
@@ -1024,7 +1097,14 @@ __device__ __forceinline__ SolveResult solve_root(const DevMedium& M, const IceC
       finish(frozen);
     }
   }
+#if AIRICE_SCALAR_STAMP
+  SolveResult sr{root_zero ? 0.0 : 0.5 * (lo + hi), status, n_eval, est, n_inside};
+  sr.t_setup = t_setup;
+  sr.t_lean = t_lean;
+  return sr;
+#else
   return SolveResult{root_zero ? 0.0 : 0.5 * (lo + hi), status, n_eval, est, n_inside};
+#endif
 }
 
 struct Solved {
@@ -1085,6 +1165,82 @@ __device__ __forceinline__ Solved evaluate_root(const DevMedium& M, const IceCon
   }
   return S;
 }
+
+// evaluate_root for one-query calls (scalar_solve_kernel; every lane holds the same query and
+// root): the four air segments -- Tx layer, layers 2 and 1, the ice layer -- on lanes 0-3 at once
+// (as eval_thd_wave), the segment in the ice beside them on every lane, then every lane forms the
+// sums from the lanes' values in evaluate_root's order.  The same bits with about a quarter of
+// its dependent chain.
+__device__ __forceinline__ Solved evaluate_root_wave(const DevMedium& M, const IceConsts& I,
+                                                     const Geometry& g, double x, int status,
+                                                     const double* tab) {
+  const int lane = (int)(threadIdx.x & 63);
+  Solved S;
+  S.status = status;
+  S.launch = x;
+  const AirPath P = make_air_path(M, g.H, g.ice);
+  S.ice_n = P.iceair.n;
+  S.thd_air = 0.0;
+  S.t_air = 0.0;
+  S.geo_air = 0.0;
+  S.inc = __builtin_nan("");
+  const bool air = !(P.top < P.bot);
+  double L0 = __builtin_nan(""), v2 = 0.0;
+  if (air) {
+    v2 = first_layer_v2(M, P.tx.n, P.rtop.n, x);
+    L0 = P.rtop.n * v2;
+  } else {
+    S.status |= AIRICE_SOLVE_NO_AIR_LAYER;
+  }
+  // lanes 0-3: the air segments, with the kernel-uniform A as evaluate_root has it (the same
+  // instruction forms, hence also the same NaN bits on rays without a solution)
+  const double A2 = M.A_air * M.A_air;
+  const RayL RL = ray_L(A2, L0);
+  Endpoint T = P.tx, R = P.rtop;  // lane 0 (and the lanes past 3, whose value is unused)
+  T = pick(lane == 1, M.start[2], T);
+  R = pick(lane == 1, M.stop[2], R);
+  T = pick(lane == 2, M.start[1], T);
+  R = pick(lane == 2, M.stop[1], R);
+  T = pick(lane == 3, start_endpoint(M, P.bot), T);
+  R = pick(lane == 3, P.iceair, R);
+  const Segment sg = segment(T, R, M.A_air, A2, RL, true, tab);
+  // the segment in the ice on every lane, beside the air segments (used when g.depth < 0)
+  const Endpoint rx = ice_endpoint(M, g.depth_pos);
+  const double A2i = M.A_ice * M.A_ice;
+  const RayL RLi = ray_L(A2i, L0);
+  const Segment si = segment(I.ice0, rx, M.A_ice, A2i, RLi, false, tab);
+  auto from = [&](int l) { return Segment{__shfl(sg.thd, l), __shfl(sg.t, l), __shfl(sg.geo, l)}; };
+  if (air) {
+    auto add = [&](const Segment& a) {
+      S.thd_air += a.thd;
+      S.t_air += a.t;
+      S.geo_air += a.geo;
+    };
+    add(from(0));
+    if (2 < P.top && 2 > P.bot) add(from(1));
+    if (1 < P.top && 1 > P.bot) add(from(2));
+    if (P.top > P.bot) add(from(3));
+    S.inc = k_asin(P.top == P.bot ? v2 : L0 / P.iceair.n) * M.r2d;
+  }
+  S.thd_ice = 0.0;
+  S.t_ice = 0.0;
+  S.geo_ice = 0.0;
+  S.ant = 0.0;
+  if (g.depth < 0) {
+    S.thd_ice = si.thd;
+    S.ant = k_asin(L0 / rx.n) * M.r2d;
+    S.t_ice = si.t;
+    S.geo_ice = si.geo;
+  }
+  return S;
+}
+
+// The root found by the one-query kernel, handed to its stage-2 body directly (WAVE) instead of
+// through the parked output slots.
+struct WaveRoot {
+  double root;
+  int status;
+};
 
 __device__ __forceinline__ double straight_angle(const DevMedium& M, double H, double D, double ice,
                                                  double depth) {
@@ -1429,16 +1585,20 @@ __device__ __forceinline__ void stage_log_table(double (*s)[2]) {
 // (pythonwrapper, AirIceRayTracing.cc:1070-1084), SoA with stride ld.
 // Stage-2 bodies (one query k, parked root in its output slots), shared by the batch out kernels
 // and the one-query fused kernel (scalar_solve_kernel).
-template <int VARIANT>
+// WAVE (one-query kernel): every lane runs the body with the root in wr; evaluate_root_wave
+// spreads the evaluation over the wave and lane 0 writes the outputs.
+template <int VARIANT, bool WAVE = false>
 __device__ __forceinline__ void solve_out_body(const DevMedium& M, const IceConsts& I,
                                                const QueryArgs& Q, double* __restrict__ out,
                                                size_t ld, uint8_t* __restrict__ status,
-                                               long long k, const double* tab) {
+                                               long long k, const double* tab,
+                                               WaveRoot wr = WaveRoot{0.0, 0}) {
   double thR;
   const Geometry g = load_query<IN_M>(M, Q, k, thR);
-  const double x = out[10 * ld + k];
-  const int st = (int)out[0 * ld + k];
-  const Solved S = evaluate_root(M, I, g, x, st, tab);
+  const double x = WAVE ? wr.root : out[10 * ld + k];
+  const int st = WAVE ? wr.status : (int)out[0 * ld + k];
+  const Solved S = WAVE ? evaluate_root_wave(M, I, g, x, st, tab) : evaluate_root(M, I, g, x, st, tab);
+  if (WAVE && threadIdx.x != 0) return;
   const double thd = S.thd_ice + S.thd_air;
   const double tt = S.t_ice + S.t_air;
   out[0 * ld + k] = g.H;
@@ -1482,15 +1642,17 @@ __global__ __launch_bounds__(kBlock) void solve_out_kernel(DevMedium M, IceConst
 }
 
 // Stage 2 of GetHorizontalDistanceToIntersectionPoint (.cc:945-989): 9 outputs (cm, rad) + bool.
+template <bool WAVE = false>
 __device__ __forceinline__ void hdtip_out_body(const DevMedium& M, const IceConsts& I,
                                                const QueryArgs& Q, double* __restrict__ out,
                                                size_t ld, uint8_t* __restrict__ ok, long long k,
-                                               const double* tab) {
+                                               const double* tab, WaveRoot wr = WaveRoot{0.0, 0}) {
   double thR;
   const Geometry g = load_query<IN_CM>(M, Q, k, thR);
-  const double x = out[4 * ld + k];
-  const int st = (int)out[0 * ld + k];
-  const Solved S = evaluate_root(M, I, g, x, st, tab);
+  const double x = WAVE ? wr.root : out[4 * ld + k];
+  const int st = WAVE ? wr.status : (int)out[0 * ld + k];
+  const Solved S = WAVE ? evaluate_root_wave(M, I, g, x, st, tab) : evaluate_root(M, I, g, x, st, tab);
+  if (WAVE && threadIdx.x != 0) return;
   const double thd = S.thd_ice + S.thd_air;
   double tS, tP;
   fresnel_from_sine(S.ice_n, I.ice0.n, S.ice_n / I.ice0.n, sin_start(S.inc * M.d2r), tS, tP);
@@ -1521,17 +1683,20 @@ __global__ __launch_bounds__(kBlock) void hdtip_out_kernel(DevMedium M, IceConst
 // (geoIce, geoAir, optIce, optAir, ...), so the optical and geometric slots trade places;
 // `ok` arrives holding the lookup's checks and is completed with CheckSolBool and
 // launchAngle < 0, then the four zeroed slots of .cc:1451-1456.
+template <bool WAVE = false>
 __device__ __forceinline__ void lookup_fallback_out_body(const DevMedium& M, const IceConsts& I,
                                                          const QueryArgs& Q,
                                                          double* __restrict__ out, size_t ld,
                                                          uint8_t* __restrict__ ok, long long k,
-                                                         const double* tab) {
+                                                         const double* tab,
+                                                         WaveRoot wr = WaveRoot{0.0, 0}) {
   if (!(Q.mask[k] & AIRICE_LOOKUP_FALLBACK)) return;
   double thR;
   const Geometry g = load_query<IN_CM100>(M, Q, k, thR);
-  const double x = out[4 * ld + k];
-  const int st = (int)out[0 * ld + k];
-  const Solved S = evaluate_root(M, I, g, x, st, tab);
+  const double x = WAVE ? wr.root : out[4 * ld + k];
+  const int st = WAVE ? wr.status : (int)out[0 * ld + k];
+  const Solved S = WAVE ? evaluate_root_wave(M, I, g, x, st, tab) : evaluate_root(M, I, g, x, st, tab);
+  if (WAVE && threadIdx.x != 0) return;
   const double thd = S.thd_ice + S.thd_air;
   double tS, tP;
   fresnel_from_sine(S.ice_n, I.ice0.n, S.ice_n / I.ice0.n, sin_start(S.inc * M.d2r), tS, tP);
@@ -1560,15 +1725,18 @@ __global__ __launch_bounds__(kBlock) void lookup_fallback_out_kernel(
 }
 
 // Stage 2 of the pythonwrapper TraceIceToAir (TraceIceToAir.C:5-73), rows of 10.
+template <bool WAVE = false>
 __device__ __forceinline__ void trace_out_body(const DevMedium& M, const IceConsts& I,
                                                const QueryArgs& Q, double* __restrict__ out10,
-                                               long long k, const double* tab) {
+                                               long long k, const double* tab,
+                                               WaveRoot wr = WaveRoot{0.0, 0}) {
   double thR;
   const Geometry g = load_query<IN_TRACE>(M, Q, k, thR);
   double* o = out10 + 10 * k;
-  const double x = o[5];
-  const int st = (int)o[9];
-  const Solved S = evaluate_root(M, I, g, x, st, tab);
+  const double x = WAVE ? wr.root : o[5];
+  const int st = WAVE ? wr.status : (int)o[9];
+  const Solved S = WAVE ? evaluate_root_wave(M, I, g, x, st, tab) : evaluate_root(M, I, g, x, st, tab);
+  if (WAVE && threadIdx.x != 0) return;
   const double thd = S.thd_ice + S.thd_air;
   const double aoi = k_asin((S.ice_n / I.ice0.n) * sin_start(S.inc * M.d2r)) * M.r2d;
   if (check_solution(thd, g.D)) {
@@ -1599,14 +1767,17 @@ __global__ __launch_bounds__(kBlock) void trace_out_kernel(DevMedium M, IceConst
 }
 
 // One query, both stages in one launch (the scalar C++ / ctypes entry points): one wave finds the
-// root with the evaluation spread over its lanes, lane 0 parks it and runs the stage-2 body of
-// the entry point (OUT).  Bit-identical to the two batch kernels.
+// root with the evaluation spread over its lanes, then runs the stage-2 body of the entry point
+// (OUT) with its evaluation spread the same way.  Bit-identical to the two batch kernels.
 enum { OUT_SOLVE_MR = 0, OUT_SOLVE_PY = 1, OUT_HDTIP = 2, OUT_FALLBACK = 3, OUT_TRACE = 4 };
 template <int IN, int OUT>
-// (out is not __restrict__: park's slots lie inside it, written here and read by the body)
+// (of park only the exact flag is used: the root goes to the stage-2 body directly)
 __global__ __launch_bounds__(64) void scalar_solve_kernel(DevMedium M, IceConsts I, QueryArgs Q,
                                                           Park park, double* out, size_t ld,
                                                           uint8_t* flag, Signal sig) {
+#if AIRICE_SCALAR_STAMP
+  const unsigned long long c0 = __builtin_amdgcn_s_memtime(), w0 = __builtin_amdgcn_s_memrealtime();
+#endif
   __shared__ __align__(16) double s_logtab[1 << kLogTableBits][2];
   for (int t = threadIdx.x; t < (1 << kLogTableBits); t += 64) {
     s_logtab[t][0] = kLogTable[t][0];
@@ -1618,17 +1789,37 @@ __global__ __launch_bounds__(64) void scalar_solve_kernel(DevMedium M, IceConsts
     return;
   }
   double thR;
+#if AIRICE_SCALAR_STAMP
+  const unsigned long long c1 = __builtin_amdgcn_s_memtime();
+#endif
   const Geometry g = load_query<IN>(M, Q, 0, thR);
   const SolveResult r = solve_root<true>(M, I, g, thR, park.exact != 0, &s_logtab[0][0]);
-  if (threadIdx.x != 0) return;
-  park.root[0] = r.root;
-  park.status[0] = (double)r.status;
+#if AIRICE_SCALAR_STAMP
+  const unsigned long long c2 = __builtin_amdgcn_s_memtime();
+#endif
+  // every lane runs the stage-2 body (its evaluation spread over the wave); lane 0 writes
   const double* tab = &s_logtab[0][0];
-  if (OUT == OUT_SOLVE_MR) solve_out_body<AIRICE_VARIANT_MULTIRAY>(M, I, Q, out, ld, flag, 0, tab);
-  if (OUT == OUT_SOLVE_PY) solve_out_body<AIRICE_VARIANT_PYWRAPPER>(M, I, Q, out, ld, flag, 0, tab);
-  if (OUT == OUT_HDTIP) hdtip_out_body(M, I, Q, out, ld, flag, 0, tab);
-  if (OUT == OUT_FALLBACK) lookup_fallback_out_body(M, I, Q, out, ld, flag, 0, tab);
-  if (OUT == OUT_TRACE) trace_out_body(M, I, Q, out, 0, tab);
+  const WaveRoot wr{r.root, r.status};
+  if (OUT == OUT_SOLVE_MR)
+    solve_out_body<AIRICE_VARIANT_MULTIRAY, true>(M, I, Q, out, ld, flag, 0, tab, wr);
+  if (OUT == OUT_SOLVE_PY)
+    solve_out_body<AIRICE_VARIANT_PYWRAPPER, true>(M, I, Q, out, ld, flag, 0, tab, wr);
+  if (OUT == OUT_HDTIP) hdtip_out_body<true>(M, I, Q, out, ld, flag, 0, tab, wr);
+  if (OUT == OUT_FALLBACK) lookup_fallback_out_body<true>(M, I, Q, out, ld, flag, 0, tab, wr);
+  if (OUT == OUT_TRACE) trace_out_body<true>(M, I, Q, out, 0, tab, wr);
+  if (threadIdx.x != 0) return;
+#if AIRICE_SCALAR_STAMP
+  const unsigned long long c3 = __builtin_amdgcn_s_memtime(), w3 = __builtin_amdgcn_s_memrealtime();
+  out[17 * ld] = (double)(c1 - c0);
+  out[18 * ld] = (double)(c2 - c1);
+  out[19 * ld] = (double)(c3 - c2);
+  out[20 * ld] = (double)(c3 - c0);
+  out[21 * ld] = (double)(w3 - w0);
+  out[22 * ld] = (double)r.n_eval;
+  out[23 * ld] = (double)r.n_inside;
+  out[24 * ld] = (double)r.t_setup;
+  out[25 * ld] = (double)r.t_lean;
+#endif
   signal_done(sig);
 }
 
