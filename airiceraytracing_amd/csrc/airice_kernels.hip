@@ -51,6 +51,9 @@ constexpr int kTableBlock = AIRICE_TABLE_BS;
 // with e.g. -DAIRICE_TWO_RAY_MIN=524288 -DAIRICE_TWO_RAY_MAX=917504.
 // AIRICE_TABLE_R2=0 leaves the R = 2 kernel out of the build (co-compiled template variants can
 // perturb each other's register allocation)
+#ifndef AIRICE_SCALAR_LDSLOG
+#define AIRICE_SCALAR_LDSLOG 0
+#endif
 #ifndef AIRICE_SCALAR_STAMP
 #define AIRICE_SCALAR_STAMP 0
 #endif
@@ -871,6 +874,13 @@ __device__ __forceinline__ SolveResult solve_root(const DevMedium& M, const IceC
   const int t_setup = (int)(__builtin_amdgcn_s_memtime() - ts0) + (int)(0.0 * (lo + hi));
 #endif
   while (phase != PH_DONE) {
+    if constexpr (WAVE) {
+      // one query per wave: the phase and the counters are the same on every lane; scalar copies
+      // let the phase dispatch branch on SCC instead of exec masks
+      phase = __builtin_amdgcn_readfirstlane(phase);
+      est = __builtin_amdgcn_readfirstlane(est);
+      iter = __builtin_amdgcn_readfirstlane(iter);
+    }
     if (phase == PH_BISECT) {
       // steps that need no evaluation: an exact zero at a bracket end (GSL returns that end),
       // or a midpoint inside a guard region, whose sign is the region's: lo (left) or hi
@@ -1778,12 +1788,19 @@ __global__ __launch_bounds__(64) void scalar_solve_kernel(DevMedium M, IceConsts
 #if AIRICE_SCALAR_STAMP
   const unsigned long long c0 = __builtin_amdgcn_s_memtime(), w0 = __builtin_amdgcn_s_memrealtime();
 #endif
+#if AIRICE_SCALAR_LDSLOG
   __shared__ __align__(16) double s_logtab[1 << kLogTableBits][2];
   for (int t = threadIdx.x; t < (1 << kLogTableBits); t += 64) {
     s_logtab[t][0] = kLogTable[t][0];
     s_logtab[t][1] = kLogTable[t][1];
   }
   __syncthreads();
+  const double* tab = &s_logtab[0][0];
+#else
+  // one wave and a handful of logarithms per evaluation: the log table is read from global
+  // memory (L1 / L2 after the first call) instead of being staged in LDS first
+  const double* tab = &kLogTable[0][0];
+#endif
   if (IN == IN_CM100 && !(Q.mask[0] & AIRICE_LOOKUP_FALLBACK)) {
     if (threadIdx.x == 0) signal_done(sig);
     return;
@@ -1793,12 +1810,11 @@ __global__ __launch_bounds__(64) void scalar_solve_kernel(DevMedium M, IceConsts
   const unsigned long long c1 = __builtin_amdgcn_s_memtime();
 #endif
   const Geometry g = load_query<IN>(M, Q, 0, thR);
-  const SolveResult r = solve_root<true>(M, I, g, thR, park.exact != 0, &s_logtab[0][0]);
+  const SolveResult r = solve_root<true>(M, I, g, thR, park.exact != 0, tab);
 #if AIRICE_SCALAR_STAMP
   const unsigned long long c2 = __builtin_amdgcn_s_memtime();
 #endif
   // every lane runs the stage-2 body (its evaluation spread over the wave); lane 0 writes
-  const double* tab = &s_logtab[0][0];
   const WaveRoot wr{r.root, r.status};
   if (OUT == OUT_SOLVE_MR)
     solve_out_body<AIRICE_VARIANT_MULTIRAY, true>(M, I, Q, out, ld, flag, 0, tab, wr);
