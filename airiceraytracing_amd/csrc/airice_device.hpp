@@ -466,9 +466,13 @@ __device__ __forceinline__ void fresnel_trans(double n1, double n2, double theta
 // Completion signal of a one-query launch (ScalarCall::arm, airice_runtime.cpp): the thread that
 // wrote the call's last output makes its stores visible to the host, then stores seq into the
 // pinned, device-mapped flag the calling host thread spins on.  flag == nullptr: no signal.
+// n_in > 0: the query's inputs (the values the call also wrote to the slot) travel here, in the
+// kernel arguments, so the kernel does not read them back from host memory over PCIe.
 struct Signal {
   unsigned* flag;
   unsigned seq;
+  int n_in;
+  double in[4];
 };
 __device__ __forceinline__ void signal_done(const Signal& s) {
   if (s.flag == nullptr) return;

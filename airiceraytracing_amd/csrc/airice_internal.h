@@ -83,8 +83,9 @@ class ScalarCall {
   ~ScalarCall();
   bool ok() const { return slot_ != nullptr; }
   ScalarSlot& slot() { return *slot_; }
-  // Arms the completion signal for the next launch on this thread (the call's only kernel).
-  void arm();
+  // Arms the completion signal for the next launch on this thread (the call's only kernel);
+  // in[0 .. n_in-1] (n_in <= 4): the query inputs in the launcher's order, passed inline.
+  void arm(const double* in = nullptr, int n_in = 0);
   // Waits for the call: on the flag when the armed signal was taken by a launcher (falling back
   // to the stream after a bounded spin), else on the slot's stream; AIRICE_OK or AIRICE_EHIP.
   int sync();
@@ -93,7 +94,7 @@ class ScalarCall {
   void* lock_ = nullptr;
   bool armed_ = false;
 };
-// The armed signal of this thread (cleared by taking it); {nullptr, 0} when none is armed.
+// The armed signal of this thread (cleared by taking it); Signal{} when none is armed.
 Signal take_scalar_signal();
 // The table lookup's minimizer fallback for one query that lk_query flagged one-sided
 // (.cc:1418-1420), on the device through the scalar slot: out9 / *ok as the batch lookup.

@@ -486,7 +486,8 @@ __global__ __launch_bounds__(kBlock) void rays_kernel(DevMedium M, IceConsts I,
   const long long k = (long long)blockIdx.x * kBlock + threadIdx.x;
   if (k >= n) return;
   double d[18];
-  ray_solution(M, I, launch[k], txh[k], in_ice != 0, d);
+  const bool inl = sig.n_in >= 2;  // one-ray call: its inputs in the kernel arguments
+  ray_solution(M, I, inl ? sig.in[0] : launch[k], inl ? sig.in[1] : txh[k], in_ice != 0, d);
 #pragma unroll
   for (int c = 0; c < 18; ++c) out[c * ld + k] = d[c];
   if (k == 0) signal_done(sig);  // armed for one-ray calls only
@@ -735,6 +736,7 @@ struct SolveResult {
   int n_eval, n_est, n_inside;  // evaluations: all, secant search, bisection midpoints (stats)
 #if AIRICE_SCALAR_STAMP
   int t_setup = 0, t_lean = 0;  // debug: shader clocks of the set-up and of the lean bisection runs
+  int t_pre = 0, t_post = 0;    //        loop top -> evaluation, evaluation -> loop top
 #endif
 };
 
@@ -873,6 +875,10 @@ __device__ __forceinline__ SolveResult solve_root(const DevMedium& M, const IceC
 #if AIRICE_SCALAR_STAMP
   const int t_setup = (int)(__builtin_amdgcn_s_memtime() - ts0) + (int)(0.0 * (lo + hi));
 #endif
+#if AIRICE_SCALAR_STAMP
+  int t_pre = 0, t_post = 0;
+  unsigned long long tq = __builtin_amdgcn_s_memtime();
+#endif
   while (phase != PH_DONE) {
     if constexpr (WAVE) {
       // one query per wave: the phase and the counters are the same on every lane; scalar copies
@@ -987,11 +993,13 @@ __device__ __forceinline__ SolveResult solve_root(const DevMedium& M, const IceC
         const double xb = phase == PH_FLO ? hi : x2 + dlt;
 #if AIRICE_SCALAR_STAMP
         const unsigned long long e0 = __builtin_amdgcn_s_memtime();
+        t_pre += (int)(e0 - tq) + (int)(0.0 * x);
 #endif
         eval_thd_wave(M, I, q, x, pair ? xb : x, tab, thd_air, thd_ice, next_air, next_ice);
 #if AIRICE_SCALAR_STAMP
         // debug: evaluation ticks in n_inside (the wave form does not count midpoints)
-        n_inside += (int)(__builtin_amdgcn_s_memtime() - e0) + (int)(0.0 * (thd_air + thd_ice));
+        tq = __builtin_amdgcn_s_memtime();
+        n_inside += (int)(tq - e0) + (int)(0.0 * (thd_air + thd_ice));
 #endif
         have_next = pair;
       }
@@ -1106,11 +1114,20 @@ __device__ __forceinline__ SolveResult solve_root(const DevMedium& M, const IceC
       }
       finish(frozen);
     }
+#if AIRICE_SCALAR_STAMP
+    if constexpr (WAVE) {
+      const unsigned long long te = __builtin_amdgcn_s_memtime();
+      t_post += (int)(te - tq) + (int)(0.0 * (lo + hi + x2));
+      tq = te;
+    }
+#endif
   }
 #if AIRICE_SCALAR_STAMP
   SolveResult sr{root_zero ? 0.0 : 0.5 * (lo + hi), status, n_eval, est, n_inside};
   sr.t_setup = t_setup;
   sr.t_lean = t_lean;
+  sr.t_pre = t_pre;
+  sr.t_post = t_post;
   return sr;
 #else
   return SolveResult{root_zero ? 0.0 : 0.5 * (lo + hi), status, n_eval, est, n_inside};
@@ -1185,23 +1202,19 @@ __device__ __forceinline__ Solved evaluate_root_wave(const DevMedium& M, const I
                                                      const Geometry& g, double x, int status,
                                                      const double* tab) {
   const int lane = (int)(threadIdx.x & 63);
+  // branch-free (selects on wave-uniform conditions): one straight block, so the angle chains
+  // (asin of the incidence and of the receive angle) overlap the segments
   Solved S;
-  S.status = status;
   S.launch = x;
   const AirPath P = make_air_path(M, g.H, g.ice);
   S.ice_n = P.iceair.n;
-  S.thd_air = 0.0;
-  S.t_air = 0.0;
-  S.geo_air = 0.0;
-  S.inc = __builtin_nan("");
   const bool air = !(P.top < P.bot);
-  double L0 = __builtin_nan(""), v2 = 0.0;
-  if (air) {
-    v2 = first_layer_v2(M, P.tx.n, P.rtop.n, x);
-    L0 = P.rtop.n * v2;
-  } else {
-    S.status |= AIRICE_SOLVE_NO_AIR_LAYER;
-  }
+  S.status = air ? status : (status | AIRICE_SOLVE_NO_AIR_LAYER);
+  const double v2 = first_layer_v2(M, P.tx.n, P.rtop.n, x);
+  const double L0 = air ? P.rtop.n * v2 : __builtin_nan("");
+  const double inc = k_asin(P.top == P.bot ? v2 : L0 / P.iceair.n) * M.r2d;
+  const Endpoint rx = ice_endpoint(M, g.depth_pos);
+  const double ant = k_asin(L0 / rx.n) * M.r2d;
   // lanes 0-3: the air segments, with the kernel-uniform A as evaluate_root has it (the same
   // instruction forms, hence also the same NaN bits on rays without a solution)
   const double A2 = M.A_air * M.A_air;
@@ -1215,33 +1228,30 @@ __device__ __forceinline__ Solved evaluate_root_wave(const DevMedium& M, const I
   R = pick(lane == 3, P.iceair, R);
   const Segment sg = segment(T, R, M.A_air, A2, RL, true, tab);
   // the segment in the ice on every lane, beside the air segments (used when g.depth < 0)
-  const Endpoint rx = ice_endpoint(M, g.depth_pos);
   const double A2i = M.A_ice * M.A_ice;
   const RayL RLi = ray_L(A2i, L0);
   const Segment si = segment(I.ice0, rx, M.A_ice, A2i, RLi, false, tab);
   auto from = [&](int l) { return Segment{__shfl(sg.thd, l), __shfl(sg.t, l), __shfl(sg.geo, l)}; };
-  if (air) {
-    auto add = [&](const Segment& a) {
-      S.thd_air += a.thd;
-      S.t_air += a.t;
-      S.geo_air += a.geo;
-    };
-    add(from(0));
-    if (2 < P.top && 2 > P.bot) add(from(1));
-    if (1 < P.top && 1 > P.bot) add(from(2));
-    if (P.top > P.bot) add(from(3));
-    S.inc = k_asin(P.top == P.bot ? v2 : L0 / P.iceair.n) * M.r2d;
-  }
-  S.thd_ice = 0.0;
-  S.t_ice = 0.0;
-  S.geo_ice = 0.0;
-  S.ant = 0.0;
-  if (g.depth < 0) {
-    S.thd_ice = si.thd;
-    S.ant = k_asin(L0 / rx.n) * M.r2d;
-    S.t_ice = si.t;
-    S.geo_ice = si.geo;
-  }
+  const Segment s0 = from(0), s1 = from(1), s2 = from(2), s3 = from(3);
+  double thd = 0.0, t = 0.0, geo = 0.0;
+  auto add = [&](bool c, const Segment& a) {
+    thd = c ? thd + a.thd : thd;
+    t = c ? t + a.t : t;
+    geo = c ? geo + a.geo : geo;
+  };
+  add(air, s0);
+  add(air && 2 < P.top && 2 > P.bot, s1);
+  add(air && 1 < P.top && 1 > P.bot, s2);
+  add(air && P.top > P.bot, s3);
+  S.thd_air = thd;
+  S.t_air = t;
+  S.geo_air = geo;
+  S.inc = air ? inc : __builtin_nan("");
+  const bool in_ice = g.depth < 0;
+  S.thd_ice = in_ice ? si.thd : 0.0;
+  S.t_ice = in_ice ? si.t : 0.0;
+  S.geo_ice = in_ice ? si.geo : 0.0;
+  S.ant = in_ice ? ant : 0.0;
   return S;
 }
 
@@ -1250,6 +1260,7 @@ __device__ __forceinline__ Solved evaluate_root_wave(const DevMedium& M, const I
 struct WaveRoot {
   double root;
   int status;
+  Geometry g;  // the query, as load_query gave it to the root finder
 };
 
 __device__ __forceinline__ double straight_angle(const DevMedium& M, double H, double D, double ice,
@@ -1277,33 +1288,38 @@ struct QueryArgs {
   const uint8_t* mask;  // IN_CM100: only lanes with AIRICE_LOOKUP_FALLBACK set
 };
 
+// inl: a one-query call whose inputs arrived in the kernel arguments (Signal::in, the same values
+// as Q's arrays hold), read from there instead of from host memory.
 template <int IN>
 __device__ __forceinline__ Geometry load_query(const DevMedium& M, const QueryArgs& Q, long long k,
-                                               double& thR) {
+                                               double& thR, const Signal* inl = nullptr) {
+  const double qa = inl ? inl->in[0] : Q.a[k];
+  const double qb = inl ? inl->in[1] : Q.b[k];
+  const double qc = inl ? inl->in[2] : Q.c[k];
   double H, D, ice, dep;
   if (IN == IN_M) {
-    H = Q.a[k];
-    D = Q.b[k];
-    dep = Q.c[k];
+    H = qa;
+    D = qb;
+    dep = qc;
     ice = Q.ice;
-    thR = Q.d != nullptr ? Q.d[k] : straight_angle(M, H, D, ice, dep);
+    thR = Q.d != nullptr ? (inl ? inl->in[3] : Q.d[k]) : straight_angle(M, H, D, ice, dep);
   } else if (IN == IN_CM) {
-    H = Q.a[k] / 100;
-    D = Q.b[k] / 100;
+    H = qa / 100;
+    D = qb / 100;
     ice = Q.ice / 100;
-    dep = Q.c[k] / 100;
+    dep = qc / 100;
     thR = straight_angle(M, H, D, ice, dep);
   } else if (IN == IN_CM100) {
-    H = (Q.a[k] * 100) / 100;
-    D = (Q.b[k] * 100) / 100;
+    H = (qa * 100) / 100;
+    D = (qb * 100) / 100;
     ice = Q.ice / 100;
-    dep = (Q.c[k] * 100) / 100;
+    dep = (qc * 100) / 100;
     thR = straight_angle(M, H, D, ice, dep);
   } else {
-    dep = Q.a[k];
-    ice = Q.b[k];
-    H = Q.c[k];
-    D = Q.d[k];
+    dep = qa;
+    ice = qb;
+    H = qc;
+    D = inl ? inl->in[3] : Q.d[k];
     thR = straight_angle(M, H, D, ice, dep);
   }
   return shift(H, D, ice, dep);
@@ -1604,7 +1620,7 @@ __device__ __forceinline__ void solve_out_body(const DevMedium& M, const IceCons
                                                long long k, const double* tab,
                                                WaveRoot wr = WaveRoot{0.0, 0}) {
   double thR;
-  const Geometry g = load_query<IN_M>(M, Q, k, thR);
+  const Geometry g = WAVE ? wr.g : load_query<IN_M>(M, Q, k, thR);
   const double x = WAVE ? wr.root : out[10 * ld + k];
   const int st = WAVE ? wr.status : (int)out[0 * ld + k];
   const Solved S = WAVE ? evaluate_root_wave(M, I, g, x, st, tab) : evaluate_root(M, I, g, x, st, tab);
@@ -1658,7 +1674,7 @@ __device__ __forceinline__ void hdtip_out_body(const DevMedium& M, const IceCons
                                                size_t ld, uint8_t* __restrict__ ok, long long k,
                                                const double* tab, WaveRoot wr = WaveRoot{0.0, 0}) {
   double thR;
-  const Geometry g = load_query<IN_CM>(M, Q, k, thR);
+  const Geometry g = WAVE ? wr.g : load_query<IN_CM>(M, Q, k, thR);
   const double x = WAVE ? wr.root : out[4 * ld + k];
   const int st = WAVE ? wr.status : (int)out[0 * ld + k];
   const Solved S = WAVE ? evaluate_root_wave(M, I, g, x, st, tab) : evaluate_root(M, I, g, x, st, tab);
@@ -1702,7 +1718,7 @@ __device__ __forceinline__ void lookup_fallback_out_body(const DevMedium& M, con
                                                          WaveRoot wr = WaveRoot{0.0, 0}) {
   if (!(Q.mask[k] & AIRICE_LOOKUP_FALLBACK)) return;
   double thR;
-  const Geometry g = load_query<IN_CM100>(M, Q, k, thR);
+  const Geometry g = WAVE ? wr.g : load_query<IN_CM100>(M, Q, k, thR);
   const double x = WAVE ? wr.root : out[4 * ld + k];
   const int st = WAVE ? wr.status : (int)out[0 * ld + k];
   const Solved S = WAVE ? evaluate_root_wave(M, I, g, x, st, tab) : evaluate_root(M, I, g, x, st, tab);
@@ -1741,7 +1757,7 @@ __device__ __forceinline__ void trace_out_body(const DevMedium& M, const IceCons
                                                long long k, const double* tab,
                                                WaveRoot wr = WaveRoot{0.0, 0}) {
   double thR;
-  const Geometry g = load_query<IN_TRACE>(M, Q, k, thR);
+  const Geometry g = WAVE ? wr.g : load_query<IN_TRACE>(M, Q, k, thR);
   double* o = out10 + 10 * k;
   const double x = WAVE ? wr.root : o[5];
   const int st = WAVE ? wr.status : (int)o[9];
@@ -1809,13 +1825,16 @@ __global__ __launch_bounds__(64) void scalar_solve_kernel(DevMedium M, IceConsts
 #if AIRICE_SCALAR_STAMP
   const unsigned long long c1 = __builtin_amdgcn_s_memtime();
 #endif
-  const Geometry g = load_query<IN>(M, Q, 0, thR);
+  const Geometry g = load_query<IN>(M, Q, 0, thR, 
+                                    sig.n_in >= ((IN == IN_TRACE || (IN == IN_M && Q.d != nullptr)) ? 4 : 3)
+                                        ? &sig
+                                        : nullptr);
   const SolveResult r = solve_root<true>(M, I, g, thR, park.exact != 0, tab);
 #if AIRICE_SCALAR_STAMP
   const unsigned long long c2 = __builtin_amdgcn_s_memtime();
 #endif
   // every lane runs the stage-2 body (its evaluation spread over the wave); lane 0 writes
-  const WaveRoot wr{r.root, r.status};
+  const WaveRoot wr{r.root, r.status, g};
   if (OUT == OUT_SOLVE_MR)
     solve_out_body<AIRICE_VARIANT_MULTIRAY, true>(M, I, Q, out, ld, flag, 0, tab, wr);
   if (OUT == OUT_SOLVE_PY)
@@ -1835,6 +1854,8 @@ __global__ __launch_bounds__(64) void scalar_solve_kernel(DevMedium M, IceConsts
   out[23 * ld] = (double)r.n_inside;
   out[24 * ld] = (double)r.t_setup;
   out[25 * ld] = (double)r.t_lean;
+  out[26 * ld] = (double)r.t_pre;
+  out[27 * ld] = (double)r.t_post;
 #endif
   signal_done(sig);
 }
@@ -2107,7 +2128,7 @@ int launch_table_multi(const DevMedium& M, const IceConsts* Ih, const airice_gri
 int launch_rays(const DevMedium& M, const IceConsts& I, const double* launch, const double* txh,
                 int in_ice, size_t n, double* out, size_t ld, hipStream_t st) {
   if (n == 0) return AIRICE_OK;
-  const Signal sig = n == 1 ? take_scalar_signal() : Signal{nullptr, 0};
+  const Signal sig = n == 1 ? take_scalar_signal() : Signal{};
   hipLaunchKernelGGL(rays_kernel, dim3(grid_for((long long)n)), dim3(kBlock), 0, st, M, I, launch,
                      txh, in_ice, (long long)n, out, ld, sig);
   return launch_ok();

@@ -285,12 +285,12 @@ struct SlotEntry {
 };
 std::mutex g_slots_mu;
 std::vector<SlotEntry*> g_slots;  // by device ordinal; never freed (process lifetime)
-thread_local Signal t_signal{nullptr, 0};
+thread_local Signal t_signal{};
 }  // namespace
 
 Signal take_scalar_signal() {
   const Signal s = t_signal;
-  t_signal = Signal{nullptr, 0};
+  t_signal = Signal{};
   return s;
 }
 
@@ -336,13 +336,18 @@ ScalarCall::ScalarCall() {
 }
 
 ScalarCall::~ScalarCall() {
-  if (armed_) t_signal = Signal{nullptr, 0};  // never leave a signal armed past the call
+  if (armed_) t_signal = Signal{};  // never leave a signal armed past the call
   delete static_cast<std::unique_lock<std::mutex>*>(lock_);
 }
 
-void ScalarCall::arm() {
+void ScalarCall::arm(const double* in, int n_in) {
   if (++slot_->seq == 0) slot_->seq = 1;  // 0 is the flag's initial value
-  t_signal = Signal{slot_->flag_d, slot_->seq};
+  Signal s{};
+  s.flag = slot_->flag_d;
+  s.seq = slot_->seq;
+  s.n_in = in != nullptr ? std::min(n_in, 4) : 0;
+  for (int i = 0; i < s.n_in; ++i) s.in[i] = in[i];
+  t_signal = s;
   armed_ = true;
 }
 
@@ -350,7 +355,7 @@ int ScalarCall::sync() {
   if (armed_) {
     armed_ = false;
     const bool taken = t_signal.flag == nullptr;
-    t_signal = Signal{nullptr, 0};
+    t_signal = Signal{};
     if (taken) {
       // the kernel's outputs are visible once the flag holds seq; a launch that has not
       // signalled after ~2 ms (first-use code loading, a fault) is waited for on its stream
@@ -918,7 +923,7 @@ void Py_TraceIceToAir(double AntennaDepth, double IceLayerHeight, double AirTxHe
   sl.h[1] = IceLayerHeight;
   sl.h[2] = AirTxHeight;
   sl.h[3] = HorizontalDistance;
-  call.arm();
+  call.arm(sl.h, 4);
   if (airice_trace_ice_to_air_launch(&g_py_medium, sl.d, sl.d + 1, sl.d + 2, sl.d + 3, 1,
                                      sl.d + 4, sl.st) != AIRICE_OK ||
       call.sync() != AIRICE_OK) {

@@ -375,7 +375,7 @@ void Air2IceRayTracing(double AirTxHeight, double HorizontalDistance, double Ice
   s.h[1] = HorizontalDistance;
   s.h[2] = AntennaDepth;
   s.h[3] = StraightAngle;
-  call.arm();
+  call.arm(s.h, 4);
   if (airice_solve_launch(&m, AIRICE_VARIANT_MULTIRAY, IceLayerHeight, s.d, s.d + 1, s.d + 2,
                           s.d + 3, 1, s.d + 4, 1, nullptr, s.st) != AIRICE_OK ||
       call.sync() != AIRICE_OK)
@@ -391,7 +391,7 @@ void GetRayTracingSolutions(double RayLaunchAngleInAir, double AirTxHeight, doub
   airice::ScalarSlot& s = call.slot();
   s.h[0] = RayLaunchAngleInAir;
   s.h[1] = AirTxHeight;
-  call.arm();
+  call.arm(s.h, 2);
   if (airice_rays_launch(&m, s.d, s.d + 1, IceLayerHeight, AntennaDepth, InIce ? 1 : 0, 1,
                          s.d + 2, 1, s.st) != AIRICE_OK ||
       call.sync() != AIRICE_OK)
@@ -414,7 +414,7 @@ bool GetHorizontalDistanceToIntersectionPoint(
   s.h[2] = RxDepthBelowIceBoundary;
   uint8_t* ok_h = reinterpret_cast<uint8_t*>(s.h + 12);
   uint8_t* ok_d = reinterpret_cast<uint8_t*>(s.d + 12);
-  call.arm();
+  call.arm(s.h, 3);
   if (airice_hdtip_launch(&m, s.d, s.d + 1, s.d + 2, IceLayerHeight, 1, s.d + 3, 1, ok_d, s.st) !=
           AIRICE_OK ||
       call.sync() != AIRICE_OK)
