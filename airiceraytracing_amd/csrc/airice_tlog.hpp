@@ -26,6 +26,16 @@
 
 #include "airice_logtab.h"
 
+#ifndef AIRICE_LEAN_ESTRIN
+#define AIRICE_LEAN_ESTRIN 0  // measured: no faster than Horner
+#endif
+// Degree of tlog_lean's log1p(r) polynomial: 5 (default; truncation <= 2^-50.6 absolute) or
+// 6 / 7 (the full form).  Degree 5 vs 7: cfg2 table 2.8 % and cfg3 solves 2 % faster, float
+// table bit-identical (tools/ab_table.py, tools/gpu_ab_solve.sh).
+#ifndef AIRICE_LEAN_DEG
+#define AIRICE_LEAN_DEG 5
+#endif
+
 namespace airice {
 
 // A polynomial coefficient held in an SGPR pair: the fma then issues as one VOP3 v_fma_f64 with the
@@ -88,10 +98,12 @@ __host__ __device__ AIRICE_INLINE double tlog_pos(double x, const double* tab = 
 }
 
 // log(x) for x positive, normal and finite, without the hi + lo bookkeeping: w = k ln2 + log c_i
-// by one fma, then w + (r + r^2 q).  ~10 FP64 ops instead of ~19; error <= 2 ulp (|w| >= 0.318
-// or 0 and |r| <= 2^-8, so the two roundings of the final sum and of w dominate; measured in
-// tests/test_tlog.py).  The ray kernels' log ratios use this form: their outputs are built from
-// differences of O(1) terms, so an ulp in one logarithm is an ulp-level absolute error there.
+// by one fma, then w + (r + r^2 q) with q of degree AIRICE_LEAN_DEG - 2 in r.  ~8 FP64 ops
+// instead of ~19.  Error bounded in ABSOLUTE terms: <= ~3 ulp of max(|log x|, 1) at degree 5
+// (truncation |r|^6/6 <= 2^-50.6 for |r| <= 2^-8, plus the roundings of w and the final sum;
+// 2 ulp at degree 7), measured in tests/test_tlog.py.  The ray kernels' log ratios use this
+// form: their outputs are built from differences of O(1) terms, so the absolute error of one
+// logarithm is what reaches them.
 __host__ __device__ AIRICE_INLINE double tlog_lean(double x, const double* tab = &kLogTable[0][0]) {
   const double Ln2 = 0x1.62e42fefa39efp-1;
   const double A0 = -0x1p-1, A1 = 0x1.5555555555555p-2, A2 = -0x1p-2, A3 = 0x1.999999999999ap-3,
@@ -106,11 +118,30 @@ __host__ __device__ AIRICE_INLINE double tlog_lean(double x, const double* tab =
   const double r = AIRICE_FMA(z, invc, -1.0);
   const double w = AIRICE_FMA((double)k, Ln2, logc);
   const double r2 = r * r;
+#if AIRICE_LEAN_ESTRIN
+  // the same polynomial with a 3-deep instead of a 5-deep dependent chain (pairs in r, then r^2)
+  const double p01 = AIRICE_FMA(r, kc(A1), kc(A0));
+  const double p23 = AIRICE_FMA(r, kc(A3), kc(A2));
+  const double p45 = AIRICE_FMA(r, A5, kc(A4));
+  const double q = AIRICE_FMA(r2, AIRICE_FMA(r2, p45, p23), p01);
+#elif AIRICE_LEAN_DEG == 5
+  // through r^5: truncation |r|^6 / 6 <= 2^-50.6 absolute
+  double q = AIRICE_FMA(r, kc(A3), kc(A2));
+  q = AIRICE_FMA(r, q, kc(A1));
+  q = AIRICE_FMA(r, q, kc(A0));
+#elif AIRICE_LEAN_DEG == 6
+  // through r^6: truncation |r|^7 / 7 <= 2^-58.8 absolute
+  double q = AIRICE_FMA(r, kc(A4), kc(A3));
+  q = AIRICE_FMA(r, q, kc(A2));
+  q = AIRICE_FMA(r, q, kc(A1));
+  q = AIRICE_FMA(r, q, kc(A0));
+#else
   double q = AIRICE_FMA(r, A5, kc(A4));
   q = AIRICE_FMA(r, q, kc(A3));
   q = AIRICE_FMA(r, q, kc(A2));
   q = AIRICE_FMA(r, q, kc(A1));
   q = AIRICE_FMA(r, q, kc(A0));
+#endif
   return AIRICE_FMA(r2, q, r) + w;
 }
 

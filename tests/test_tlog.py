@@ -68,9 +68,11 @@ def test_twin_against_mpmath(tmp_path):
 
 
 def test_lean_twin_within_two_ulps(tmp_path):
-    """tlog_lean (the log-ratio logarithm of the ray kernels): no hi + lo bookkeeping."""
+    """tlog_lean (the log-ratio logarithm of the ray kernels): no hi + lo bookkeeping and a
+    degree-5 log1p polynomial, so its bound is absolute: ulps of max(|log x|, 1).  (Relative to
+    log x it reaches ~1,400 ulp next to x = 1, where log x ~ 2^-8: ~2^-50.6 absolute.)"""
     rep, _ = _cpu(tmp_path, lean=True)
-    assert rep["max_ulp"] < 2.5, rep  # 1.91 measured
+    assert rep["max_ulp_floor1"] < 3.5, rep  # 2.89 measured (degree 7: 1.91)
 
 
 @pytest.mark.gpu
