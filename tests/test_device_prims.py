@@ -82,7 +82,9 @@ def test_device_primitives(tmp_path):
         lr = (np.log(a.astype(np.longdouble)) - np.log(b.astype(np.longdouble))).astype(np.float64)
     fin = np.isfinite(lr)
     err = np.abs(o[fin, 5] - lr[fin]) / np.maximum(np.spacing(np.abs(lr[fin])), 2.0**-53)
-    assert err.max() <= 4.0, err.max()
+    # absolute error of the degree-5 lean log (<= 2.9 x 2^-52, tests/test_tlog.py) plus the
+    # quotient's rounding: 6 units of 2^-53 measured (degree 7: 4)
+    assert err.max() <= 8.0, err.max()
     assert np.array_equal(o[~fin, 5], lr[~fin], equal_nan=True), (a[~fin], b[~fin], o[~fin, 5])
     # mpmath sample for asin
     mpmath = pytest.importorskip("mpmath")
