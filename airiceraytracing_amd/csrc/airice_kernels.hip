@@ -396,7 +396,7 @@ __device__ __forceinline__ void table_block(const DevMedium& M, const IceConsts&
                                             WaveTrace* __restrict__ trace, unsigned block) {
   extern __shared__ __align__(16) unsigned char smem[];
   RowConst* rows = reinterpret_cast<RowConst*>(smem);
-  // the log table (4 KB) staged in LDS: 16-byte entries, (1 << kLogTableBits) / BS per thread
+  // the log table (16 B x 2^kLogTableBits) staged in LDS: 16-byte entries, (1 << kLogTableBits) / BS per thread
   __shared__ __align__(16) double s_logtab[1 << kLogTableBits][2];
 #pragma unroll
   for (unsigned t = threadIdx.x; t < (1u << kLogTableBits); t += BS) {
@@ -1391,10 +1391,9 @@ __global__ __launch_bounds__(kRootsBlock, AIRICE_ROOTS_WAVES) void roots_kernel(
   // the log table in LDS (one 16-byte entry per thread), as in table_kernel: every evaluation's
   // log ratios read it instead of global memory
   __shared__ __align__(16) double s_logtab[1 << kLogTableBits][2];
-  static_assert(kRootsBlock >= (1 << kLogTableBits), "one table entry per thread");
-  if (threadIdx.x < (1u << kLogTableBits)) {
-    s_logtab[threadIdx.x][0] = kLogTable[threadIdx.x][0];
-    s_logtab[threadIdx.x][1] = kLogTable[threadIdx.x][1];
+  for (unsigned t = threadIdx.x; t < (1u << kLogTableBits); t += kRootsBlock) {
+    s_logtab[t][0] = kLogTable[t][0];
+    s_logtab[t][1] = kLogTable[t][1];
   }
   const long long k0 = (long long)blockIdx.x * kRootsBlock;
   const long long kt = k0 + threadIdx.x;
@@ -1599,11 +1598,12 @@ __device__ __forceinline__ bool check_solution(double thd, double D) {
   return good;
 }
 
-// The stage-2 kernels read the log table from LDS like the solve (one entry per thread).
-static_assert(kBlock == (1 << kLogTableBits), "one log-table entry per thread");
+// The stage-2 kernels read the log table from LDS like the solve.
 __device__ __forceinline__ void stage_log_table(double (*s)[2]) {
-  s[threadIdx.x][0] = kLogTable[threadIdx.x][0];
-  s[threadIdx.x][1] = kLogTable[threadIdx.x][1];
+  for (unsigned t = threadIdx.x; t < (1u << kLogTableBits); t += kBlock) {
+    s[t][0] = kLogTable[t][0];
+    s[t][1] = kLogTable[t][1];
+  }
   __syncthreads();
 }
 

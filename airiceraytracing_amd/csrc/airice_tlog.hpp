@@ -124,6 +124,10 @@ __host__ __device__ AIRICE_INLINE double tlog_lean(double x, const double* tab =
   const double p23 = AIRICE_FMA(r, kc(A3), kc(A2));
   const double p45 = AIRICE_FMA(r, A5, kc(A4));
   const double q = AIRICE_FMA(r2, AIRICE_FMA(r2, p45, p23), p01);
+#elif AIRICE_LEAN_DEG == 4
+  // through r^4 (for a table of >= 1024 entries, |r| <= 2^-11: truncation <= 2^-57.3 absolute)
+  double q = AIRICE_FMA(r, kc(A2), kc(A1));
+  q = AIRICE_FMA(r, q, kc(A0));
 #elif AIRICE_LEAN_DEG == 5
   // through r^5: truncation |r|^6 / 6 <= 2^-50.6 absolute
   double q = AIRICE_FMA(r, kc(A3), kc(A2));
