@@ -133,7 +133,8 @@ EXPORTED_SYMBOLS = (
     "airice_table_host", "airice_rays_launch", "airice_solve_launch", "airice_solve_host",
     "airice_hdtip_launch", "airice_table_lookup_launch", "airice_lookup_pack", "airice_single_ray_plan",
     "airice_single_ray_launch", "airice_single_ray_host", "airice_trace_ice_to_air_launch",
-    "airice_trace_ice_to_air_host", "airice_rtf_outputs", "airice_rtf_eval", "Py_TraceIceToAir", "airice_device_count", "airice_set_device", "airice_malloc",
+    "airice_trace_ice_to_air_host", "airice_rtf_outputs", "airice_rtf_eval",
+    "airice_rtf_eval_variant", "Py_TraceIceToAir", "airice_device_count", "airice_set_device", "airice_malloc",
     "airice_free", "airice_memcpy_h2d", "airice_memcpy_d2h", "airice_synchronize",
     "airice_kernel_timing", "airice_kernel_time",
 )
@@ -196,6 +197,7 @@ def lib() -> ctypes.CDLL:
         "airice_single_ray_host": ([M, D, D, D, D, P, P, P, S], I),
         "airice_rtf_outputs": ([I, I], I),
         "airice_rtf_eval": ([M, I, P, S, P, S], I),
+        "airice_rtf_eval_variant": ([M, I, I, P, S, P, S], I),
         "airice_trace_ice_to_air_launch": ([M, P, P, P, P, S, P, P], I),
         "airice_trace_ice_to_air_host": ([M, P, P, P, P, S, P], I),
         "Py_TraceIceToAir": ([D, D, D, D, ctypes.POINTER(D)], None),

@@ -2,6 +2,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <atomic>
 #include <mutex>
 
 #include "airice.h"
@@ -104,13 +105,13 @@ int lookup_fallback_one(const airice_medium* m, double src_cm, double dist_cm, d
 // Kernel timing for the bench (airice_kernel_timing): when enabled, launches of the kernels
 // below are bracketed by a hipEvent pair on their stream.  Off by default: one relaxed load.
 enum KTimerId { KT_TABLE = 0, KT_ROOTS, KT_GROUP, KT_OUT, KT_LOOKUP, KT_COUNT };
-extern bool g_ktimer_on;
+extern std::atomic<bool> g_ktimer_on;
 void ktimer_record(int id, bool begin, hipStream_t st);
 inline void ktimer_begin(int id, hipStream_t st) {
-  if (g_ktimer_on) ktimer_record(id, true, st);
+  if (g_ktimer_on.load(std::memory_order_relaxed)) ktimer_record(id, true, st);
 }
 inline void ktimer_end(int id, hipStream_t st) {
-  if (g_ktimer_on) ktimer_record(id, false, st);
+  if (g_ktimer_on.load(std::memory_order_relaxed)) ktimer_record(id, false, st);
 }
 
 }  // namespace airice

@@ -2027,8 +2027,8 @@ int launch_table(const DevMedium& M, const IceConsts& I, const airice_grid* g, i
 
 // Several antennas' whole tables in one launch of table_multi_kernel.  Ih[a], grids[a]: antenna
 // a's constants and grid (the rows it holds: grids[a].table_rows); tables[a] its output, column
-// stride lds[a].  The per-antenna constants are uploaded to a device buffer that is kept and
-// reused while the same set is launched again (bench steps, repeated builds).
+// stride lds[a].  The per-antenna constants live in a device buffer per distinct set, kept for
+// repeated launches of the same set (bench steps, repeated builds).
 int launch_table_multi(const DevMedium& M, const IceConsts* Ih, const airice_grid* grids, int n,
                        float* const* tables, const size_t* lds, hipStream_t st) {
   if (n <= 0) return AIRICE_OK;
@@ -2078,42 +2078,52 @@ int launch_table_multi(const DevMedium& M, const IceConsts* Ih, const airice_gri
   }
   map.begin[n] = (int)blocks;
   if (blocks == 0) return AIRICE_OK;
-  // device copy of the per-antenna constants, reused while unchanged (per device)
-  struct Cache {
+  // Device copies of the per-antenna constants, one immutable buffer per distinct constant set
+  // (up to kConstSets per device, least recently used evicted).  A buffer is written once, by a
+  // synchronous copy before any launch reads it, and never overwritten; eviction frees it with
+  // hipFree, which waits for the kernels still reading it, on any stream.  The lock is held until
+  // the launch is enqueued, so no other thread can evict the buffer in between.
+  struct ConstSet {
     std::vector<unsigned char> host;
     void* dev = nullptr;
-    size_t cap = 0;
+    unsigned long long used = 0;
   };
+  constexpr size_t kConstSets = 8;
   static std::mutex mu;
-  static std::vector<Cache> caches;
+  static std::vector<std::vector<ConstSet>> caches;
+  static unsigned long long tick = 0;
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess) return AIRICE_EHIP;
   const size_t bytes_i = sizeof(IceConsts) * n, bytes = bytes_i + sizeof(TableArgs) * n;
   std::vector<unsigned char> packed(bytes);
   std::memcpy(packed.data(), Ih, bytes_i);
   std::memcpy(packed.data() + bytes_i, Ah.data(), sizeof(TableArgs) * n);
-  void* dconst = nullptr;
-  {
-    std::lock_guard<std::mutex> lock(mu);
-    if (caches.size() <= (size_t)dev) caches.resize(dev + 1);
-    Cache& c = caches[dev];
-    if (c.host != packed) {
-      if (c.cap < bytes) {
-        if (c.dev != nullptr) (void)hipFree(c.dev);
-        c.dev = nullptr;
-        c.cap = 0;
-        if (hipMalloc(&c.dev, bytes) != hipSuccess) return AIRICE_EHIP;
-        c.cap = bytes;
-      }
-      // ordered before this launch on st; the previous launches reading the old contents have
-      // completed when a synchronous copy returns
-      if (hipStreamSynchronize(st) != hipSuccess ||
-          hipMemcpy(c.dev, packed.data(), bytes, hipMemcpyHostToDevice) != hipSuccess)
-        return AIRICE_EHIP;
-      c.host = packed;
+  std::lock_guard<std::mutex> lock(mu);
+  if (caches.size() <= (size_t)dev) caches.resize(dev + 1);
+  std::vector<ConstSet>& sets = caches[dev];
+  ConstSet* c = nullptr;
+  for (ConstSet& e : sets)
+    if (e.host == packed) c = &e;
+  if (c == nullptr) {
+    if (sets.size() >= kConstSets) {  // evict the least recently used set
+      size_t old = 0;
+      for (size_t k = 1; k < sets.size(); ++k)
+        if (sets[k].used < sets[old].used) old = k;
+      if (hipFree(sets[old].dev) != hipSuccess) return AIRICE_EHIP;
+      sets.erase(sets.begin() + (long)old);
     }
-    dconst = c.dev;
+    ConstSet e;
+    if (hipMalloc(&e.dev, bytes) != hipSuccess) return AIRICE_EHIP;
+    if (hipMemcpy(e.dev, packed.data(), bytes, hipMemcpyHostToDevice) != hipSuccess) {
+      (void)hipFree(e.dev);
+      return AIRICE_EHIP;
+    }
+    e.host = std::move(packed);
+    sets.push_back(std::move(e));
+    c = &sets.back();
   }
+  c->used = ++tick;
+  void* dconst = c->dev;
   const size_t lds_bytes = sizeof(RowConst) * (size_t)rpb;
   ktimer_begin(KT_TABLE, st);
   hipLaunchKernelGGL(table_multi_kernel<kTableBlock>, dim3((unsigned)blocks), dim3(kTableBlock),

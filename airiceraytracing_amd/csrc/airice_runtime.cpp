@@ -5,6 +5,7 @@
 #include <cmath>
 #include <cstdarg>
 #include <algorithm>
+#include <atomic>
 #include <cstdio>
 #include <cstdlib>
 #include <chrono>
@@ -253,8 +254,9 @@ void build_ice_consts(const DevMedium& M, double ice_h, double rx_depth, IceCons
 }
 
 // ---- kernel timer (bench only) ---------------------------------------------------------
-bool g_ktimer_on = false;
+std::atomic<bool> g_ktimer_on{false};
 static std::mutex g_kt_mu;
+static constexpr size_t kKtMaxPairs = 1 << 16;  // closed pairs kept per kernel until a reset
 struct KtPair {
   hipEvent_t a = nullptr, b = nullptr;
 };
@@ -266,8 +268,18 @@ static const char* const kKtNames[KT_COUNT] = {"table_kernel", "roots_kernel", "
 void ktimer_record(int id, bool begin, hipStream_t st) {
   std::lock_guard<std::mutex> lock(g_kt_mu);
   if (begin) {
+    if (g_kt_open[id].a != nullptr) {  // a begin whose launch failed before its end: drop it
+      (void)hipEventDestroy(g_kt_open[id].a);
+      (void)hipEventDestroy(g_kt_open[id].b);
+      g_kt_open[id] = KtPair();
+    }
+    if (g_kt_done[id].size() >= kKtMaxPairs) return;  // bounded: time no more until a reset
     KtPair p;
-    if (hipEventCreate(&p.a) != hipSuccess || hipEventCreate(&p.b) != hipSuccess) return;
+    if (hipEventCreate(&p.a) != hipSuccess) return;
+    if (hipEventCreate(&p.b) != hipSuccess) {
+      (void)hipEventDestroy(p.a);
+      return;
+    }
     (void)hipEventRecord(p.a, st);
     g_kt_open[id] = p;
   } else if (g_kt_open[id].a != nullptr) {
@@ -362,7 +374,14 @@ int ScalarCall::sync() {
       const unsigned want = slot_->seq;
       const auto t0 = std::chrono::steady_clock::now();
       for (unsigned spins = 0;; ++spins) {
-        if (__atomic_load_n(slot_->flag_h, __ATOMIC_ACQUIRE) == want) return AIRICE_OK;
+        if (__atomic_load_n(slot_->flag_h, __ATOMIC_ACQUIRE) == want) {
+          // the outputs are complete; an asynchronous fault of this call's launch (after its
+          // last store) is reported here, not by a later, unrelated call
+          const hipError_t q = hipStreamQuery(slot_->st);
+          if (q == hipSuccess || q == hipErrorNotReady) return AIRICE_OK;
+          set_error("scalar call: %s", hipGetErrorString(q));
+          return AIRICE_EHIP;
+        }
         if ((spins & 255) == 255 &&
             std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(2000))
           break;
@@ -409,7 +428,7 @@ int lookup_fallback_one(const airice_medium* m, double src_cm, double dist_cm, d
 using namespace airice;
 
 extern "C" int airice_kernel_timing(int on) {
-  g_ktimer_on = on != 0;
+  g_ktimer_on.store(on != 0, std::memory_order_relaxed);
   return AIRICE_OK;
 }
 
@@ -768,6 +787,11 @@ int airice_lookup_pack(const airice_lookup_table* t, float* d_entries, void* str
     set_error("ld < n_entries or entries not 16-byte aligned");
     return AIRICE_EINVAL;
   }
+  if (t->n_entries < 1 || t->total_angle_steps < 1) {  // the row records divide by the row length
+    set_error("lookup pack: n_entries (%zu) and total_angle_steps (%d) must be >= 1",
+              t->n_entries, t->total_angle_steps);
+    return AIRICE_EINVAL;
+  }
   const int rc = launch_lookup_pack(t, d_entries, (hipStream_t)stream);
   if (rc) set_error("lookup pack failed: %s", hipGetErrorString(hipGetLastError()));
   return rc;
@@ -802,12 +826,21 @@ int airice_rtf_outputs(int op, int max_layers) { return airice::rtf_outputs(op, 
 
 int airice_rtf_eval(const airice_medium* m, int op, const double* args, size_t n_args, double* out,
                     size_t n_out) {
+  return airice_rtf_eval_variant(m, AIRICE_VARIANT_MULTIRAY, op, args, n_args, out, n_out);
+}
+
+int airice_rtf_eval_variant(const airice_medium* m, int variant, int op, const double* args,
+                            size_t n_args, double* out, size_t n_out) {
   if (m == nullptr || out == nullptr || (n_args > 0 && args == nullptr)) {
     set_error("null argument");
     return AIRICE_EINVAL;
   }
+  if (variant != AIRICE_VARIANT_MULTIRAY && variant != AIRICE_VARIANT_PYWRAPPER) {
+    set_error("unknown variant %d", variant);
+    return AIRICE_EINVAL;
+  }
   DevMedium M;
-  int rc = build_dev_medium(m, AIRICE_VARIANT_MULTIRAY, &M);
+  int rc = build_dev_medium(m, variant, &M);
   if (rc) return rc;
   const int need = airice::rtf_outputs(op, M.ml);
   if (need < 0) {
@@ -888,49 +921,6 @@ int airice_trace_ice_to_air_host(const airice_medium* m, const double* depth, co
   int rc = airice_trace_ice_to_air_launch(m, dd, di, dt, ds, n, dout, nullptr);
   if (rc == AIRICE_OK) HIP_TRY(hipMemcpy(out10, dout, sizeof(double) * 10 * n, hipMemcpyDeviceToHost));
   return rc;
-}
-
-// Py_TraceIceToAir drop-in (TraceIceToAir.C:75-79).  The reference re-parses
-// "Atmosphere.dat" from the working directory on every call (TraceIceToAir.C:25);
-// here it is parsed once per process; each call runs in the current device's scalar slot.
-static std::mutex g_py_mu;
-static bool g_py_ready = false;
-static airice_medium g_py_medium;
-
-void Py_TraceIceToAir(double AntennaDepth, double IceLayerHeight, double AirTxHeight,
-                      double HorizontalDistance, double ArrayParameters[10]) {
-  std::lock_guard<std::mutex> lock(g_py_mu);
-  for (int i = 0; i < 10; ++i) ArrayParameters[i] = -1000;
-  if (!g_py_ready) {
-    int rc = airice_atmosphere_load("Atmosphere.dat", AIRICE_VARIANT_PYWRAPPER, &g_py_medium);
-    if (rc != AIRICE_OK) {
-      const char* env = std::getenv("AIRICE_ATMOSPHERE");
-      if (env == nullptr ||
-          airice_atmosphere_load(env, AIRICE_VARIANT_PYWRAPPER, &g_py_medium) != AIRICE_OK) {
-        std::fprintf(stderr, "Py_TraceIceToAir: %s\n", airice_last_error());
-        return;
-      }
-    }
-    g_py_ready = true;
-  }
-  ScalarCall call;
-  if (!call.ok()) {
-    std::fprintf(stderr, "Py_TraceIceToAir: %s\n", airice_last_error());
-    return;
-  }
-  ScalarSlot& sl = call.slot();
-  sl.h[0] = AntennaDepth;
-  sl.h[1] = IceLayerHeight;
-  sl.h[2] = AirTxHeight;
-  sl.h[3] = HorizontalDistance;
-  call.arm(sl.h, 4);
-  if (airice_trace_ice_to_air_launch(&g_py_medium, sl.d, sl.d + 1, sl.d + 2, sl.d + 3, 1,
-                                     sl.d + 4, sl.st) != AIRICE_OK ||
-      call.sync() != AIRICE_OK) {
-    std::fprintf(stderr, "Py_TraceIceToAir: %s\n", airice_last_error());
-    return;
-  }
-  std::memcpy(ArrayParameters, sl.h + 4, sizeof(double) * 10);
 }
 
 int airice_device_count(int* count) {

@@ -12,6 +12,8 @@
 #include <string>
 #include <vector>
 
+#include "airice.h"
+
 namespace airice_compat {
 
 // Atmosphere.dat from the working directory, as the reference opens it, else $AIRICE_ATMOSPHERE.
@@ -91,6 +93,35 @@ inline int read_nh(const std::string& text, const double ATMLAY[5],
   nh_data.back().pop_back();
   lognh_data.back().pop_back();
   return (int)h_data.size() + 1;
+}
+
+// FillInAirRefractiveIndex (MultiRayAirIceRefraction.cc:193-213 == RayTracingFunctions.cc:149-170
+// == pythonwrapper/AirIceRayTracing.cc:154-170) over a namespace's ATMLAY / abc: C_air from the
+// scale heights, B_air chained for continuity from N0 (the natural cubic spline of the profile at
+// 0 m, which the library's parse of the same file computes) with the namespace's A_air
+inline void fill_air_index(const double ATMLAY[5], const double abc[5][3], double A_air,
+                           double N0_spline, double C_air[5], double B_air[5]) {
+  double N0 = 0;
+  for (int il = 0; il < 5; il++) {
+    const double hlow = ATMLAY[il] / 100;
+    C_air[il] = 1.0 / (abc[il][2] / 100);
+    if (il > 0) N0 = A_air + B_air[il - 1] * std::exp(-hlow * C_air[il - 1]);
+    if (il == 0) N0 = N0_spline;
+    B_air[il] = ((N0 - 1) / std::exp(-hlow * C_air[il]));
+  }
+}
+
+// The medium a call runs on: the parse of the file (N0, profile size and top) with the namespace's
+// current ATMLAY, B_air, C_air and MaxLayers -- the reference reads those at every call, so a
+// caller's edits after MakeAtmosphere take effect
+inline void apply_namespace(airice_medium& m, const double ATMLAY[5], const double B_air[5],
+                            const double C_air[5], int MaxLayers) {
+  for (int i = 0; i < 5; i++) {
+    m.atmlay_cm[i] = ATMLAY[i];
+    m.B_air[i] = B_air[i];
+    m.C_air[i] = C_air[i];
+  }
+  m.max_layers = MaxLayers;
 }
 
 // flatten (MultiRayAirIceRefraction.cc:649-658 == RayTracingFunctions.cc:517-527)

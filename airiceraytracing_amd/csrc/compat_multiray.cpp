@@ -76,8 +76,9 @@ namespace {
 namespace MR = MultiRayAirIceRefraction;
 
 std::mutex g_mu;  // the medium and the HBM table copies
-airice_medium g_medium;
+airice_medium g_medium;     // the parse of Atmosphere.dat (N0, profile size)
 bool g_have_medium = false;
+bool g_ns_filled = false;   // MakeAtmosphere has filled the namespace data
 
 [[noreturn]] void die(const char* what) {
   std::fprintf(stderr, "MultiRayAirIceRefraction: %s failed: %s\n", what, airice_last_error());
@@ -86,8 +87,10 @@ bool g_have_medium = false;
 
 std::string atmosphere_text() { return airice_compat::atmosphere_text("MultiRayAirIceRefraction"); }
 
-// The parsed medium with the namespace's current ice model (A_ice / B_ice / C_ice are mutable
-// namespace variables in the reference, read by Getnz_ice at every call).
+// The medium of the next call: the parse of the file with the namespace's current air model
+// (ATMLAY, B_air, C_air, MaxLayers once MakeAtmosphere has filled them) and ice model (A_ice /
+// B_ice / C_ice) -- mutable namespace variables the reference reads at every call.  Before any
+// MakeAtmosphere the file is parsed on first use.
 airice_medium medium() {
   std::lock_guard<std::mutex> lock(g_mu);
   if (!g_have_medium) {
@@ -98,6 +101,7 @@ airice_medium medium() {
     g_have_medium = true;
   }
   airice_medium m = g_medium;
+  if (g_ns_filled) airice_compat::apply_namespace(m, MR::ATMLAY, MR::B_air, MR::C_air, MR::MaxLayers);
   m.A_ice = MR::A_ice;
   m.B_ice = MR::B_ice;
   m.C_ice = MR::C_ice;
@@ -146,7 +150,9 @@ airice::LkTable host_lk(const std::vector<std::vector<float>>& cols) {
 }
 
 // Cheap content fingerprint of a host table: the column buffers, their length and 64 sampled
-// entries per column.  The HBM copy of a table is reused only while this is unchanged.
+// entries per column.  The HBM copy of a table is reused only while this is unchanged: a table the
+// caller replaced, resized or refilled is uploaded again, but an in-place edit of entries other
+// than the sampled ones is NOT detected (hashing every entry would cost more than the lookups).
 uint64_t table_fingerprint(const std::vector<std::vector<float>>& cols) {
   uint64_t h = 1469598103934665603ull;
   auto mix = [&h](uint64_t v) {
@@ -168,12 +174,13 @@ uint64_t table_fingerprint(const std::vector<std::vector<float>>& cols) {
 
 // HBM copy of AllTableAllAntData[i] for the batch lookup: the copy MakeRayTracingTable left
 // behind, or an upload.  A table whose fingerprint changed since (a caller-filled, replaced or
-// edited table) is uploaded again.
+// resized table) is uploaded again.
 struct DevTable {
   uint64_t fp = 0;
   size_t n = 0;
   float* dev = nullptr;
   float* packed = nullptr;  // airice_lookup_pack copy, made at the first batch lookup
+  int packed_asteps = 0;    // the TotalAngleSteps its row records were folded with
 };
 std::vector<DevTable> g_tables;
 
@@ -228,6 +235,7 @@ int readnhFromFile() {
 
 // N0 from the natural cubic spline of the profile at 0 m, then B_air chained for continuity
 // (.cc:193-213): the library's parse of the same file does exactly this
+// over the namespace's ATMLAY / abc
 int FillInAirRefractiveIndex() {
   const std::string text = atmosphere_text();
   std::lock_guard<std::mutex> lock(g_mu);
@@ -235,10 +243,7 @@ int FillInAirRefractiveIndex() {
       AIRICE_OK)
     die("FillInAirRefractiveIndex");
   g_have_medium = true;
-  for (int i = 0; i < 5; i++) {
-    C_air[i] = g_medium.C_air[i];
-    B_air[i] = g_medium.B_air[i];
-  }
+  airice_compat::fill_air_index(ATMLAY, abc, A_air, g_medium.N0, C_air, B_air);
   return 0;
 }
 
@@ -250,6 +255,8 @@ int MakeAtmosphere() {
   readATMpar();
   readnhFromFile();
   FillInAirRefractiveIndex();
+  std::lock_guard<std::mutex> lock(g_mu);
+  g_ns_filled = true;
   return 0;
 }
 
@@ -261,7 +268,7 @@ double Getnz_ice(double z) {
   return airice_nz_ice(&m, z);
 }
 
-static int layer_of(double z) {
+static int layer_of(double z) {  // the GetB_air / GetC_air scan (.cc:216-257)
   const airice_medium m = medium();
   const double zabs = std::fabs(z);
   int which = 0;
@@ -662,10 +669,17 @@ void TableLookupBatch(const double* SrcHeightASL, const double* HorizontalDistan
   t.total_height_steps = TotalHeightSteps;
   t.total_angle_steps = TotalAngleSteps;
   t.entries = nullptr;
+  // the row records fix the row spans to the angle grid in force: re-pack when it changed
+  if (dt.packed != nullptr && dt.packed_asteps != t.total_angle_steps) {
+    (void)hipFree(dt.packed);
+    dt.packed = nullptr;
+  }
   if (dt.packed == nullptr) {
-    if (hipMalloc(&dt.packed, sizeof(float) * AIRICE_LOOKUP_PACK_FLOATS(entries, t.total_angle_steps)) != hipSuccess ||
+    if (t.total_angle_steps < 1 ||
+        hipMalloc(&dt.packed, sizeof(float) * AIRICE_LOOKUP_PACK_FLOATS(entries, t.total_angle_steps)) != hipSuccess ||
         airice_lookup_pack(&t, dt.packed, nullptr) != AIRICE_OK)
       die("airice_lookup_pack");
+    dt.packed_asteps = t.total_angle_steps;
   }
   t.entries = dt.packed;
   // one device block: src | dist | depth | out (9 columns) | ok | flags

@@ -40,15 +40,20 @@ bool g_have_medium = false;
 
 std::string atmosphere_text() { return airice_compat::atmosphere_text("RayTracingFunctions"); }
 
-const airice_medium& medium() {
+// The medium of the next call: the parse of the file with the namespace's current ATMLAY, B_air,
+// C_air and MaxLayers (the reference reads them at every call, so edits take effect)
+airice_medium medium() {
   if (!g_have_medium) R::MakeAtmosphere();
-  return g_medium;
+  airice_medium m = g_medium;
+  airice_compat::apply_namespace(m, R::ATMLAY, R::B_air, R::C_air, R::MaxLayers);
+  return m;
 }
 
 // one GPU evaluation of a RayTracingFunctions quantity
 void rtf(int op, std::initializer_list<double> args, double* out, size_t n_out) {
   const std::vector<double> a(args);
-  if (airice_rtf_eval(&medium(), op, a.data(), a.size(), out, n_out) != AIRICE_OK)
+  const airice_medium m = medium();
+  if (airice_rtf_eval(&m, op, a.data(), a.size(), out, n_out) != AIRICE_OK)
     die("airice_rtf_eval");
 }
 
@@ -99,10 +104,7 @@ int FillInAirRefractiveIndex() {
       AIRICE_OK)
     die("FillInAirRefractiveIndex");
   g_have_medium = true;
-  for (int i = 0; i < 5; i++) {
-    C_air[i] = g_medium.C_air[i];
-    B_air[i] = g_medium.B_air[i];
-  }
+  airice_compat::fill_air_index(ATMLAY, abc, A_air, g_medium.N0, C_air, B_air);
   return 0;
 }
 
@@ -117,7 +119,10 @@ int MakeAtmosphere() {
 
 double GetB_ice(double) { return -0.43; }  // .cc:126-133
 double GetC_ice(double) { return 0.0132; } // .cc:135-142
-double Getnz_ice(double z) { return airice_nz_ice(&medium(), z); }
+double Getnz_ice(double z) {
+  const airice_medium m = medium();
+  return airice_nz_ice(&m, z);
+}
 double GetB_air(double z) {
   medium();
   return B_air[layer_of(z)];
@@ -126,7 +131,10 @@ double GetC_air(double z) {
   medium();
   return C_air[layer_of(z)];
 }
-double Getnz_air(double z) { return airice_nz_air(&medium(), z); }
+double Getnz_air(double z) {
+  const airice_medium m = medium();
+  return airice_nz_air(&m, z);
+}
 
 // Refl_S / Refl_P (.cc:222-255): power reflectances, NaN -> 1
 double Refl_S(double thetai, double IceLayerHeight) {

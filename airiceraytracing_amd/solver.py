@@ -149,8 +149,11 @@ class AirIceSolver:
         it and the next entry, then one 32-byte record per table row; torch tensor on the table's
         device) that ``lt`` then reads; the tensor is kept on ``lt``."""
         import torch
-        n = int(lt.n_entries)
-        floats = n * _lib.LOOKUP_ENTRY_FLOATS + (n // int(lt.total_angle_steps)) * _lib.LOOKUP_ROW_FLOATS
+        n, asteps = int(lt.n_entries), int(lt.total_angle_steps)
+        if n < 1 or asteps < 1:  # as airice_lookup_pack: the row records divide by the row length
+            raise ValueError(f"lookup_pack: n_entries ({n}) and total_angle_steps ({asteps}) "
+                             "must be >= 1")
+        floats = n * _lib.LOOKUP_ENTRY_FLOATS + (n // asteps) * _lib.LOOKUP_ROW_FLOATS
         packed = torch.empty(floats, dtype=torch.float32,
                              device=torch.device("cuda", torch.cuda.current_device()))
         check(lib().airice_lookup_pack(ctypes.byref(lt), ptr(packed), _stream_handle(stream)),

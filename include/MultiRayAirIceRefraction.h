@@ -20,8 +20,9 @@
  *     FindExtrapolationLimit (.cc:997-1031) and the atmosphere file readers are host code as in
  *     the reference.
  *
- * Not provided: FindFunctionRoot and the gsl_interp_accel / gsl_spline statics (their types are
- * GNU GSL's, absent from this build; the root finding lives in the kernels), and the deprecated
+ * FindFunctionRoot (.cc:340-374) keeps its GSL-typed signature (airice_gsl_roots.h) and runs GSL's
+ * bisection / Brent on the caller's host function.  Not provided: the gsl_interp_accel /
+ * gsl_spline statics (GSL objects; N0 comes from the library's own spline), and the deprecated
  * MakeTable / GetInterpolatedValue (.cc:1618-1794, "Do not use this function").
  *
  * Namespace data: the reference defines it as header statics (one copy per translation unit,
@@ -38,6 +39,8 @@
 
 #include <cstddef>
 #include <vector>
+
+#include "airice_gsl_roots.h"
 
 /* Defined by the caller (reference .h:23-24, RunMultiRayCode.C:3-4). */
 extern std::vector<double> AntennaDepths;
@@ -117,6 +120,10 @@ bool GetHorizontalDistanceToIntersectionPoint(
     double& transmissionCoefficientP, double& RecievedAngleInIce);
 
 double oneDLinearInterpolation(double x, double xa, double ya, double xb, double yb);
+
+/* GSL root-solver driver (.cc:340-374, max_iter 40): bisection or Brent, by the solver's name. */
+double FindFunctionRoot(gsl_function F, double x_lo, double x_hi, const gsl_root_fsolver_type* T,
+                        double tolerance);
 
 /* The ray layer (.cc:377-917), evaluated on the GPU.  *Par functions return new[]'d arrays the
  * caller delete[]s, as with the reference: GetLayerHitPointPar / GetIcePropagationPar 5 doubles

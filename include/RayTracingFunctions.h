@@ -13,13 +13,16 @@
  *   - MakeAtmosphere() reads "Atmosphere.dat" from the working directory (fallback
  *     $AIRICE_ATMOSPHERE) and fills ATMLAY, abc, B_air, C_air, MaxLayers, h_data, nh_data,
  *     lognh_data.  The reference defines these as header statics; here they are one shared copy.
- * Not provided: FindFunctionRoot and the GSL spline/accelerator statics (their signatures need GNU
- * GSL types, absent from this build; the minimizer lives in airice_solve_* instead).
+ * FindFunctionRoot (.cc:256-290, max_iter 20) keeps its GSL-typed signature (airice_gsl_roots.h)
+ * and runs GSL's bisection / Brent on the caller's host function.  Not provided: the GSL
+ * spline/accelerator statics (GSL objects; N0 comes from the library's own spline).
  * Link: -L<repo>/airiceraytracing_amd -lairice. */
 #ifndef AIRICE_RAYTRACINGFUNCTIONS_H_
 #define AIRICE_RAYTRACINGFUNCTIONS_H_
 
 #include <vector>
+
+#include "airice_gsl_roots.h"
 
 namespace RayTracingFunctions {
 
@@ -49,6 +52,9 @@ double GetC_air(double z);
 double Getnz_air(double z);
 double Refl_S(double thetai, double IceLayerHeight);
 double Refl_P(double thetai, double IceLayerHeight);
+
+double FindFunctionRoot(gsl_function F, double x_lo, double x_hi, const gsl_root_fsolver_type *T,
+                        double tolerance);
 
 struct fDnfR_params { double a, b, c, l; };
 double fDnfR(double x, void *params);

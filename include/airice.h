@@ -260,9 +260,10 @@ int airice_trace_ice_to_air_launch(const airice_medium *m, const double *d_depth
 int airice_trace_ice_to_air_host(const airice_medium *m, const double *depth, const double *ice,
                                  const double *txh, const double *dist, size_t n, double *out10);
 
-/* Drop-in for the reference ctypes symbol (TraceIceToAir.C:75-79).  Reads
- * "Atmosphere.dat" from the working directory like the reference (once, cached;
- * falls back to $AIRICE_ATMOSPHERE), then solves on the GPU. */
+/* Drop-in for the reference ctypes symbol (TraceIceToAir.C:75-79): the C++ TraceIceToAir of
+ * include/AirIceRayTracing.h, which reads "Atmosphere.dat" from the working directory like the
+ * reference (parsed once while the file is unchanged; falls back to $AIRICE_ATMOSPHERE), then
+ * solves on the GPU. */
 void Py_TraceIceToAir(double AntennaDepth, double IceLayerHeight, double AirTxHeight,
                       double HorizontalDistance, double ArrayParameters[10]);
 
@@ -318,6 +319,12 @@ void Py_TraceIceToAir(double AntennaDepth, double IceLayerHeight, double AirTxHe
 int airice_rtf_outputs(int op, int max_layers);
 int airice_rtf_eval(const airice_medium *m, int op, const double *args, size_t n_args,
                     double *out, size_t n_out);
+/* The same ops with the numerics of another reference namespace: AIRICE_VARIANT_PYWRAPPER gives the
+ * pythonwrapper's AirIceRayTracing:: ray layer (pythonwrapper/AirIceRayTracing.cc:356-857, the
+ * AIRICE_MR_* / FDNFR / FTIMED / OPTICAL_PATH / PROPAGATION_TIME ops with pi = 4*atan(1) and its
+ * UseConstantRefractiveIndex medium); airice_rtf_eval is AIRICE_VARIANT_MULTIRAY. */
+int airice_rtf_eval_variant(const airice_medium *m, int variant, int op, const double *args,
+                            size_t n_args, double *out, size_t n_out);
 
 /* Device bookkeeping (thin wrappers so ctypes callers need no HIP runtime binding). */
 int airice_device_count(int *count);

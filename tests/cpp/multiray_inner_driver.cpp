@@ -96,6 +96,22 @@ int main() {
     M::A_ice = M::A_ice_def;
     arr("a_ice_1775", v, 2);
   }
+  // the air model is namespace data read at every call (.h:56-61): an edit of B_air[1] (the
+  // 3217-8363 m layer) after MakeAtmosphere changes the next solve, ray and n(z), then is undone
+  {
+    const double keep = M::B_air[1];
+    M::B_air[1] = keep * 1.001;
+    double d[20], rr[20];
+    const double thR = 180 - (std::atan(1000.0 / 2200.0) * (180.0 / M::pi));
+    M::Air2IceRayTracing(5000.0, 1000.0, 3000.0, -200.0, thR, d);
+    arr("air2ice_b_air_edit", d, 17);
+    bool in_ice = true;
+    M::GetRayTracingSolutions(170.0, 20000.0, 3000.0, -200.0, rr, in_ice);
+    arr("ray_b_air_edit", rr, 18);
+    const double nz[2] = {M::Getnz_air(5000), M::GetB_air(5000)};
+    arr("nz_b_air_edit", nz, 2);
+    M::B_air[1] = keep;
+  }
   // coarse table through the reference's globals, two antennas with table dedupe
   HeightStepSize = 2000;
   AngleStepSize = 5;

@@ -52,7 +52,15 @@ int main() {
                           R::ftimeD(100.0, &tp),
                           R::GetRayOpticalPath(R::A_air, 3000.0, 8000.0, 0.4, 1),
                           R::GetRayPropagationTime(R::A_ice, 150.0, 0.0, 0.9, 0)};
-  arr("scalars", scal, 5, true);
+  arr("scalars", scal, 5);
+  // namespace data is read at every call: edit C_air of the 3217-8363 m layer, then undo it
+  const double keep = R::C_air[1];
+  R::C_air[1] = keep * 1.002;
+  double* ep = R::GetAirPropagationPar(170.0, 20000.0, 3000.0);
+  const double ed[3] = {ep[0] + ep[4] + ep[8], R::Getnz_air(5000.0), R::GetC_air(5000.0)};
+  delete[] ep;
+  R::C_air[1] = keep;
+  arr("c_air_edit", ed, 3, true);
   std::printf("}\n");
   return 0;
 }

@@ -150,9 +150,10 @@ def test_product_does_not_import_oracle():
 
 
 # The MultiRayAirIceRefraction.h surface of the reference (its .h:26-204), as demangled
-# signatures: every function a caller of the reference can link against, bar the GSL-typed
-# FindFunctionRoot and the deprecated MakeTable / GetInterpolatedValue (.cc:1618-1794).
+# signatures: every function a caller of the reference can link against, bar the deprecated
+# MakeTable / GetInterpolatedValue (.cc:1618-1794).
 MULTIRAY_FUNCTIONS = [
+    "FindFunctionRoot(gsl_function_struct, double, double, gsl_root_fsolver_type const*, double)",
     "readATMpar()", "readnhFromFile()", "GetB_ice(double)", "GetC_ice(double)",
     "Getnz_ice(double)", "FillInAirRefractiveIndex()", "GetB_air(double)", "GetC_air(double)",
     "Getnz_air(double)", "Refl_S(double, double)", "Trans_S(double, double)",
@@ -209,3 +210,73 @@ def test_multiray_dropin_exports_the_reference_surface():
     assert not [v for v in MULTIRAY_DATA if ns + v not in defined]
     assert not [v for v in GLOBAL_DATA if v not in defined]
     assert {"AntennaDepths", "AntennaTableAlreadyMade"} <= weak
+
+
+# The exported text symbols of the reference's prebuilt pythonwrapper/libAirIceRayTracing.so
+# (nm -D --defined-only, its own std:: template instantiations left out): the AirIceRayTracing::
+# namespace of pythonwrapper/AirIceRayTracing.h:23-146, the C++ TraceIceToAir (TraceIceToAir.C:5)
+# and the ctypes entry Py_TraceIceToAir (TraceIceToAir.C:75-79).
+PYWRAPPER_SYMBOLS = """
+Py_TraceIceToAir _Z13TraceIceToAirddddPd
+_ZN16AirIceRayTracing10readATMparENSt7__cxx1112basic_stringIcSt11char_traitsIcESaIcEEE
+_ZN16AirIceRayTracing14MakeAtmosphereENSt7__cxx1112basic_stringIcSt11char_traitsIcESaIcEEE
+_ZN16AirIceRayTracing14readnhFromFileENSt7__cxx1112basic_stringIcSt11char_traitsIcESaIcEEE
+_ZN16AirIceRayTracing16FindFunctionRootE19gsl_function_structddPK21gsl_root_fsolver_typedi
+_ZN16AirIceRayTracing17Air2IceRayTracingEdddddPd _ZN16AirIceRayTracing19GetLayerHitPointParEddddi
+_ZN16AirIceRayTracing19GetRayGeometricPathEddddi _ZN16AirIceRayTracing20GetAirPropagationParEddd
+_ZN16AirIceRayTracing20GetIcePropagationParEdddd _ZN16AirIceRayTracing20GetRayHorizontalPathEddddi
+_ZN16AirIceRayTracing21GetRayPropagationTimeEddddi
+_ZN16AirIceRayTracing21GetRayTracingSolutionEddddRdS0_S0_S0_S0_S0_S0_S0_
+_ZN16AirIceRayTracing22MinimizeforLaunchAngleEdPv _ZN16AirIceRayTracing24FillInAirRefractiveIndexEv
+_ZN16AirIceRayTracing5fDnfREdPv _ZN16AirIceRayTracing6Refl_PEdd _ZN16AirIceRayTracing6Refl_SEdd
+_ZN16AirIceRayTracing6fpathDEdPv _ZN16AirIceRayTracing6ftimeDEdPv _ZN16AirIceRayTracing7Trans_PEdd
+_ZN16AirIceRayTracing7Trans_SEdd _ZN16AirIceRayTracing7flattenERKSt6vectorIS0_IdSaIdEESaIS2_EE
+_ZN16AirIceRayTracing8GetB_airEd _ZN16AirIceRayTracing8GetB_iceEd _ZN16AirIceRayTracing8GetC_airEd
+_ZN16AirIceRayTracing8GetC_iceEd _ZN16AirIceRayTracing9Getnz_airEd _ZN16AirIceRayTracing9Getnz_iceEd
+""".split()
+PYWRAPPER_DATA = ["nh_data", "lognh_data", "h_data", "ATMLAY", "abc", "C_air", "B_air",
+                  "MaxLayers", "UseConstantRefractiveIndex", "A_air", "A_const"]
+
+
+def test_pywrapper_dropin_exports_the_reference_symbols():
+    """Every symbol the reference's libAirIceRayTracing.so exports is defined by libairice.so
+    under the same mangled name, so a C++ object built against pythonwrapper/AirIceRayTracing.h
+    (or a ctypes user of Py_TraceIceToAir) relinks unchanged; the namespace data is exported too
+    (include/AirIceRayTracing.h: one shared copy instead of the reference's header statics)."""
+    from airiceraytracing_amd import _lib
+    out = subprocess.run(["nm", "-D", "--defined-only", _lib.LIB_PATH], capture_output=True,
+                         text=True, check=True).stdout
+    syms = {ln.split()[-1] for ln in out.splitlines() if len(ln.split()) == 3}
+    assert len(PYWRAPPER_SYMBOLS) == 30
+    missing = [s for s in PYWRAPPER_SYMBOLS if s not in syms]
+    assert not missing, missing
+    dem = subprocess.run(["nm", "-DC", "--defined-only", _lib.LIB_PATH], capture_output=True,
+                         text=True, check=True).stdout
+    data = {ln.split(None, 2)[2].strip() for ln in dem.splitlines()
+            if len(ln.split(None, 2)) == 3 and ln.split(None, 2)[1] in "DB"}
+    assert not [v for v in PYWRAPPER_DATA if "AirIceRayTracing::" + v not in data]
+    # and the GSL-typed FindFunctionRoot of the two other namespaces
+    for ns in ("_ZN24MultiRayAirIceRefraction", "_ZN19RayTracingFunctions"):
+        assert ns + "16FindFunctionRootE19gsl_function_structddPK21gsl_root_fsolver_typed" in syms
+
+
+def test_lookup_pack_rejects_empty_angle_grid():
+    """airice_lookup_pack validates the row length before folding row records: a
+    zero TotalAngleSteps or an empty table is AIRICE_EINVAL, not a division by zero.  No device
+    memory is touched (the pointers are never dereferenced), so this runs on the CPU."""
+    import ctypes
+    from airiceraytracing_amd import _lib
+    from airiceraytracing_amd.solver import AirIceSolver
+    L = _lib.lib()
+    for n, asteps in ((100, 0), (0, 10)):
+        t = _lib.LookupTable()
+        t.table = 0x10000
+        t.ld = max(n, 1)
+        t.n_entries = n
+        t.loop_stop_height, t.height_step = 3000.0, 10.0
+        t.total_height_steps, t.total_angle_steps = 10, asteps
+        rc = L.airice_lookup_pack(ctypes.byref(t), ctypes.c_void_p(0x20000), None)
+        assert rc == -1, rc  # AIRICE_EINVAL
+        assert b"total_angle_steps" in L.airice_last_error()
+        with pytest.raises(ValueError):
+            AirIceSolver.lookup_pack(t)

@@ -167,6 +167,21 @@ def test_cpp_inner_api_against_oracle(tmp_path, oracle_medium):
     m2.A_ice = 1.775
     _close(r["a_ice_1775"], [oracle.getnz_ice(m2, -100), oracle.rtf_eval(m2, 13,
                                                                           [30.0, 3000, -200, 0.9])[0]])
+    # B_air is read at every call: the edited medium's solve, ray and n(z)
+    m3 = oracle.load_atmosphere(ATMOSPHERE_GZ)
+    m3.B_air[1] = m.B_air[1] * 1.001
+    thR = 180 - (math.atan(1000.0 / 2200.0) * (180.0 / 3.1415927))
+    ref_e, st_e = oracle.air2ice(m3, 5000.0, 1000.0, 3000.0, -200.0, thR)
+    rep = parity.compare_columns(np.array(r["air2ice_b_air_edit"])[:, None], ref_e[:, None],
+                                 parity.SOLVE_FLOORS)
+    assert rep["ok"] and st_e == 0, rep
+    ref_e0, _ = oracle.air2ice(m, 5000.0, 1000.0, 3000.0, -200.0, thR)
+    assert abs(r["air2ice_b_air_edit"][2] - ref_e0[2]) > 1e-6  # the edit changed the ray
+    rep = parity.compare_columns(np.array(r["ray_b_air_edit"])[:, None],
+                                 oracle.ray_solution(m3, 170.0, 20000.0, 3000.0, -200.0,
+                                                     True)[:, None], parity.RAY_FLOORS)
+    assert rep["ok"], rep
+    assert r["nz_b_air_edit"] == [oracle.getnz_air(m3, 5000.0), m3.B_air[1]]
     # MakeRayTracingTables (one launch for three antennas) == one MakeRayTracingTable each
     assert r["multi_tables_equal"] == [1, 1, 1]
     # table walks on table 0, bit for bit against the oracle's restatement on the same floats

@@ -83,6 +83,12 @@ def test_rtf_cpp_caller(tmp_path):
            oracle.rtf_eval(m, 1, [1.0, 3000.0, 8000.0, 0.4, 1])[0],
            oracle.rtf_eval(m, 2, [1.78, 150.0, 0.0, 0.9, 0])[0]]
     _close(r["scalars"], ref, floor=1e-15)
+    m2 = _medium()
+    m2.C_air[1] = m.C_air[1] * 1.002
+    air2 = oracle.rtf_eval(m2, 3, [170.0, 20000.0, 3000.0])
+    _close(r["c_air_edit"], [air2[0] + air2[4] + air2[8], oracle.getnz_air(m2, 5000.0),
+                             m2.C_air[1]])
+    assert abs(r["c_air_edit"][0] - (air[0] + air[4] + air[8])) > 1e-6
 
 
 @pytest.mark.gpu
