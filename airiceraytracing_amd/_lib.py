@@ -136,7 +136,8 @@ EXPORTED_SYMBOLS = (
     "airice_trace_ice_to_air_host", "airice_rtf_outputs", "airice_rtf_eval",
     "airice_rtf_eval_variant", "Py_TraceIceToAir", "airice_device_count", "airice_set_device", "airice_malloc",
     "airice_free", "airice_memcpy_h2d", "airice_memcpy_d2h", "airice_synchronize",
-    "airice_kernel_timing", "airice_kernel_time",
+    "airice_kernel_timing", "airice_kernel_time", "airice_table_to_host",
+    "airice_host_register", "airice_host_unregister",
 )
 
 
@@ -198,6 +199,9 @@ def lib() -> ctypes.CDLL:
         "airice_rtf_outputs": ([I, I], I),
         "airice_rtf_eval": ([M, I, P, S, P, S], I),
         "airice_rtf_eval_variant": ([M, I, I, P, S, P, S], I),
+        "airice_table_to_host": ([P, S, S, P, S, P], I),
+        "airice_host_register": ([P, S], I),
+        "airice_host_unregister": ([P], I),
         "airice_trace_ice_to_air_launch": ([M, P, P, P, P, S, P, P], I),
         "airice_trace_ice_to_air_host": ([M, P, P, P, P, S, P], I),
         "Py_TraceIceToAir": ([D, D, D, D, ctypes.POINTER(D)], None),

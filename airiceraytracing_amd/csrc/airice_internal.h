@@ -7,6 +7,7 @@
 
 #include "airice.h"
 #include "airice_device.hpp"
+#include "airice_host.h"
 
 namespace airice {
 
@@ -58,7 +59,7 @@ int launch_rtf(const DevMedium& M, int op, const double* args, size_t n_args, do
 int launch_trace(const DevMedium& M, const IceConsts& I, const double* depth, const double* ice,
                  const double* txh, const double* dist, size_t n, double* out10, hipStream_t st);
 
-void set_error(const char* fmt, ...);
+static_assert(kMaxParsedLayers == kMaxLayers, "parse and kernels agree on the layer count");
 
 // One-query calls of the scalar drop-ins (the C++ MultiRayAirIceRefraction:: / RayTracingFunctions::
 // functions, Py_TraceIceToAir, airice_rtf_eval): a pinned, device-mapped staging block per device

@@ -42,6 +42,10 @@ sys.path.insert(0, ROOT)
 PEAK_FP64_VALU_TOPS = 256 * 64 * 2.4e9 / 1e12
 CFG2 = dict(depth_cm=-20000.0, ice_cm=300000.0, height_step=20.0, start_angle=92.0,
             stop_angle=180.0, angle_step=0.5)
+# BASELINE cfg4: TxH 100000 -> 3000 m @ 1 m x 90.1 -> 180 deg @ 0.01 deg, antenna 200 m below the
+# ice: 97,001 x 8,991 = 872,135,991 rays, 38.4 GB of float columns
+CFG4 = dict(depth_cm=-20000.0, ice_cm=300000.0, height_step=1.0, start_angle=90.1,
+            stop_angle=180.0, angle_step=0.01)
 # survey-session probe of the real reference (8-core container Xeon, g++ -O2,
 # compiled against a GSL stand-in): quoted beside the oracle's CPU baseline, never measured here
 SURVEY_REFERENCE_PROBE = {
@@ -69,9 +73,17 @@ def parse():
     p.add_argument("--no-multi", action="store_true",
                    help="skip the several-antenna line item (tables on concurrent streams)")
     p.add_argument("--no-scalar", action="store_true", help="skip the scalar-call latencies")
-    p.add_argument("--default-grid", action="store_true",
-                   help="also time the reference default grid (8.7M rays; off by default so "
-                        "every table_kernel launch of the run is the cfg2 workload)")
+    p.add_argument("--no-default-grid", action="store_true",
+                   help="skip the reference default grid line item (8.7M rays)")
+    p.add_argument("--no-cfg4", action="store_true", help="skip the cfg4 fine-table line item")
+    p.add_argument("--cfg4-only", action="store_true",
+                   help="run only the cfg4 fine-table line item (PMC passes of its launch)")
+    p.add_argument("--cfg4-reps", type=int, default=3)
+    p.add_argument("--cfg4-host", choices=("auto", "none"), default="auto",
+                   help="assemble the cfg4 table in host memory (default) or keep it in HBM")
+    p.add_argument("--workload", choices=("cfg2", "cfg4"), default="cfg2",
+                   help="N>1 sharded headline: the cfg2 grid refined N-fold (weak scaling, "
+                        "default) or the cfg4 fine table split over the N GPUs (strong scaling)")
     p.add_argument("--lookup-n", type=int, default=1_000_000)
     p.add_argument("--trace-n", type=int, default=10_000_000)
     p.add_argument("--no-trace", action="store_true", help="skip the cfg5 pythonwrapper line item")
@@ -193,8 +205,32 @@ def main():
         if distributed:
             dist.barrier()
 
+    if args.cfg4_only:
+        rep = table_cfg4(args, solver, world, rank, dev, stream, distributed, coll_dev, pmc)
+        if rank == 0:
+            os.write(json_fd, (json.dumps({"table_cfg4": rep}) + "\n").encode())
+        if distributed:
+            dist.destroy_process_group()
+        return
+
     # ---------------------------------------------------------------- headline: table steps
-    if sharded:
+    cfg4_headline = sharded and args.workload == "cfg4"
+    if cfg4_headline:
+        # the cfg4 fine table split over the N GPUs (strong scaling): K builds of every rank's
+        # TxH-row slab, then one host assembly (table_cfg4)
+        args.cfg4_reps = args.steps
+        rep4 = table_cfg4(args, solver, world, rank, dev, stream, distributed, coll_dev, pmc)
+        grid = make_grid(CFG4["depth_cm"], CFG4["ice_cm"], CFG4["height_step"],
+                         CFG4["start_angle"], CFG4["stop_angle"], CFG4["angle_step"])
+        depth_cm = CFG4["depth_cm"]
+        elapsed = elapsed_bar = rep4["ms_per_build"] * args.steps / 1e3
+        total_rays = grid.n_rays * args.steps
+        n_local = rep4["roofline"]["units_per_launch"]
+        kern_ms = rep4["kernel_ms_rank0"]
+        table = None
+        shard_rep = {k: v for k, v in rep4.items() if k != "roofline"}
+        args.no_cfg4 = True
+    elif sharded:
         depth_cm = CFG2["depth_cm"]
         grid = make_grid(depth_cm, CFG2["ice_cm"],
                          sharded_step_grid_step(CFG2["height_step"], world), CFG2["start_angle"],
@@ -204,8 +240,11 @@ def main():
         grid = make_grid(depth_cm, CFG2["ice_cm"], CFG2["height_step"], CFG2["start_angle"],
                          CFG2["stop_angle"], CFG2["angle_step"])
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    shard_rep = None
-    if sharded:
+    if not cfg4_headline:
+        shard_rep = None
+    if cfg4_headline:
+        pass
+    elif sharded:
         def compute(begin, count, slab):
             solver.table_device(grid, slab, None, row_begin=begin, row_count=count,
                                 ld=slab.shape[1], stream=stream)
@@ -279,7 +318,8 @@ def main():
         elapsed, elapsed_bar = (float(x) for x in el.tolist())
         total_rays = world * n_local * args.steps
     torch.cuda.synchronize()
-    kern_ms = ev0.elapsed_time(ev1) / args.steps
+    if not cfg4_headline:
+        kern_ms = ev0.elapsed_time(ev1) / args.steps
     value = total_rays / elapsed
     extra = {}
 
@@ -511,7 +551,7 @@ def main():
             "value": n_local / (pms * 1e-3), "unit": "rays/s", "ms": pms, "d2h_ms": cms,
             "d2h_GBps": 44 * n_local / (cms * 1e-3) / 1e9}
         del host
-    if args.default_grid:
+    if not args.no_default_grid:
         # the reference's default grid (10 m x 0.1 deg, 8,730,900 rays): throughput at a size
         # where launch ramp and tail are amortised
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -528,6 +568,9 @@ def main():
         extra["table_default_grid"] = {"rays": gd.n_rays, "ms": dms,
                                        "value": gd.n_rays / (dms * 1e-3), "unit": "rays/s"}
         del td
+    if not args.no_cfg4:
+        extra["table_cfg4"] = table_cfg4(args, solver, world, rank, dev, stream, distributed,
+                                         coll_dev, pmc)
     if rank == 0 and not args.no_scalar:
         extra["scalar_latency_us"] = scalar_latencies(args)
 
@@ -588,12 +631,18 @@ def main():
         if isinstance(extra.get("scalar_latency_us"), dict):
             extra["scalar_latency_us"]["cpu_oracle_per_call_us"] = scalar_cpu_per_call(om, og, ot)
 
-    roof = counter_roofline("table_kernel", n_local, kern_ms, pmc, 44.0)
+    roof = counter_roofline("table_kernel_cfg4" if cfg4_headline else "table_kernel", n_local,
+                            kern_ms, pmc, 44.0)
     roof["ocml_priced"] = ocml_priced(grid, n_local, kern_ms)
 
     if rank == 0:
-        if sharded:
-            par = f"rows-sharded+gather (dp{world}: TxH-row slabs, one RCCL gather to rank 0)"
+        if cfg4_headline:
+            par = shard_rep["parallelism"]
+            workload = ("MakeRayTracingTable cfg4 (BASELINE configs[3]): TxH 100000->3000 m @1 m x "
+                        "90.1->180 deg @0.01 deg, one table sharded by TxH rows over %d GPUs, "
+                        "assembled in host memory" % world)
+        elif sharded:
+            par = f"rows-sharded+gather (dp{world}: TxH-row slabs, per-column RCCL gathers to rank 0)"
             workload = ("MakeRayTracingTable cfg2 grid refined %dx in TxH (step %g m), one "
                         "table sharded by TxH rows over %d GPUs" % (world, grid.height_step, world))
         else:
@@ -610,7 +659,7 @@ def main():
             "ms_per_step": elapsed / args.steps * 1e3,
             "ms_per_step_incl_trailing_barrier": elapsed_bar / args.steps * 1e3,
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if cfg4_headline else "weak",
             "vs_baseline": None,
             "dtype": "f64",
             "data": "synthetic (BASELINE cfg2 grid) over the reference GDAS Atmosphere.dat",
@@ -627,6 +676,160 @@ def main():
         os.write(json_fd, (json.dumps(line) + "\n").encode())
     if distributed:
         dist.destroy_process_group()
+
+
+def cfg4_check_rows(height_steps: int) -> list[int]:
+    """Rows of the cfg4 table checked against the oracle: the first and last rows, the rows on
+    either side of each atmosphere-layer bound the Tx heights cross (23141.75, 8363.54 and
+    3217.48 m: rows 76858/76859, 91636/91637, 96782/96783), and evenly spaced rows between."""
+    rows = {0, 1, height_steps - 1, 76858, 76859, 91636, 91637, 96782, 96783}
+    rows |= {int(r) for r in np.linspace(0, height_steps - 1, 6)}
+    return sorted(r for r in rows if 0 <= r < height_steps)
+
+
+def table_cfg4(args, solver, world, rank, dev, stream, distributed, coll_dev, pmc) -> dict:
+    """BASELINE cfg4, the fine table (872,135,991 rays, 38.4 GB): built in HBM (N=1: the whole
+    grid on one GPU; N>1: contiguous TxH-row slabs, one per GPU), timed over cfg4_reps builds, then
+    assembled in host memory where the reference keeps AllTableAllAntData (.cc:2079-2136): one
+    2-D DMA per GPU (airice_table_to_host) into page-locked host pages -- a private buffer at N=1,
+    a node-shared mapping (distributed.SharedHostTable) that every rank fills in parallel at N>1.
+    Rank 0 checks cfg4_check_rows() of the host table against the oracle."""
+    import ctypes
+    import torch
+    import torch.distributed as dist
+    from airiceraytracing_amd import _lib, make_grid
+    from airiceraytracing_amd.distributed import run_sharded_table, shard_rows
+    L = _lib.lib()
+    g = make_grid(CFG4["depth_cm"], CFG4["ice_cm"], CFG4["height_step"], CFG4["start_angle"],
+                  CFG4["stop_angle"], CFG4["angle_step"])
+    asteps, n = g.angle_steps, g.n_rays
+    begin, count, per = shard_rows(g.table_rows, world, rank)
+    from airiceraytracing_amd.solver import _stream_handle
+    h = _stream_handle(stream)
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    st = {"i": 0}
+
+    def compute(b, c, slab):
+        if st["i"] == 1:
+            ev0.record(stream)
+        solver.table_device(g, slab, None, row_begin=b, row_count=c, ld=slab.shape[1],
+                            stream=stream)
+        st["i"] += 1
+        if st["i"] == 1 + args.cfg4_reps:
+            ev1.record(stream)
+
+    def host_copy(slab, cnt, host, first):
+        _lib.check(L.airice_table_to_host(ctypes.c_void_p(slab.data_ptr()), slab.stride(0), cnt,
+                                          ctypes.c_void_p(host.data_ptr() + 4 * first),
+                                          host.stride(0), h), "airice_table_to_host")
+
+    def register(ptr, nbytes):
+        _lib.check(L.airice_host_register(ctypes.c_void_p(ptr), nbytes), "airice_host_register")
+
+    def unregister(ptr):
+        _lib.check(L.airice_host_unregister(ctypes.c_void_p(ptr)), "airice_host_unregister")
+
+    want_host = args.cfg4_host != "none"
+    rep = {"metric": "cfg4 fine table rays/s (BASELINE cfg4: MakeRayTracingTable TxH 100000->3000 "
+                     "m @1 m x 90.1->180 deg @0.01 deg, antenna 200 m below 3000 m ice)",
+           "rays": n, "rows": g.table_rows, "angles": asteps, "table_bytes": 44 * n,
+           "n_gpus": world, "unit": "rays/s"}
+    host_tab = None
+    if distributed:
+        mode = "host" if want_host else "rccl"
+        path = [f"/dev/shm/airice_cfg4_{os.getpid()}_{int(time.time())}"]
+        dist.broadcast_object_list(path, src=0)
+        try:
+            r = run_sharded_table(g, compute, args.cfg4_reps, 1, device=dev, coll_device=coll_dev,
+                                  sync=torch.cuda.synchronize, gather_reps=1, assemble=mode,
+                                  host_path=path[0], host_copy=host_copy,
+                                  host_register=register, host_unregister=unregister)
+        except OSError as e:  # no room for the shared host table: assemble on the root's GPU
+            rep["host_assembly_error"] = str(e)
+            st["i"] = 0
+            mode = "rccl"
+            r = run_sharded_table(g, compute, args.cfg4_reps, 1, device=dev, coll_device=coll_dev,
+                                  sync=torch.cuda.synchronize, gather_reps=1, assemble="rccl")
+        torch.cuda.synchronize()
+        build_s = r["elapsed_s"] / args.cfg4_reps
+        rep.update({"value": n / build_s, "ms_per_build": build_s * 1e3,
+                    "kernel_ms_rank0": ev0.elapsed_time(ev1) / args.cfg4_reps,
+                    "rows_per_rank": r["rows_per_rank"], "assemble": mode,
+                    "assemble_ms": r["gather_s"] * 1e3,
+                    "assemble_GBps": r["bytes_assembled"] / r["gather_s"] / 1e9
+                    if r["gather_s"] > 0 else None,
+                    "value_incl_assembly": n / (build_s + r["gather_s"]),
+                    "parallelism": f"rows-sharded dp{world}: TxH-row slabs, "
+                                   + ("per-rank D2H into one node-shared host table (no "
+                                      "collective)" if mode == "host" else
+                                      "per-column RCCL gathers into rank 0's HBM")})
+        host_tab = r["assembled"] if rank == 0 else None
+        kern_units = r["rays_this_rank"]
+        slab_holder = [r]
+    else:
+        slab = torch.empty((11, n), dtype=torch.float32, device=dev)
+        compute(0, g.table_rows, slab)  # warm-up (st i: 0 -> 1)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(args.cfg4_reps):
+            compute(0, g.table_rows, slab)
+        torch.cuda.synchronize()
+        build_s = (time.perf_counter() - t0) / args.cfg4_reps
+        kms = ev0.elapsed_time(ev1) / args.cfg4_reps
+        rep.update({"value": n / build_s, "ms_per_build": build_s * 1e3, "kernel_ms": kms,
+                    "kernel_value": n / (kms * 1e-3), "parallelism": "single GPU"})
+        kern_units = n
+        if want_host:
+            t1 = time.perf_counter()
+            host_np = np.empty((11, n), dtype=np.float32)
+            register(host_np.ctypes.data, host_np.nbytes)
+            rep["host_alloc_register_s"] = time.perf_counter() - t1
+            host_tab = torch.from_numpy(host_np)
+            e2, e3 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e2.record(stream)
+            host_copy(slab, n, host_tab, 0)
+            e3.record(stream)
+            torch.cuda.synchronize()
+            d2h_ms = e2.elapsed_time(e3)
+            rep.update({"assemble": "host", "assemble_ms": d2h_ms,
+                        "assemble_GBps": 44 * n / (d2h_ms * 1e-3) / 1e9,
+                        "value_incl_assembly": n / (build_s + d2h_ms * 1e-3)})
+        else:
+            host_tab = slab
+        slab_holder = [slab]
+    rep["roofline"] = counter_roofline("table_kernel_cfg4", kern_units,
+                                       rep.get("kernel_ms") or rep.get("kernel_ms_rank0"), pmc,
+                                       44.0)
+    if rank == 0 and not args.no_cpu:
+        import oracle
+        from tests import parity
+        om = oracle.load_atmosphere(os.path.join(ROOT, "airiceraytracing_amd", "data",
+                                                 "Atmosphere.dat.gz"))
+        og = oracle.grid_init(CFG4["depth_cm"], CFG4["ice_cm"], CFG4["height_step"],
+                              CFG4["start_angle"], CFG4["stop_angle"], CFG4["angle_step"])
+        rows = cfg4_check_rows(g.table_rows)
+        worst, nan_ok = 0, True
+        for r_ in rows:
+            got = host_tab[:, r_ * asteps:(r_ + 1) * asteps].cpu().numpy()
+            ref = oracle.table_rows(om, og, r_, r_ + 1, nthreads=min(16, args.cpu_threads))
+            worst = max(worst, parity.float_ulp_diff(got, ref))
+            nan_ok &= bool(np.array_equal(np.isnan(got), np.isnan(ref)))
+        rep["parity_vs_cpu"] = {"rows": rows, "rays": len(rows) * asteps,
+                                "checked_in": "host-assembled table" if rep.get("assemble") ==
+                                "host" else "device table",
+                                "max_float_ulps": int(worst), "nan_pattern_equal": nan_ok}
+    # release the 38.4 GB (device slab, page-locked host table) before the next line item
+    if distributed:
+        r = slab_holder[0]
+        if r.get("host") is not None:
+            r["host"].unregister(unregister)
+            r["host"].close()
+    elif want_host:
+        unregister(host_np.ctypes.data)
+    del host_tab, slab_holder
+    torch.cuda.synchronize()
+    torch.cuda.empty_cache()
+    return rep
 
 
 def minimizer_cpu_baseline(args, om, txh, dst, dep, nthr, info) -> dict:

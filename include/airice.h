@@ -335,6 +335,18 @@ int airice_memcpy_h2d(void *dst, const void *src, size_t bytes);
 int airice_memcpy_d2h(void *dst, const void *src, size_t bytes);
 int airice_synchronize(void);
 
+/* Host assembly of tables (MakeRayTracingTable keeps AllTableAllAntData in host memory,
+ * .cc:2101-2136): copy n_rays entries of the 11 float columns of a device table (column stride
+ * d_ld) into a host table (column stride h_ld), stream-ordered (one 2-D DMA: hipMemcpy2DAsync).
+ * h_table should be pinned (hipHostMalloc'd or registered with airice_host_register) for the copy
+ * to be asynchronous at full PCIe rate.  A rank of a sharded build copies its row slab to
+ * h_table + (first ray of the slab). */
+int airice_table_to_host(const float *d_table, size_t d_ld, size_t n_rays, float *h_table,
+                         size_t h_ld, void *stream);
+/* Page-lock an existing host range for DMA (hipHostRegister, portable) / undo it. */
+int airice_host_register(void *ptr, size_t bytes);
+int airice_host_unregister(void *ptr);
+
 /* Kernel timing (bench.py's roofline legs; no reference counterpart).  When on, each launch
  * of a timed kernel is bracketed by a hipEvent pair on its own stream.  Names:
  * "table_kernel", "roots_kernel" (roots_kernel / roots_sorted_kernel, the minimizer's root

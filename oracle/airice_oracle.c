@@ -198,7 +198,11 @@ int or_parse_atmosphere(const char *text, size_t len, double pi, or_medium *m) {
     }
     if (layer > 0) { if (ngroups < 16) group_end[ngroups] = (int)npts; ngroups++; }
   }
-  if (ngroups < 1 || npts < 3) { free(h); free(nv); return -1; }
+  /* GSL's cspline needs >= 3 knots (gsl_spline_alloc fails, and the reference's default GSL
+   * error handler aborts, .cc:932); a profile past the ATMLAY bounds (more than 4 air layers)
+   * makes the reference index ATMLAY out of range (.cc:110).  Both are rejected, as the library
+   * rejects them (airice_host.cpp). */
+  if (ngroups < 1 || ngroups + 1 > 4 || npts < 4) { free(h); free(nv); return -1; }
   /* drop the duplicated last data point from the last group (.cc:138-140) */
   npts -= 1;
   group_end[ngroups - 1] -= 1;
@@ -1259,7 +1263,11 @@ void or_table_lookup_batch(const or_medium *m, const or_lookup_table *t, const d
                            const double *dist_cm, const double *depth_cm, double ice_cm, size_t n,
                            double *out, size_t ld, unsigned char *ok, unsigned char *flags,
                            int nthreads) {
+#ifdef _OPENMP
   if (nthreads <= 0) nthreads = omp_get_max_threads();
+#else
+  (void)nthreads;
+#endif
 #pragma omp parallel for schedule(dynamic, 256) num_threads(nthreads)
   for (long i = 0; i < (long)n; ++i) {
     double o[9];

@@ -136,3 +136,55 @@ def test_gloo_bench_sharded_mode_assembles_table_bitwise(world):
     assert ncalls == 3 and gathered
     # every rank but the root sends its rows: 11 float columns per ray
     assert nbytes == (g.height_steps - shard_rows(g.height_steps, world, 0)[1]) * g.angle_steps * 44
+
+
+def _cfg4_mode_worker(rank, world, port, q, assemble, host_path):
+    """bench.py's cfg4 item / --workload cfg4 logic (run_sharded_table with the cfg4 angle grid,
+    coarsened in TxH for the CPU) with the oracle as the slab compute: the table assembled in host
+    memory (SharedHostTable, every rank writing its rows) or by per-column gathers."""
+    import oracle
+    from airiceraytracing_amd.distributed import run_sharded_table
+    from tests.conftest import ATMOSPHERE_GZ
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    m = oracle.load_atmosphere(ATMOSPHERE_GZ)
+    g = oracle.grid_init(-20000.0, 300000.0, 997.0, 90.1, 180.0, 0.37)  # cfg4 angles, coarse
+
+    def compute(begin, count, slab):
+        t = oracle.table_rows(m, g, begin, begin + count)
+        slab[:, :t.shape[1]] = torch.from_numpy(t)
+
+    r = run_sharded_table(g, compute, steps=1, warmup=0, gather_reps=2, assemble=assemble,
+                          host_path=host_path)
+    if rank == 0:
+        q.put((r["assembled"].clone().numpy(), r["bytes_assembled"], r["assemble"]))
+    dist.barrier()
+    if r["host"] is not None:
+        r["host"].close()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("assemble,world", [("host", 2), ("host", 3), ("rccl", 3)])
+def test_gloo_cfg4_mode_assembles_table_bitwise(tmp_path, assemble, world):
+    import oracle
+    from tests.conftest import ATMOSPHERE_GZ
+    ctx = mp.get_context("spawn")
+    q = ctx.SimpleQueue()
+    port = _free_port()
+    host_path = str(tmp_path / "airice_host_table")
+    procs = [ctx.Process(target=_cfg4_mode_worker, args=(r, world, port, q, assemble, host_path))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    table, nbytes, mode = q.get()
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    m = oracle.load_atmosphere(ATMOSPHERE_GZ)
+    g = oracle.grid_init(-20000.0, 300000.0, 997.0, 90.1, 180.0, 0.37)
+    ref = oracle.table_rows(m, g, 0, g.height_steps)
+    assert mode == assemble and table.shape == ref.shape
+    np.testing.assert_array_equal(table.view(np.int32), ref.view(np.int32))
+    if assemble == "host":
+        assert nbytes == ref.size * 4
+        assert not os.path.exists(host_path)  # unlinked once every rank had it mapped

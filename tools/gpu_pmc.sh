@@ -15,10 +15,15 @@ run() { # name, counters, cmd...
   timeout -k 10 300 rocprofv3 --pmc $ctr -d $OUT/$name -o $name --output-format csv -- "$@" > $OUT/$name.log 2>&1 || { echo "pass $name failed rc=$?"; tail -5 $OUT/$name.log; return 1; }
 }
 run ow_a "$P1" /tmp/opweights_bench && \
-run bench_a "$P1" python $R/bench.py --no-cpu --no-multi --no-scalar --steps 3 --warmup 1 --solve-steps 1 && \
-run bench_b "$P2" python $R/bench.py --no-cpu --no-multi --no-scalar --steps 3 --warmup 1 --solve-steps 1 && \
-run bench_w "WRITE_SIZE" python $R/bench.py --no-cpu --no-multi --no-scalar --steps 3 --warmup 1 --solve-steps 1 && \
-run bench_f "FETCH_SIZE" python $R/bench.py --no-cpu --no-multi --no-scalar --steps 3 --warmup 1 --solve-steps 1 && \
+run bench_a "$P1" python $R/bench.py --no-cpu --no-multi --no-scalar --no-cfg4 --no-default-grid --steps 3 --warmup 1 --solve-steps 1 && \
+run bench_b "$P2" python $R/bench.py --no-cpu --no-multi --no-scalar --no-cfg4 --no-default-grid --steps 3 --warmup 1 --solve-steps 1 && \
+run bench_w "WRITE_SIZE" python $R/bench.py --no-cpu --no-multi --no-scalar --no-cfg4 --no-default-grid --steps 3 --warmup 1 --solve-steps 1 && \
+run bench_f "FETCH_SIZE" python $R/bench.py --no-cpu --no-multi --no-scalar --no-cfg4 --no-default-grid --steps 3 --warmup 1 --solve-steps 1 && \
+run cfg4_a "$P1" python $R/bench.py --cfg4-only --cfg4-reps 1 --cfg4-host none --no-cpu && \
+run cfg4_b "$P2" python $R/bench.py --cfg4-only --cfg4-reps 1 --cfg4-host none --no-cpu && \
+run cfg4_w "WRITE_SIZE" python $R/bench.py --cfg4-only --cfg4-reps 1 --cfg4-host none --no-cpu && \
+run cfg4_f "FETCH_SIZE" python $R/bench.py --cfg4-only --cfg4-reps 1 --cfg4-host none --no-cpu && \
 python $R/tools/pmc_summarize.py $OUT/opweights_pmc.json $OUT/ow_a && \
+python $R/tools/pmc_summarize.py $OUT/cfg4_pmc.json $OUT/cfg4_a $OUT/cfg4_b $OUT/cfg4_w $OUT/cfg4_f && \
 python $R/tools/pmc_summarize.py $OUT/bench_pmc.json $OUT/bench_a $OUT/bench_b $OUT/bench_w $OUT/bench_f && \
-python $R/tools/make_pmc_summary.py $OUT/bench_pmc.json $OUT/pmc_summary.json > /dev/null
+python $R/tools/make_pmc_summary.py $OUT/bench_pmc.json $OUT/pmc_summary.json $OUT/cfg4_pmc.json > /dev/null

@@ -41,17 +41,27 @@ def derive(name, c, n_units, kernel_ns=None):
     return d
 
 
+# the cfg4 fine table (`bench.py --cfg4-only`): 97,001 x 8,991 rays in one launch
+UNITS_CFG4 = [("table_kernel", "table_kernel_cfg4", 872135991)]
+
+
 if __name__ == "__main__":
     src, dst = sys.argv[1], sys.argv[2]
     with open(src) as f:
         raw = json.load(f)
-    out = {"_source": "rocprofv3 --pmc passes of `python bench.py --no-cpu --steps 3 "
-                      "--warmup 1 --solve-steps 1` (tools/gpu_pmc.sh), mean per dispatch"}
-    for k, c in raw.items():
-        for prefix, key, n in UNITS:
-            if k.startswith(prefix):
-                out[key] = {**derive(k, c, n), "kernel": k,
-                            "raw": {a: b for a, b in c.items() if not a.startswith("_")}}
+    out = {"_source": "rocprofv3 --pmc passes of `python bench.py --no-cpu --no-cfg4 "
+                      "--no-default-grid --steps 3 --warmup 1 --solve-steps 1` and of `bench.py "
+                      "--cfg4-only` (tools/gpu_pmc.sh), mean per dispatch"}
+    sets = [(raw, UNITS)]
+    if len(sys.argv) > 3:
+        with open(sys.argv[3]) as f:
+            sets.append((json.load(f), UNITS_CFG4))
+    for data, units in sets:
+        for k, c in data.items():
+            for prefix, key, n in units:
+                if k.startswith(prefix):
+                    out[key] = {**derive(k, c, n), "kernel": k,
+                                "raw": {a: b for a, b in c.items() if not a.startswith("_")}}
     with open(dst, "w") as f:
         json.dump(out, f, indent=1)
     print(json.dumps(out, indent=1)[:3000])
