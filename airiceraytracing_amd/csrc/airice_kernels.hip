@@ -1325,6 +1325,32 @@ __device__ __forceinline__ Geometry load_query(const DevMedium& M, const QueryAr
   return shift(H, D, ice, dep);
 }
 
+// A query's raw inputs as the grouping pass stores them in sorted order (group_scatter_kernel):
+// {a, b, c, d} of QueryArgs at the query's index (d: IN_M's thR when given, IN_TRACE's dist).
+struct QueryRec {
+  double a, b, c, d;
+};
+
+// load_query<IN> on a stored record: the same arithmetic on the same values.
+template <int IN>
+__device__ __forceinline__ Geometry load_rec(const DevMedium& M, const QueryArgs& Q,
+                                             const QueryRec& r, double& thR) {
+  Signal s{};
+  s.n_in = 4;
+  s.in[0] = r.a;
+  s.in[1] = r.b;
+  s.in[2] = r.c;
+  s.in[3] = r.d;
+  return load_query<IN>(M, Q, 0, thR, &s);
+}
+
+// Stage 1's (root, status) of a grouped batch, in sorted order; stage 2 finds query k's record
+// at inv[k].  rec == nullptr: the parked output slots (Park) hold them.
+struct SortedPark {
+  const double2* rec;
+  const int* inv;
+};
+
 // Where stage 1 parks (root, status) for stage 2.
 struct Park {
   double* root;
@@ -1517,9 +1543,11 @@ __global__ __launch_bounds__(kGroupThreads) void group_count_kernel(DevMedium M,
 static_assert(kGroupThreads % kGroupBuckets == 0, "lanes per bucket");
 constexpr int kLanesPerBucket = kGroupThreads / kGroupBuckets;
 static_assert((kLanesPerBucket & (kLanesPerBucket - 1)) == 0, "power-of-two lanes per bucket");
+template <int IN>
 __global__ __launch_bounds__(kGroupThreads) void group_scatter_kernel(
-    const int8_t* __restrict__ key, long long n, int rounds, const int* __restrict__ cnt,
-    int* __restrict__ grouped, int* __restrict__ perm) {
+    QueryArgs Q, const int8_t* __restrict__ key, long long n, int rounds,
+    const int* __restrict__ cnt, int* __restrict__ grouped, int* __restrict__ inv,
+    QueryRec* __restrict__ recs) {
   __shared__ int s_tot[kGroupBuckets][kLanesPerBucket], s_pre[kGroupBuckets][kLanesPerBucket];
   __shared__ int s_base[kGroupBuckets];
   const int nb = gridDim.x, blk = blockIdx.x;
@@ -1565,15 +1593,22 @@ __global__ __launch_bounds__(kGroupThreads) void group_scatter_kernel(
     for (int i = 0; i < kGroupItems; ++i) {
       const long long k = k0 + i * kGroupThreads;
       const int b = rr == 0 ? b0[i] : (k < n ? (int)key[k] : -1);
-      if (b >= 0) perm[atomicAdd(&s_base[b], 1)] = (int)k;
+      if (b >= 0) {
+        // the query's inputs move to its sorted position (one 32-byte record), so the root finder
+        // reads them contiguously; inv[k] tells stage 2 where the query's result is parked
+        const int pos = atomicAdd(&s_base[b], 1);
+        const bool has_d = IN == IN_TRACE || (IN == IN_M && Q.d != nullptr);
+        recs[pos] = QueryRec{Q.a[k], Q.b[k], Q.c[k], has_d ? Q.d[k] : 0.0};
+        inv[k] = pos;
+      }
     }
   }
 }
 
 template <int IN>
 __global__ __launch_bounds__(kSortedBlock, AIRICE_SORTED_WAVES) void roots_sorted_kernel(
-    DevMedium M, IceConsts I, QueryArgs Q, Park park, const int* __restrict__ perm,
-    const int* __restrict__ grouped) {
+    DevMedium M, IceConsts I, QueryArgs Q, Park park, const QueryRec* __restrict__ recs,
+    double2* __restrict__ sorted_park, const int* __restrict__ grouped) {
   __shared__ __align__(16) double s_logtab[1 << kLogTableBits][2];
   for (int t = threadIdx.x; t < (1 << kLogTableBits); t += kSortedBlock) {
     s_logtab[t][0] = kLogTable[t][0];
@@ -1581,13 +1616,24 @@ __global__ __launch_bounds__(kSortedBlock, AIRICE_SORTED_WAVES) void roots_sorte
   }
   __syncthreads();
   const long long ks = (long long)blockIdx.x * kSortedBlock + threadIdx.x;
-  if (ks >= *grouped) return;  // past the queries with a bucket (the lookup's fallback lanes)
-  const long long k = perm[ks];
+  if (ks >= *grouped) return;  // past the queries with a bucket
   double thR;
-  const Geometry g = load_query<IN>(M, Q, k, thR);
+  const Geometry g = load_rec<IN>(M, Q, recs[ks], thR);
   const SolveResult r = solve_root(M, I, g, thR, park.exact != 0, &s_logtab[0][0]);
-  park.root[k * park.stride] = r.root;
-  park.status[k * park.stride] = (double)r.status;
+  sorted_park[ks] = make_double2(r.root, (double)r.status);
+}
+
+// Stage 1's result of query k for stage 2.
+__device__ __forceinline__ void parked(const SortedPark& sp, const double* root_slot,
+                                       const double* status_slot, long long k, double& x, int& st) {
+  if (sp.rec != nullptr) {
+    const double2 p = sp.rec[sp.inv[k]];
+    x = p.x;
+    st = (int)p.y;
+  } else {
+    x = *root_slot;
+    st = (int)*status_slot;
+  }
 }
 
 __device__ __forceinline__ bool check_solution(double thd, double D) {
@@ -1618,11 +1664,13 @@ __device__ __forceinline__ void solve_out_body(const DevMedium& M, const IceCons
                                                const QueryArgs& Q, double* __restrict__ out,
                                                size_t ld, uint8_t* __restrict__ status,
                                                long long k, const double* tab,
-                                               WaveRoot wr = WaveRoot{0.0, 0}) {
+                                               WaveRoot wr = WaveRoot{0.0, 0},
+                                               SortedPark sp = SortedPark{nullptr, nullptr}) {
   double thR;
   const Geometry g = WAVE ? wr.g : load_query<IN_M>(M, Q, k, thR);
-  const double x = WAVE ? wr.root : out[10 * ld + k];
-  const int st = WAVE ? wr.status : (int)out[0 * ld + k];
+  double x = wr.root;
+  int st = wr.status;
+  if (!WAVE) parked(sp, out + 10 * ld + k, out + 0 * ld + k, k, x, st);
   const Solved S = WAVE ? evaluate_root_wave(M, I, g, x, st, tab) : evaluate_root(M, I, g, x, st, tab);
   if (WAVE && threadIdx.x != 0) return;
   const double thd = S.thd_ice + S.thd_air;
@@ -1659,12 +1707,13 @@ __device__ __forceinline__ void solve_out_body(const DevMedium& M, const IceCons
 template <int VARIANT>
 __global__ __launch_bounds__(kBlock) void solve_out_kernel(DevMedium M, IceConsts I, QueryArgs Q,
                                                            double* __restrict__ out, size_t ld,
-                                                           uint8_t* __restrict__ status) {
+                                                           uint8_t* __restrict__ status,
+                                                           SortedPark sp) {
   const long long k = (long long)blockIdx.x * kBlock + threadIdx.x;
   __shared__ __align__(16) double s_logtab[1 << kLogTableBits][2];
   stage_log_table(s_logtab);
   if (k >= Q.n) return;
-  solve_out_body<VARIANT>(M, I, Q, out, ld, status, k, &s_logtab[0][0]);
+  solve_out_body<VARIANT>(M, I, Q, out, ld, status, k, &s_logtab[0][0], WaveRoot{0.0, 0}, sp);
 }
 
 // Stage 2 of GetHorizontalDistanceToIntersectionPoint (.cc:945-989): 9 outputs (cm, rad) + bool.
@@ -1672,11 +1721,13 @@ template <bool WAVE = false>
 __device__ __forceinline__ void hdtip_out_body(const DevMedium& M, const IceConsts& I,
                                                const QueryArgs& Q, double* __restrict__ out,
                                                size_t ld, uint8_t* __restrict__ ok, long long k,
-                                               const double* tab, WaveRoot wr = WaveRoot{0.0, 0}) {
+                                               const double* tab, WaveRoot wr = WaveRoot{0.0, 0},
+                                               SortedPark sp = SortedPark{nullptr, nullptr}) {
   double thR;
   const Geometry g = WAVE ? wr.g : load_query<IN_CM>(M, Q, k, thR);
-  const double x = WAVE ? wr.root : out[4 * ld + k];
-  const int st = WAVE ? wr.status : (int)out[0 * ld + k];
+  double x = wr.root;
+  int st = wr.status;
+  if (!WAVE) parked(sp, out + 4 * ld + k, out + 0 * ld + k, k, x, st);
   const Solved S = WAVE ? evaluate_root_wave(M, I, g, x, st, tab) : evaluate_root(M, I, g, x, st, tab);
   if (WAVE && threadIdx.x != 0) return;
   const double thd = S.thd_ice + S.thd_air;
@@ -1696,12 +1747,12 @@ __device__ __forceinline__ void hdtip_out_body(const DevMedium& M, const IceCons
 
 __global__ __launch_bounds__(kBlock) void hdtip_out_kernel(DevMedium M, IceConsts I, QueryArgs Q,
                                                            double* __restrict__ out, size_t ld,
-                                                           uint8_t* __restrict__ ok) {
+                                                           uint8_t* __restrict__ ok, SortedPark sp) {
   const long long k = (long long)blockIdx.x * kBlock + threadIdx.x;
   __shared__ __align__(16) double s_logtab[1 << kLogTableBits][2];
   stage_log_table(s_logtab);
   if (k >= Q.n) return;
-  hdtip_out_body(M, I, Q, out, ld, ok, k, &s_logtab[0][0]);
+  hdtip_out_body(M, I, Q, out, ld, ok, k, &s_logtab[0][0], WaveRoot{0.0, 0}, sp);
 }
 
 // Stage 2 of the table lookup's minimizer fallback (.cc:1417-1456): the reference passes its
@@ -1755,12 +1806,14 @@ template <bool WAVE = false>
 __device__ __forceinline__ void trace_out_body(const DevMedium& M, const IceConsts& I,
                                                const QueryArgs& Q, double* __restrict__ out10,
                                                long long k, const double* tab,
-                                               WaveRoot wr = WaveRoot{0.0, 0}) {
+                                               WaveRoot wr = WaveRoot{0.0, 0},
+                                               SortedPark sp = SortedPark{nullptr, nullptr}) {
   double thR;
   const Geometry g = WAVE ? wr.g : load_query<IN_TRACE>(M, Q, k, thR);
   double* o = out10 + 10 * k;
-  const double x = WAVE ? wr.root : o[5];
-  const int st = WAVE ? wr.status : (int)o[9];
+  double x = wr.root;
+  int st = wr.status;
+  if (!WAVE) parked(sp, o + 5, o + 9, k, x, st);
   const Solved S = WAVE ? evaluate_root_wave(M, I, g, x, st, tab) : evaluate_root(M, I, g, x, st, tab);
   if (WAVE && threadIdx.x != 0) return;
   const double thd = S.thd_ice + S.thd_air;
@@ -1784,12 +1837,13 @@ __device__ __forceinline__ void trace_out_body(const DevMedium& M, const IceCons
 }
 
 __global__ __launch_bounds__(kBlock) void trace_out_kernel(DevMedium M, IceConsts I, QueryArgs Q,
-                                                           double* __restrict__ out10) {
+                                                           double* __restrict__ out10,
+                                                           SortedPark sp) {
   const long long k = (long long)blockIdx.x * kBlock + threadIdx.x;
   __shared__ __align__(16) double s_logtab[1 << kLogTableBits][2];
   stage_log_table(s_logtab);
   if (k >= Q.n) return;
-  trace_out_body(M, I, Q, out10, k, &s_logtab[0][0]);
+  trace_out_body(M, I, Q, out10, k, &s_logtab[0][0], WaveRoot{0.0, 0}, sp);
 }
 
 // One query, both stages in one launch (the scalar C++ / ctypes entry points): one wave finds the
@@ -1904,9 +1958,13 @@ size_t group_min_batch() {
 
 // Stage 1 of every minimizer launch: roots_kernel (block-local grouping) for small batches and
 // debug statistics, the batch-wide grouping otherwise (stream-ordered scratch, scratch_alloc).
+// A grouped launch returns the sorted parking (sp) its stage-2 kernel reads, and the scratch
+// block (ws) to release after that kernel: release_roots().
 template <int IN>
 static int launch_roots(const DevMedium& M, const IceConsts& I, const QueryArgs& Q,
-                        const Park& park, size_t n, hipStream_t st) {
+                        const Park& park, size_t n, hipStream_t st, SortedPark& sp, void*& ws) {
+  sp = SortedPark{nullptr, nullptr};
+  ws = nullptr;
   const size_t group_min = group_min_batch();
   // (the table lookup's fallback pass stays block-local: its batch is the whole lookup batch,
   // of which typically well under 1 % of lanes are fallback lanes)
@@ -1929,27 +1987,36 @@ static int launch_roots(const DevMedium& M, const IceConsts& I, const QueryArgs&
   const int rounds = (int)((chunks + kGroupBlocks - 1) / kGroupBlocks);
   const unsigned nb = (unsigned)((chunks + rounds - 1) / rounds);
   const size_t m = (size_t)kGroupBuckets * nb;
-  const size_t ws_bytes = sizeof(int) * (m + 1 + n) + n;  // cnt, grouped count, perm, keys
-  void* ws = nullptr;
+  // scratch: sorted query records (32 B), sorted (root, status) (16 B), inv (4 B) and key (1 B)
+  // per query, then the bucket counts and the grouped count
+  const size_t ws_bytes = (sizeof(QueryRec) + sizeof(double2) + sizeof(int) + 1) * n +
+                          sizeof(int) * (m + 1);
   if (scratch_alloc(&ws, ws_bytes, st) != hipSuccess) return AIRICE_EHIP;
-  int* cnt = static_cast<int*>(ws);
+  QueryRec* recs = static_cast<QueryRec*>(ws);
+  double2* sorted = reinterpret_cast<double2*>(recs + n);
+  int* inv = reinterpret_cast<int*>(sorted + n);
+  int* cnt = inv + n;
   int* grouped = cnt + m;
-  int* perm = grouped + 1;
-  int8_t* key = reinterpret_cast<int8_t*>(perm + n);
+  int8_t* key = reinterpret_cast<int8_t*>(grouped + 1);
   ktimer_begin(KT_GROUP, st);
   hipLaunchKernelGGL(group_count_kernel<IN>, dim3(nb), dim3(kGroupThreads), 0, st, M, Q,
                      thresholds, rounds, key, cnt);
-  hipLaunchKernelGGL(group_scatter_kernel, dim3(nb), dim3(kGroupThreads), 0, st, key,
-                     (long long)n, rounds, cnt, grouped, perm);
+  hipLaunchKernelGGL(group_scatter_kernel<IN>, dim3(nb), dim3(kGroupThreads), 0, st, Q, key,
+                     (long long)n, rounds, cnt, grouped, inv, recs);
   ktimer_end(KT_GROUP, st);
   const unsigned sorted_blocks = (unsigned)((n + kSortedBlock - 1) / kSortedBlock);
   ktimer_begin(KT_ROOTS, st);
   hipLaunchKernelGGL(roots_sorted_kernel<IN>, dim3(sorted_blocks), dim3(kSortedBlock), 0, st, M, I,
-                     Q, park, perm, grouped);
+                     Q, park, recs, sorted, grouped);
   ktimer_end(KT_ROOTS, st);
-  const int rc = launch_ok();
-  if (hipFreeAsync(ws, st) != hipSuccess) return AIRICE_EHIP;
-  return rc;
+  sp = SortedPark{sorted, inv};
+  return launch_ok();
+}
+
+// Stream-ordered release of a grouped launch's scratch (after its stage-2 kernel).
+static int release_roots(void* ws, hipStream_t st) {
+  if (ws != nullptr && hipFreeAsync(ws, st) != hipSuccess) return AIRICE_EHIP;
+  return AIRICE_OK;
 }
 
 
@@ -2164,7 +2231,9 @@ int launch_solve(const DevMedium& M, const IceConsts& I, int variant, const doub
                          Q, park, out, ld, status, sig);
     return launch_ok();
   }
-  if (int rc = launch_roots<IN_M>(M, I, Q, park, n, st)) return rc;
+  SortedPark sp;
+  void* ws;
+  if (int rc = launch_roots<IN_M>(M, I, Q, park, n, st, sp, ws)) return rc;
   if (park.stats != nullptr) {  // debug: append the per-query counts (synchronous)
     std::vector<int> h(3 * n);
     if (hipStreamSynchronize(st) != hipSuccess ||
@@ -2179,12 +2248,14 @@ int launch_solve(const DevMedium& M, const IceConsts& I, int variant, const doub
   ktimer_begin(KT_OUT, st);
   if (variant == AIRICE_VARIANT_MULTIRAY)
     hipLaunchKernelGGL(solve_out_kernel<AIRICE_VARIANT_MULTIRAY>, grid, block, 0, st, M, I, Q, out,
-                       ld, status);
+                       ld, status, sp);
   else
     hipLaunchKernelGGL(solve_out_kernel<AIRICE_VARIANT_PYWRAPPER>, grid, block, 0, st, M, I, Q,
-                       out, ld, status);
+                       out, ld, status, sp);
   ktimer_end(KT_OUT, st);
-  return launch_ok();
+  const int rc = launch_ok();
+  if (int rf = release_roots(ws, st)) return rf;
+  return rc;
 }
 
 int launch_hdtip(const DevMedium& M, const IceConsts& I, const double* src, const double* dist,
@@ -2199,11 +2270,15 @@ int launch_hdtip(const DevMedium& M, const IceConsts& I, const double* src, cons
                        park, out, ld, ok, take_scalar_signal());
     return launch_ok();
   }
-  if (int rc = launch_roots<IN_CM>(M, I, Q, park, n, st)) return rc;
+  SortedPark sp;
+  void* ws;
+  if (int rc = launch_roots<IN_CM>(M, I, Q, park, n, st, sp, ws)) return rc;
   ktimer_begin(KT_OUT, st);
-  hipLaunchKernelGGL(hdtip_out_kernel, grid, block, 0, st, M, I, Q, out, ld, ok);
+  hipLaunchKernelGGL(hdtip_out_kernel, grid, block, 0, st, M, I, Q, out, ld, ok, sp);
   ktimer_end(KT_OUT, st);
-  return launch_ok();
+  const int rc = launch_ok();
+  if (int rf = release_roots(ws, st)) return rf;
+  return rc;
 }
 
 int launch_lookup_fallback(const DevMedium& M, const IceConsts& I, const double* src,
@@ -2221,7 +2296,10 @@ int launch_lookup_fallback(const DevMedium& M, const IceConsts& I, const double*
                        I, Q, park, out, ld, ok, take_scalar_signal());
     return launch_ok();
   }
-  if (int rc = launch_roots<IN_CM100>(M, I, Q, park, n, st)) return rc;
+  SortedPark sp;  // the fallback pass is never grouped (launch_roots): the parked slots
+  void* ws;
+  if (int rc = launch_roots<IN_CM100>(M, I, Q, park, n, st, sp, ws)) return rc;
+  if (sp.rec != nullptr) return AIRICE_EINVAL;
   hipLaunchKernelGGL(lookup_fallback_out_kernel, grid, block, 0, st, M, I, Q, out, ld, ok);
   return launch_ok();
 }
@@ -2237,11 +2315,15 @@ int launch_trace(const DevMedium& M, const IceConsts& I, const double* depth, co
                        park, out10, 0, nullptr, take_scalar_signal());
     return launch_ok();
   }
-  if (int rc = launch_roots<IN_TRACE>(M, I, Q, park, n, st)) return rc;
+  SortedPark sp;
+  void* ws;
+  if (int rc = launch_roots<IN_TRACE>(M, I, Q, park, n, st, sp, ws)) return rc;
   ktimer_begin(KT_OUT, st);
-  hipLaunchKernelGGL(trace_out_kernel, grid, block, 0, st, M, I, Q, out10);
+  hipLaunchKernelGGL(trace_out_kernel, grid, block, 0, st, M, I, Q, out10, sp);
   ktimer_end(KT_OUT, st);
-  return launch_ok();
+  const int rc = launch_ok();
+  if (int rf = release_roots(ws, st)) return rf;
+  return rc;
 }
 
 }  // namespace airice

@@ -7,4 +7,4 @@ ROOT=$(cd "$(dirname "$0")/.." && pwd)
 cd "$SRC"
 /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -ffp-contract=off -fno-fast-math -mllvm -disable-machine-licm \
   -Wno-unused-result -I"$ROOT/include" -I. "$@" -shared -o "$OUT" \
-  airice_kernels.hip airice_lookup.hip airice_path.hip airice_rtf.hip airice_runtime.cpp compat_multiray.cpp compat_rtf.cpp
+  $(ls *.hip *.cpp | grep -v '^cli_')
