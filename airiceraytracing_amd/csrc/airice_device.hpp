@@ -48,6 +48,16 @@
 #ifndef AIRICE_RCP_NEWTON
 #define AIRICE_RCP_NEWTON 1
 #endif
+// fast_sqrt's q = 0 case without a select: v_rsq_f64(q + 2^-1074) is finite at q = 0 and the
+// added 2^-1074 leaves every q >= 2^-1020 (and every q <= 0, NaN) unchanged
+#ifndef AIRICE_SQRT_TINY
+#define AIRICE_SQRT_TINY 1
+#endif
+// log_ratio's fast-path test as two v_cmp_class (q and b positive normal) instead of the
+// integer range tests on their high words
+#ifndef AIRICE_CLASS_CHECK
+#define AIRICE_CLASS_CHECK 1
+#endif
 
 namespace airice {
 
@@ -238,7 +248,11 @@ __device__ __forceinline__ void sqrt_rsqrt(double q, double& s, double& rs) {
 
 // sqrt(q) (same iteration, no reciprocal): within ~1 ulp; q = 0 -> 0, q < 0 / NaN -> NaN.
 __device__ __forceinline__ double fast_sqrt(double q) {
+#if AIRICE_SQRT_TINY
+  const double y = __builtin_amdgcn_rsq(q + 0x1p-1074);
+#else
   const double y = __builtin_amdgcn_rsq(q);
+#endif
   double g = q * y, h = 0.5 * y;
   const double e = __builtin_fma(-h, g, 0.5);
   g = __builtin_fma(g, e, g);
@@ -249,7 +263,11 @@ __device__ __forceinline__ double fast_sqrt(double q) {
     d = __builtin_fma(-g, g, q);
     g = __builtin_fma(d, h, g);
   }
+#if AIRICE_SQRT_TINY
+  return g;  // q = 0: y finite, so g = 0 * y = 0 through every step
+#else
   return (q == 0.0) ? q : g;
+#endif
 }
 
 // a / b for b positive and normal (2^-1000 <= b < 2^1000): v_rcp_f64 (24 bits, measured by
@@ -334,7 +352,12 @@ __device__ __forceinline__ double log_ratio_fast(double a, double b, const doubl
   const double q = __builtin_fma(__builtin_fma(-b, q0, a), y, q0);
   // a > 0 and q in range cover a (a tiny / huge / inf / NaN shows in q or in a > 0); b in range
   // keeps v_rcp_f64 and the Newton steps clear of overflow and denormals
-#if AIRICE_INT_RANGE
+#if AIRICE_CLASS_CHECK
+  // b and q positive normal (class mask 1 << 8): a <= 0 or NaN, b <= 0, NaN, denormal or so
+  // large that v_rcp_f64 leaves the normal range, and q zero, denormal, infinite or NaN all fail;
+  // with b > 0 and q > 0 also a > 0
+  ok = __builtin_amdgcn_class(b, 1 << 8) && __builtin_amdgcn_class(q, 1 << 8);
+#elif AIRICE_INT_RANGE
   // the same test on the high words: 2^-1000 <= b, q < 2^1000 as unsigned exponent ranges
   // (a negative, zero, NaN or infinite value falls outside; a <= 0 or NaN makes q so)
   ok = (hi_word(b) - 0x01700000u < 0x7D000000u) && (hi_word(q) - 0x01700000u < 0x7D000000u);

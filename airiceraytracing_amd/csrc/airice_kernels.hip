@@ -75,6 +75,12 @@ constexpr int kTableBlock = AIRICE_TABLE_BS;
 #ifndef AIRICE_TWO_RAY_MAX
 #define AIRICE_TWO_RAY_MAX 0
 #endif
+// table stores with an SGPR column base and a 32-bit lane byte offset (global_store saddr form):
+// launches are split at 2^30 rays so that 4 k < 2^32
+#ifndef AIRICE_SADDR_STORE
+#define AIRICE_SADDR_STORE 1
+#endif
+constexpr long long kMaxLaunchRays = AIRICE_SADDR_STORE ? (1LL << 30) : (1LL << 31);
 constexpr int kTwoRayMin = AIRICE_TWO_RAY_MIN;
 constexpr int kTwoRayMax = AIRICE_TWO_RAY_MAX;
 
@@ -211,6 +217,14 @@ __device__ __forceinline__ void prio_remaining(bool on, int rem) {
     __builtin_amdgcn_s_setprio(1);
   else
     __builtin_amdgcn_s_setprio(0);
+}
+
+// I.lower[il].ratio for a lane-varying il (selects)
+__device__ __forceinline__ double sel_lower_ratio(const IceConsts& I, int il) {
+  double r = I.lower[0].ratio;
+#pragma unroll
+  for (int l = 1; l < kMaxLayers; ++l) r = (il == l) ? I.lower[l].ratio : r;
+  return r;
 }
 
 // want_inc: dummy[12] (the incidence angle on the ice, one asin) is not a table column
@@ -359,6 +373,29 @@ __device__ __forceinline__ void table_ray(const DevMedium& M, const IceConsts& I
   double d[18];
   ray_solution_row(M, I, rc, th, G.in_ice != 0, d, full != nullptr, tab, top_hi, prio_after);
   const size_t ld = G.ld;
+#if AIRICE_SADDR_STORE
+  // AllTableAllAntData columns (.cc:2101-2111): the column base is wave-uniform, the lane's byte
+  // offset fits 32 bits (k < 2^30 per launch)
+  {
+    char* tb = reinterpret_cast<char*>(table);
+    const size_t ldb = ld * sizeof(float);
+    const uint32_t off = (uint32_t)k * 4u;
+    auto st = [&](int c, double v) { *reinterpret_cast<float*>(tb + c * ldb + off) = (float)v; };
+    st(0, d[1]);
+    st(1, d[2]);
+    st(2, d[7]);
+    st(3, d[6]);
+    st(4, d[11]);
+    st(5, d[3]);
+    st(6, d[14]);
+    st(7, d[15]);
+    st(8, d[16]);
+    st(9, d[17]);
+    st(10, d[13]);
+  }
+  if (false)
+#endif
+  {
   // AllTableAllAntData columns (.cc:2101-2111)
   table[0 * ld + k] = (float)d[1];
   table[1 * ld + k] = (float)d[2];
@@ -371,6 +408,7 @@ __device__ __forceinline__ void table_ray(const DevMedium& M, const IceConsts& I
   table[8 * ld + k] = (float)d[16];
   table[9 * ld + k] = (float)d[17];
   table[10 * ld + k] = (float)d[13];
+  }
   if (full != nullptr) {
 #pragma unroll
     for (int c = 0; c < 18; ++c) full[c * ld + k] = d[c];
@@ -476,6 +514,136 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(AIRICE_TABLE
   a = __builtin_amdgcn_readfirstlane(a);
   table_block<BS, 1, false>(M, Iv[a], Gv[a], map.table[a], nullptr, nullptr,
                             blockIdx.x - (unsigned)map.begin[a]);
+}
+
+// One forward ray spread over a wave (the one-query GetRayTracingSolutions call): the running
+// sine chain is cheap, so every lane walks it and knows the input sine of each segment; lane 0
+// then traces the Tx-layer segment, lanes 1-3 the lower layers (top-1, top-2, top-3 while >= bot),
+// lane 4 the segment in the ice, all at once, while the angle outputs and the Fresnel
+// coefficients (functions of the chain's sines only) run beside them on every lane; the sums are
+// formed in ray_solution_row's order from the lanes' values.  The same operations on the same
+// values as ray_solution (hence the same bits), with the ~1,000-deep one-lane chain cut to about
+// one segment.
+__device__ __forceinline__ void ray_solution_wave(const DevMedium& M, const IceConsts& I,
+                                                  double theta, double H, bool in_ice, double* d,
+                                                  const double* tab) {
+  const int lane = (int)(threadIdx.x & 63);
+  const RowConst rc = row_const(M, I, H);
+  const int top = rc.top, bot = I.bot;
+  const bool any = rc.any != 0;
+  const double A2 = M.A_air * M.A_air, A2i = M.A_ice * M.A_ice;
+  // the chain: input sine of every segment, and the sine after the air layers
+  double v = sin_start((180 - theta) * M.d2r);
+  double sin_in[5] = {0.0, 0.0, 0.0, 0.0, 0.0};
+  bool on[5] = {false, false, false, false, false};
+  if (any) {
+    sin_in[0] = sin_asin(v);
+    on[0] = true;
+    v = sin_asin(rc.seg.ratio * sin_in[0]);
+  }
+#pragma unroll
+  for (int j = 1; j <= 3; ++j) {
+    const int il = top - j;
+    if (il >= bot && il >= 0) {
+      sin_in[j] = v;
+      on[j] = true;
+      v = sin_asin(sel_lower_ratio(I, il) * v);
+    }
+  }
+  const double vinc = any ? v : 0.0;
+  const double u_ice = sin_asin(I.n_ratio * vinc);
+  sin_in[4] = u_ice;
+  on[4] = in_ice;
+  // this lane's segment
+  const int j = lane < 5 ? lane : 0;
+  SegConst S = rc.seg;
+  double sj = sin_in[0];
+#pragma unroll
+  for (int q = 1; q <= 4; ++q) {
+    const bool me = j == q;
+    sj = me ? sin_in[q] : sj;
+  }
+  const int il = top - j;
+#pragma unroll
+  for (int l = 0; l < kMaxLayers; ++l) {
+    const bool me = j >= 1 && j <= 3 && il == l;
+    const SegConst& c = I.lower[l];
+    S = SegConst{me ? c.Tn : S.Tn,       me ? c.Ty2 : S.Ty2,     me ? c.TAy : S.TAy,
+                 me ? c.Rn : S.Rn,       me ? c.Ry2 : S.Ry2,     me ? c.RAy : S.RAy,
+                 me ? c.ratio : S.ratio, me ? c.invC : S.invC,   me ? c.invCc : S.invCc,
+                 me ? c.dCx : S.dCx,     me ? c.dACx : S.dACx};
+  }
+  {
+    const bool me = j == 4;
+    const SegConst& c = I.iceseg;
+    S = SegConst{me ? c.Tn : S.Tn,       me ? c.Ty2 : S.Ty2,     me ? c.TAy : S.TAy,
+                 me ? c.Rn : S.Rn,       me ? c.Ry2 : S.Ry2,     me ? c.RAy : S.RAy,
+                 me ? c.ratio : S.ratio, me ? c.invC : S.invC,   me ? c.invCc : S.invCc,
+                 me ? c.dCx : S.dCx,     me ? c.dACx : S.dACx};
+  }
+  const bool air = j != 4;
+  double v_unused;
+  const Segment sg = segment_const(S, air ? M.A_air : M.A_ice, air ? A2 : A2i, sj, air, v_unused,
+                                   tab);
+  // outputs that are functions of the chain's sines (every lane; lane 0 writes)
+  const double inc = any ? k_asin(vinc) * M.r2d : 0.0;
+  const double recv_ice = k_asin(sin_asin(I.iceseg.ratio * u_ice)) * M.r2d;
+  double tS, tP;
+  fresnel_from_sine(I.n_air_ice, I.n_ice0, I.n_ratio, vinc, tS, tP);
+  double thd_air = 0.0, t_air = 0.0, geo_air = 0.0;
+#pragma unroll
+  for (int q = 0; q <= 3; ++q) {
+    const double a = __shfl(sg.thd, q), b = __shfl(sg.t, q), c = __shfl(sg.geo, q);
+    if (on[q]) {
+      thd_air += a;
+      t_air += b;
+      geo_air += c;
+    }
+  }
+  double thd_ice = 0.0, t_ice = 0.0, geo_ice = 0.0;
+  {
+    const double a = __shfl(sg.thd, 4), b = __shfl(sg.t, 4), c = __shfl(sg.geo, 4);
+    if (on[4]) {
+      thd_ice += a;
+      t_ice += b;
+      geo_ice += c;
+    }
+  }
+  if (lane != 0) return;
+  d[0] = 0;
+  d[1] = H;
+  d[2] = thd_air + thd_ice;
+  d[3] = thd_air;
+  d[4] = thd_ice;
+  d[5] = (t_ice + t_air) * kSpeedC;
+  d[6] = t_air * kSpeedC;
+  d[7] = t_ice * kSpeedC;
+  d[8] = (t_ice + t_air) * 1e9;
+  d[9] = t_air * 1e9;
+  d[10] = t_ice * 1e9;
+  d[11] = theta;
+  d[12] = inc;
+  d[13] = in_ice ? recv_ice : 0.0;
+  d[14] = tS;
+  d[15] = tP;
+  d[16] = geo_air;
+  d[17] = geo_ice;
+}
+
+// One-ray launch (n = 1): one wave, ray_solution_wave, lane 0 writes dummy[0..17].
+__global__ __launch_bounds__(64) void scalar_ray_kernel(DevMedium M, IceConsts I,
+                                                        const double* __restrict__ launch,
+                                                        const double* __restrict__ txh, int in_ice,
+                                                        double* __restrict__ out, size_t ld,
+                                                        Signal sig) {
+  const bool inl = sig.n_in >= 2;  // the inputs in the kernel arguments
+  double d[18];
+  ray_solution_wave(M, I, inl ? sig.in[0] : launch[0], inl ? sig.in[1] : txh[0], in_ice != 0, d,
+                    &kLogTable[0][0]);
+  if (threadIdx.x != 0) return;
+#pragma unroll
+  for (int c = 0; c < 18; ++c) out[c * ld] = d[c];
+  signal_done(sig);
 }
 
 __global__ __launch_bounds__(kBlock) void rays_kernel(DevMedium M, IceConsts I,
@@ -2039,8 +2207,8 @@ int launch_table(const DevMedium& M, const IceConsts& I, const airice_grid* g, i
   A.rows_per_block = std::min(kTableBlock, (kTableBlock - 1) / g->angle_steps + 2);
   static const char* trace_path = getenv("AIRICE_TABLE_TRACE");
   static const int force_r = getenv("AIRICE_TABLE_RPL") ? atoi(getenv("AIRICE_TABLE_RPL")) : 0;
-  // ray indices are 32-bit inside a launch: grids of 2^31 rays or more go in row slabs
-  const int max_rows = (int)std::max<long long>(1, ((1LL << 31) - 2 * kTableBlock) / g->angle_steps);
+  // ray indices are 32-bit inside a launch: grids of kMaxLaunchRays or more go in row slabs
+  const int max_rows = (int)std::max<long long>(1, (kMaxLaunchRays - 2 * kTableBlock) / g->angle_steps);
   for (int done = 0; done < row_count;) {
     const int rows = std::min(max_rows, row_count - done);
     const size_t off = (size_t)done * (size_t)g->angle_steps;
@@ -2132,7 +2300,7 @@ int launch_table_multi(const DevMedium& M, const IceConsts* Ih, const airice_gri
     A.rows_per_block = rpb;
     A.row0 = 0;
     const long long rays = (long long)g->table_rows * g->angle_steps;
-    if (rays >= (1LL << 31) - 2 * kTableBlock || lds[a] < (size_t)rays) {
+    if (rays >= kMaxLaunchRays - 2 * kTableBlock || lds[a] < (size_t)rays) {
       set_error("antenna %d: %lld rays (ld %zu) do not fit one multi-antenna launch", a, rays,
                 lds[a]);
       return AIRICE_EINVAL;
@@ -2205,9 +2373,13 @@ int launch_table_multi(const DevMedium& M, const IceConsts* Ih, const airice_gri
 int launch_rays(const DevMedium& M, const IceConsts& I, const double* launch, const double* txh,
                 int in_ice, size_t n, double* out, size_t ld, hipStream_t st) {
   if (n == 0) return AIRICE_OK;
-  const Signal sig = n == 1 ? take_scalar_signal() : Signal{};
+  if (n == 1) {  // one ray: spread over a wave (ray_solution_wave)
+    hipLaunchKernelGGL(scalar_ray_kernel, dim3(1), dim3(64), 0, st, M, I, launch, txh, in_ice, out,
+                       ld, take_scalar_signal());
+    return launch_ok();
+  }
   hipLaunchKernelGGL(rays_kernel, dim3(grid_for((long long)n)), dim3(kBlock), 0, st, M, I, launch,
-                     txh, in_ice, (long long)n, out, ld, sig);
+                     txh, in_ice, (long long)n, out, ld, Signal{});
   return launch_ok();
 }
 

@@ -91,16 +91,23 @@ __device__ double rtf_prop_time(const DevMedium& M, double A, double Rx, double 
   return t;
 }
 
-// GetLayerHitPointPar (.cc:399-527): {x1, ReceiveAngle (deg), L, time}
-__device__ void rtf_hit_point(const DevMedium& M, double n_layer1, double Rx, double Tx,
-                              double IncidentAng, int air, double out[4]) {
+// The Snell part of GetLayerHitPointPar (.cc:399-454): the receive angle (radians) and L.
+__device__ void rtf_hit_L(const DevMedium& M, double n_layer1, double Rx, double Tx,
+                          double IncidentAng, int air, double& ReceiveAngle, double& Lvalue) {
   const double SurfaceRayIncidentAngle = IncidentAng * M.d2r;
-  const double A = air ? M.A_air : M.A_ice;
   const double nzRx = rtf_nz(M, Rx, air);
   const double nzTx = rtf_nz(M, Tx, air);
   const double Lang = asin((n_layer1 / nzTx) * sin(SurfaceRayIncidentAngle));
-  const double ReceiveAngle = asin((rtf_nz(M, Tx, air) * sin(Lang)) / rtf_nz(M, Rx, air));
-  const double Lvalue = nzRx * sin(ReceiveAngle);
+  ReceiveAngle = asin((rtf_nz(M, Tx, air) * sin(Lang)) / rtf_nz(M, Rx, air));
+  Lvalue = nzRx * sin(ReceiveAngle);
+}
+
+// GetLayerHitPointPar (.cc:399-527): {x1, ReceiveAngle (deg), L, time}
+__device__ void rtf_hit_point(const DevMedium& M, double n_layer1, double Rx, double Tx,
+                              double IncidentAng, int air, double out[4]) {
+  const double A = air ? M.A_air : M.A_ice;
+  double ReceiveAngle, Lvalue;
+  rtf_hit_L(M, n_layer1, Rx, Tx, IncidentAng, air, ReceiveAngle, Lvalue);
   out[0] = rtf_optical_path(M, A, Rx, Tx, Lvalue, air);
   out[1] = ReceiveAngle * M.r2d;
   out[2] = Lvalue;
@@ -498,12 +505,131 @@ __device__ double mr_min_launch(const DevMedium& M, double x, double AirTxHeight
   return D - (thd_ice + thd_air);
 }
 
+// ---- one call spread over a wave (GetAirPropagationPar, MinimizeforLaunchAngle) ------------
+// The reference's layer loop (.cc:529-659 / MultiRay .cc:661-804) derives L in its first layer
+// and reuses it below (.cc:757-771), so once L is known the layers are independent: every lane
+// derives L (the cheap Snell part of the first layer), then lane j evaluates layer
+// il = top - j -- the same functions on the same arguments as the loop, all layers at once.
+// W = 4: RayTracingFunctions {THD, Recv deg, L, t}; W = 5: MultiRay, + geometric path.
+// Lane `ice_lane` (>= 0) evaluates the in-ice segment with the same path functions instead
+// (GetIcePropagationPar's THD, .cc:661-681 / :807-869), for MinimizeforLaunchAngle.
+struct LayerLane {
+  int nf;     // layers filled
+  double L0;  // Lvalue[0]
+  double o[5];
+};
+
+template <int W>
+__device__ LayerLane air_prop_lane(const DevMedium& M, double LaunchAngleAir, double AirTxHeight,
+                                   double IceLayerHeight, int j, bool full, int ice_lane,
+                                   double AntennaDepth) {
+  LayerLane R;
+  const int SkipLayersAbove = rtf_skip_above(M, AirTxHeight);
+  const int SkipLayersBelow = rtf_skip_below(M, IceLayerHeight);
+  const int top = M.ml - SkipLayersAbove - 1;
+  R.nf = top >= SkipLayersBelow ? top - SkipLayersBelow + 1 : 0;
+  // the first layer's Snell step (every lane): L
+  const int t0 = top < 0 ? 0 : (top > 4 ? 4 : top);
+  const double StopH0 = (top == (SkipLayersBelow - 1) + 1) ? IceLayerHeight : sel5(M.atm, t0);
+  const double Start_nh0 = rtf_nz_air(M, AirTxHeight);
+  double Recv0, L;
+  rtf_hit_L(M, Start_nh0, StopH0, AirTxHeight, 180 - LaunchAngleAir, 1, Recv0, L);
+  R.L0 = L;
+  // this lane's layer
+  const int il = top - j;
+  const int ic = il < 0 ? 0 : (il > 3 ? 3 : il);
+  const double StartH = (j == 0) ? AirTxHeight : sel5(M.atm, ic + 1) - 0.00001;
+  const double StopH = (il == (SkipLayersBelow - 1) + 1) ? IceLayerHeight : sel5(M.atm, ic);
+  const bool ice = j == ice_lane;
+  const double A = ice ? M.A_ice : M.A_air;
+  const double Rx = ice ? AntennaDepth : StopH, Tx = ice ? 0.0 : StartH;
+  const int air = ice ? 0 : 1;
+  R.o[0] = rtf_optical_path(M, A, Rx, Tx, L, air);
+  if (full) {
+    const double nzStopHeight = rtf_nz_air(M, StopH);
+    R.o[1] = (j == 0) ? Recv0 * M.r2d : asin(L / nzStopHeight) * M.r2d;
+    R.o[2] = L;
+    R.o[3] = rtf_prop_time(M, A, Rx, Tx, L, air);
+    if (W == 5) R.o[4] = mr_geo_path(M, A, Rx, Tx, L, air);
+  }
+  return R;
+}
+
+// GetAirPropagationPar on a wave: lane j < MaxLayers writes its layer's W slots (zeros past the
+// filled layers, as the one-lane form leaves them), lane 0 the count.
+template <int W>
+__device__ void air_prop_wave(const DevMedium& M, double LaunchAngleAir, double AirTxHeight,
+                              double IceLayerHeight, double* __restrict__ out) {
+  const int lane = (int)(threadIdx.x & 63);
+  const LayerLane R = air_prop_lane<W>(M, LaunchAngleAir, AirTxHeight, IceLayerHeight, lane, true,
+                                       -1, 0.0);
+  if (lane < M.ml)
+    for (int k = 0; k < W; k++) out[W * lane + k] = lane < R.nf ? R.o[k] : 0.0;
+  if (lane == 0) {
+    if (W == 5) out[W * M.ml] = 0.0;
+    out[W * M.ml + (W == 5 ? 1 : 0)] = R.nf;
+  }
+}
+
+// MinimizeforLaunchAngle on a wave: the air layers on lanes 0-3, the in-ice THD on lane 4, the
+// sums in the one-lane form's order.  rtf_min_launch: thd_ice = ice[0]; mr_min_launch:
+// thd_ice += ice[0] (from 0).
+template <int W>
+__device__ double min_launch_wave(const DevMedium& M, double x, double AirTxHeight,
+                                  double IceLayerHeight, double AntennaDepth, double D) {
+  const int lane = (int)(threadIdx.x & 63);
+  const LayerLane R = air_prop_lane<W>(M, x, AirTxHeight, IceLayerHeight, lane, false, 4,
+                                       AntennaDepth);
+  double thd_air = 0;
+  for (int i = 0; i < kMaxLayers; i++) {
+    const double a = __shfl(R.o[0], i);
+    if (i < R.nf) thd_air += a;
+  }
+  const double ice0 = __shfl(R.o[0], 4);
+  double thd_ice = 0;
+  if (AntennaDepth != 0 && R.nf > 0) {
+    if (W == 5)
+      thd_ice += ice0;
+    else
+      thd_ice = ice0;
+  } else if (AntennaDepth != 0) {
+    // no air layer: L is the reference's unset slot (UB), modelled as NaN (the one-lane form)
+    double ice[4];
+    rtf_ice_prop(M, AntennaDepth, __builtin_nan(""), ice);
+    if (W == 5)
+      thd_ice += ice[0];
+    else
+      thd_ice = ice[0];
+  }
+  return D - (thd_ice + thd_air);
+}
+
 struct RtfCall {
   int op, n_out;
   double a[8];
 };
 
 __global__ void rtf_kernel(DevMedium M, RtfCall c, double* __restrict__ out, Signal sig) {
+  // the layer-loop ops run on the whole wave (air_prop_wave, min_launch_wave); the rest on lane 0
+  if (c.op == AIRICE_RTF_AIR_PROPAGATION || c.op == AIRICE_MR_AIR_PROPAGATION) {
+    if (c.op == AIRICE_RTF_AIR_PROPAGATION)
+      air_prop_wave<4>(M, c.a[0], c.a[1], c.a[2], out);
+    else
+      air_prop_wave<5>(M, c.a[0], c.a[1], c.a[2], out);
+    __syncthreads();  // every lane's slots are written before lane 0 signals
+    if (threadIdx.x == 0) signal_done(sig);
+    return;
+  }
+  if (c.op == AIRICE_RTF_MIN_LAUNCH || c.op == AIRICE_MR_MIN_LAUNCH) {
+    const double f = c.op == AIRICE_RTF_MIN_LAUNCH
+                         ? min_launch_wave<4>(M, c.a[0], c.a[1], c.a[2], c.a[3], c.a[4])
+                         : min_launch_wave<5>(M, c.a[0], c.a[1], c.a[2], c.a[3], c.a[4]);
+    if (threadIdx.x == 0) {
+      out[0] = f;
+      signal_done(sig);
+    }
+    return;
+  }
   if (threadIdx.x != 0 || blockIdx.x != 0) return;
   double r[AIRICE_RTF_AIR2ICE_FIELDS > 5 * kMaxLayers + 2 ? AIRICE_RTF_AIR2ICE_FIELDS
                                                          : 5 * kMaxLayers + 2];

@@ -35,6 +35,11 @@
 #ifndef AIRICE_LEAN_DEG
 #define AIRICE_LEAN_DEG 5
 #endif
+// tlog_lean's table address as one shift and one mask of the high word (the byte offset of
+// entry i) instead of the entry index scaled afterwards
+#ifndef AIRICE_TLOG_IDX2
+#define AIRICE_TLOG_IDX2 1
+#endif
 
 namespace airice {
 
@@ -111,10 +116,16 @@ __host__ __device__ AIRICE_INLINE double tlog_lean(double x, const double* tab =
   const uint64_t ix = dbits(x);
   const uint32_t hx = (uint32_t)(ix >> 32);
   const uint32_t htmp = hx - 0x3fe60000u;
-  const int i = (int)((htmp >> (20 - kLogTableBits)) & ((1u << kLogTableBits) - 1));
   const int k = (int32_t)htmp >> 20;
   const double z = bitsd(((uint64_t)(hx - (htmp & 0xfff00000u)) << 32) | (ix & 0xffffffffULL));
+#if AIRICE_TLOG_IDX2
+  const uint32_t off = (htmp >> (20 - kLogTableBits - 4)) & (((1u << kLogTableBits) - 1) << 4);
+  const double* ent = reinterpret_cast<const double*>(reinterpret_cast<const char*>(tab) + off);
+  const double invc = ent[0], logc = ent[1];
+#else
+  const int i = (int)((htmp >> (20 - kLogTableBits)) & ((1u << kLogTableBits) - 1));
   const double invc = tab[2 * i], logc = tab[2 * i + 1];
+#endif
   const double r = AIRICE_FMA(z, invc, -1.0);
   const double w = AIRICE_FMA((double)k, Ln2, logc);
   const double r2 = r * r;

@@ -83,3 +83,34 @@ def test_one_query_hdtip_and_trace_match_the_batch():
                                    rows1[i:i + 1])
     torch.cuda.synchronize()
     assert _same(rows.cpu().numpy(), rows1.cpu().numpy())
+
+
+def test_one_ray_matches_the_batch():
+    """GetRayTracingSolutions for one ray (scalar_ray_kernel: the segments on lanes 0-4 of one
+    wave) against the batch rays_kernel, bit for bit, over launch angles 90..180 deg, Tx heights
+    across every layer (on a layer bound, just above the ice, above the atmosphere), Rx in the ice
+    and in the air, and the NaN rays (grazing launches)."""
+    import torch
+    from airiceraytracing_amd import AirIceSolver
+    dev = torch.device("cuda:0")
+    s = AirIceSolver()
+    rng = np.random.default_rng(11)
+    la = np.concatenate([rng.uniform(90.0, 180.0, 150), [90.0, 90.1, 92.0, 179.99, 180.0, 135.0]])
+    h = np.concatenate([rng.uniform(3000.0, 100000.0, 150),
+                        [8363.53902, 23141.7538, 3000.0001, 150000.0, 3217.48275, 50000.0]])
+    for ice_m, depth_m in ((3000.0, -200.0), (3000.0, 100.0), (2000.0, -5.0)):
+        launch = torch.from_numpy(la).to(dev)
+        txh = torch.from_numpy(h).to(dev)
+        n = launch.numel()
+        out = torch.empty((18, n), dtype=torch.float64, device=dev)
+        s.rays_device(launch, txh, ice_m, depth_m, depth_m < 0, out)
+        one = torch.empty((18, n), dtype=torch.float64, device=dev)
+        o1 = torch.empty((18, 1), dtype=torch.float64, device=dev)
+        for i in range(n):
+            s.rays_device(launch[i:i + 1], txh[i:i + 1], ice_m, depth_m, depth_m < 0, o1)
+            one[:, i] = o1[:, 0]
+        torch.cuda.synchronize()
+        a, b = out.cpu().numpy(), one.cpu().numpy()
+        bad = np.flatnonzero(~np.all(a.view(np.int64) == b.view(np.int64), axis=0))
+        assert bad.size == 0, (ice_m, depth_m, bad[:10], a[:, bad[:2]], b[:, bad[:2]])
+        assert np.isnan(a[2]).any() and np.isfinite(a[2]).any()

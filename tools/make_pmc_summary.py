@@ -16,7 +16,7 @@ UNITS = [("table_kernel", "table_kernel", 858627),
          ("roots_kernel<0>", "roots_kernel", 1000000),
          ("roots_sorted_kernel<0>", "roots_sorted_kernel", 1000000),
          ("group_count_kernel<0>", "group_count_kernel", 1000000),
-         ("group_scatter_kernel", "group_scatter_kernel", 1000000),
+         ("group_scatter_kernel<0>", "group_scatter_kernel", 1000000),
          ("solve_out_kernel<0>", "solve_out_kernel", 1000000),
          ("lookup_kernel", "lookup_kernel", 1000000)]
 
