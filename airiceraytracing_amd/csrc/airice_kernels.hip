@@ -63,6 +63,14 @@ constexpr int kTableBlock = AIRICE_TABLE_BS;
 #ifndef AIRICE_GUARD_SKIP
 #define AIRICE_GUARD_SKIP 0
 #endif
+// the root finder evaluates f(lo) and f(hi) together, before its loop (solve_root)
+#ifndef AIRICE_PAIR_ENDS
+#define AIRICE_PAIR_ENDS 1
+#endif
+// ... and both guards of a lane in one pass
+#ifndef AIRICE_PAIR_GUARDS
+#define AIRICE_PAIR_GUARDS 0
+#endif
 #ifndef AIRICE_ROWCONST_ALIGN16
 #define AIRICE_ROWCONST_ALIGN16 0
 #endif
@@ -813,6 +821,71 @@ __device__ __forceinline__ double air_thd(const DevMedium& M, const Query& q, do
   return thd;
 }
 
+// delta_D at two ray parameters (two launch angles) on the same segment: the two chains in one
+// straight-line block, so each hides the other's latency; every value as delta_D forms it.
+__device__ __forceinline__ void delta_D2(const Slim& T, const Slim& R, const RayL& Ra,
+                                         const RayL& Rb, const double* tab, double& xa,
+                                         double& xb) {
+  const double syRa = fast_sqrt(R.y2 - Ra.LL), syTa = fast_sqrt(T.y2 - Ra.LL);
+  const double syRb = fast_sqrt(R.y2 - Rb.LL), syTb = fast_sqrt(T.y2 - Rb.LL);
+  double da, db;
+  log_ratio2(R.Ay - Ra.LL + Ra.sAL * syRa, T.Ay - Ra.LL + Ra.sAL * syTa,
+             R.Ay - Rb.LL + Rb.sAL * syRb, T.Ay - Rb.LL + Rb.sAL * syTb, tab, da, db);
+  xa = (Ra.L * R.invC) * Ra.rsAL * ((R.Cx - T.Cx) - da);
+  xb = (Rb.L * R.invC) * Rb.rsAL * ((R.Cx - T.Cx) - db);
+}
+
+// MinimizeforLaunchAngle's THD in air and in the ice at two angles (the root finder's bracket
+// ends f(lo), f(hi)), as air_thd + the ice term of solve_root's evaluation site computes each:
+// the same operations in the same order per angle, the two angles' chains interleaved.
+__device__ __forceinline__ void eval_thd2(const DevMedium& M, const IceConsts& I, const Query& q,
+                                          double ta, double tb, const double* tab,
+                                          double& air_a, double& ice_a, double& air_b,
+                                          double& ice_b) {
+  double La = __builtin_nan(""), Lb = __builtin_nan("");
+  air_a = 0.0;
+  air_b = 0.0;
+  if (q.top >= q.bot) {
+    const double v1a = sin_start((180 - ta) * M.d2r);
+    const double v1b = sin_start((180 - tb) * M.d2r);
+    La = q.n_rtop * sin_asin(q.ratio * sin_asin(v1a));
+    Lb = q.n_rtop * sin_asin(q.ratio * sin_asin(v1b));
+    const RayL Ra = ray_L(M.A_air * M.A_air, La), Rb = ray_L(M.A_air * M.A_air, Lb);
+    double xa, xb;
+    delta_D2(q.tx, q.rtop, Ra, Rb, tab, xa, xb);
+    xa *= -1;
+    xb *= -1;
+    air_a += xa;
+    air_b += xb;
+#pragma unroll
+    for (int il = kMaxLayers - 2; il >= 1; --il) {
+      if (il < q.top && il > q.bot) {
+        delta_D2(slim(M.start[il]), slim(M.stop[il]), Ra, Rb, tab, xa, xb);
+        xa *= -1;
+        xb *= -1;
+        air_a += xa;
+        air_b += xb;
+      }
+    }
+    if (q.top > q.bot) {
+      delta_D2(start_slim(M, q.bot), q.iceair, Ra, Rb, tab, xa, xb);
+      xa *= -1;
+      xb *= -1;
+      air_a += xa;
+      air_b += xb;
+    }
+  }
+  ice_a = 0;
+  ice_b = 0;
+  if (q.depth_pos != 0) {
+    const RayL Ra = ray_L(M.A_ice * M.A_ice, La), Rb = ray_L(M.A_ice * M.A_ice, Lb);
+    double xa, xb;
+    delta_D2(slim(I.ice0), q.rx, Ra, Rb, tab, xa, xb);
+    ice_a += xa;
+    ice_b += xb;
+  }
+}
+
 // Two evaluations of f spread over a wave, for one-query calls (scalar_solve_kernel): lanes 0-4
 // take the Tx layer, layers 2 and 1 (when strictly between), the ice layer and the segment in the
 // ice at theta_a, lanes 32-36 the same at theta_b, each with the same delta_D as air_thd, and the
@@ -1015,6 +1088,9 @@ __device__ __forceinline__ SolveResult solve_root(const DevMedium& M, const IceC
   // bits, two sequential evaluations fewer)
   bool have_next = false;
   double next_air = 0.0, next_ice = 0.0;
+#if AIRICE_PAIR_GUARDS
+  double f_g2 = 0.0;  // f at the second guard, from the first guard's trip
+#endif
   auto guard = [&](double x, double f) {
     if (!(fabs(f) >= tau) || !(x > gL && x < gR)) return;
     if ((f < 0.0) == (fL < 0.0)) {
@@ -1040,6 +1116,58 @@ __device__ __forceinline__ SolveResult solve_root(const DevMedium& M, const IceC
     if (cont && iter == 40) status |= AIRICE_SOLVE_MAXITER;
     if (frozen || !cont || iter == 40) phase = PH_DONE;
   };
+  // gsl_root_fsolver_set's second end, f(hi) (fL holds f(lo)): the bracket state, the guards and
+  // the secant search's first guess
+  auto on_fhi = [&](double f) {
+    phase = PH_BISECT;
+    if (!isfinite(f)) {
+      status |= AIRICE_SOLVE_NONFINITE_END;
+    } else {
+      f_lower = fL;
+      f_upper = f;
+      if (!exact) {
+        gL = lo;
+        gR = hi;
+        fR = f;
+        okL = fabs(fL) >= tau;
+        okR = fabs(fR) >= tau;
+        if (okL && okR) {
+          if ((fL < 0.0) == (fR < 0.0)) {
+            gL = hi;  // no sign change: every midpoint has the ends' sign
+          } else {
+            const float ul = __tanf((float)((180 - lo) * M.d2r));
+            const float uh = __tanf((float)((180 - hi) * M.d2r));
+            const float un = uh - (float)fR * ((uh - ul) / (float)(fR - fL));
+            x1 = hi;
+            f1 = fR;
+            x2 = 180 - (double)atanf(un) * M.r2d;  // first guess, evaluated first
+            phase = PH_EST;
+          }
+        }
+      }
+    }
+  };
+#if AIRICE_PAIR_ENDS
+  if constexpr (!WAVE) {
+    // f(lo) and f(hi) in one pass (eval_thd2: two independent chains per lane, ~1.3x the time of
+    // one evaluation instead of 2x) before the loop, so that the loop carries no extra state; the
+    // probing lanes reach PH_FLO inside the loop and evaluate the ends there
+    if (phase == PH_FLO) {
+      double air_a, ice_a, air_b, ice_b;
+      eval_thd2(M, I, q, lo, hi, tab, air_a, ice_a, air_b, ice_b);
+      const double fa = (q.dist - (ice_a + air_a));
+      ++n_eval;
+      if (!isfinite(fa)) {
+        status |= AIRICE_SOLVE_NONFINITE_END;
+        phase = PH_BISECT;
+      } else {
+        fL = fa;
+        ++n_eval;
+        on_fhi(q.dist - (ice_b + air_b));
+      }
+    }
+  }
+#endif
 #if AIRICE_SCALAR_STAMP
   const int t_setup = (int)(__builtin_amdgcn_s_memtime() - ts0) + (int)(0.0 * (lo + hi));
 #endif
@@ -1172,12 +1300,23 @@ __device__ __forceinline__ SolveResult solve_root(const DevMedium& M, const IceC
         have_next = pair;
       }
     } else {
-      double L;
-      thd_air = air_thd(M, q, x, L, tab);
-      thd_ice = 0;
-      if (q.depth_pos != 0) {
-        const RayL RL = ray_L(M.A_ice * M.A_ice, L);
-        thd_ice += delta_D(slim(I.ice0), q.rx, RL, tab);
+#if AIRICE_PAIR_GUARDS
+      // a wave with lanes at their first guard evaluates both guards of those lanes in one
+      // interleaved pass (the second, x2 + dlt, is consumed in this trip's update)
+      if (__ballot(phase == PH_G1) != 0) {
+        double air_b, ice_b;
+        eval_thd2(M, I, q, x, phase == PH_G1 ? x2 + dlt : x, tab, thd_air, thd_ice, air_b, ice_b);
+        f_g2 = (q.dist - (ice_b + air_b));
+      } else
+#endif
+      {
+        double L;
+        thd_air = air_thd(M, q, x, L, tab);
+        thd_ice = 0;
+        if (q.depth_pos != 0) {
+          const RayL RL = ray_L(M.A_ice * M.A_ice, L);
+          thd_ice += delta_D(slim(I.ice0), q.rx, RL, tab);
+        }
       }
     }
     const double f = (q.dist - (thd_ice + thd_air));
@@ -1204,33 +1343,7 @@ __device__ __forceinline__ SolveResult solve_root(const DevMedium& M, const IceC
         phase = PH_FHI;
       }
     } else if (phase == PH_FHI) {
-      phase = PH_BISECT;
-      if (!isfinite(f)) {
-        status |= AIRICE_SOLVE_NONFINITE_END;
-      } else {
-        f_lower = fL;
-        f_upper = f;
-        if (!exact) {
-          gL = lo;
-          gR = hi;
-          fR = f;
-          okL = fabs(fL) >= tau;
-          okR = fabs(fR) >= tau;
-          if (okL && okR) {
-            if ((fL < 0.0) == (fR < 0.0)) {
-              gL = hi;  // no sign change: every midpoint has the ends' sign
-            } else {
-              const float ul = __tanf((float)((180 - lo) * M.d2r));
-              const float uh = __tanf((float)((180 - hi) * M.d2r));
-              const float un = uh - (float)fR * ((uh - ul) / (float)(fR - fL));
-              x1 = hi;
-              f1 = fR;
-              x2 = 180 - (double)atanf(un) * M.r2d;  // first guess, evaluated first
-              phase = PH_EST;
-            }
-          }
-        }
-      }
+      on_fhi(f);
     } else if (phase == PH_EST) {
       if (est > 0) {
         x1 = x2;
@@ -1261,6 +1374,13 @@ __device__ __forceinline__ SolveResult solve_root(const DevMedium& M, const IceC
       if (isfinite(f)) guard(x, f);
       phase = (phase == PH_G1 && !(AIRICE_GUARD_SKIP && gR - x2 <= 0.25e-9 * gL)) ? PH_G2
                                                                                : PH_BISECT;
+#if AIRICE_PAIR_GUARDS
+      if (!WAVE && phase == PH_G2) {  // the second guard, evaluated with the first
+        ++n_eval;
+        if (isfinite(f_g2)) guard(x2 + dlt, f_g2);
+        phase = PH_BISECT;
+      }
+#endif
     } else {  // PH_BISECT: gsl_root_fsolver_iterate at a midpoint between the guards
       if (!exact && isfinite(f)) guard(x, f);
       ++iter;

@@ -58,6 +58,8 @@ struct AtmFile {
   struct timespec mtime = {0, 0};
   std::string text;
   airice_medium parsed;
+  double atmlay[5];  // readATMpar of the text (ATMLAY, abc), kept with it
+  double abc[5][3];
   bool valid = false;
   unsigned long long gen = 0;  // parse number
 };
@@ -94,6 +96,7 @@ const AtmFile& atmosphere_file(const std::string& name) {
     if (airice_atmosphere_parse(f.text.data(), f.text.size(), AIRICE_VARIANT_PYWRAPPER,
                                 &f.parsed) != AIRICE_OK)
       die("MakeAtmosphere");
+    airice_compat::read_atm_par(f.text, f.atmlay, f.abc);
     f.valid = true;
     f.gen = g_atm.gen + 1;
     g_atm = std::move(f);
@@ -212,7 +215,10 @@ std::vector<double> flatten(const std::vector<std::vector<double>>& v) {  // .cc
 int MakeAtmosphere(std::string atmosFileName) {
   std::lock_guard<std::recursive_mutex> lock(g_mu);
   const AtmFile& f = atmosphere_file(atmosFileName);
-  airice_compat::read_atm_par(f.text, ATMLAY, abc);
+  // readATMpar's values for this file (parsed once per file version: TraceIceToAir calls this on
+  // every query, TraceIceToAir.C:25)
+  std::memcpy(ATMLAY, f.atmlay, sizeof(ATMLAY));
+  std::memcpy(abc, f.abc, sizeof(abc));
   // the profile vectors are re-read when the file changed or their shape differs; their values
   // feed only the spline, whose N0 comes from the same file
   static unsigned long long filled_gen = 0;
