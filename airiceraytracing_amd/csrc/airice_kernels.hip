@@ -1758,7 +1758,12 @@ __global__ __launch_bounds__(kRootsBlock, AIRICE_ROOTS_WAVES) void roots_kernel(
 // solved on its own and written by its index: results are identical either way.
 // ---------------------------------------------------------------------------
 constexpr int kGroupAngles = AIRICE_GROUP_BUCKETS;   // straight-line-angle classes
-constexpr int kGroupHeights = AIRICE_GROUP_HBINS;     // Tx-height classes within each
+// AIRICE_GROUP_BY_SPAN: the classes within each angle class are the number of air layers the path
+// spans (0-3+): a wave then runs only the middle-layer segments its own queries have
+#ifndef AIRICE_GROUP_BY_SPAN
+#define AIRICE_GROUP_BY_SPAN 1
+#endif
+constexpr int kGroupHeights = AIRICE_GROUP_BY_SPAN ? 4 : AIRICE_GROUP_HBINS;  // classes within each
 constexpr int kGroupBuckets = kGroupAngles * kGroupHeights;
 constexpr int kGroupItems = AIRICE_GROUP_ITEMS;  // queries per thread in the sort passes
 constexpr int kGroupThreads = AIRICE_GROUP_THREADS;  // threads per block of the sort passes
@@ -1788,7 +1793,10 @@ __device__ __forceinline__ int query_bucket(const DevMedium& M, const QueryArgs&
 #pragma unroll
     for (int j = 0; j < kGroupAngles - 1; ++j) b += (g.D <= K.t[j] * den) ? 1 : 0;
   }
-  if (kGroupHeights > 1) {  // Tx height between the ice and the top of the atmosphere
+  if (AIRICE_GROUP_BY_SPAN) {
+    const int span = top_layer(M, g.H) - bottom_layer(M, g.ice);
+    b = b * kGroupHeights + (span < 0 ? 0 : (span > 3 ? 3 : span));
+  } else if (kGroupHeights > 1) {  // Tx height between the ice and the top of the atmosphere
     const double h = (g.H - g.ice) / (M.atm[kMaxLayers] - g.ice) * kGroupHeights;
     b = b * kGroupHeights + ((h > 0) ? ((h < kGroupHeights) ? (int)h : kGroupHeights - 1) : 0);
   }

@@ -16,6 +16,11 @@
 #include "airice.h"
 #include "airice_internal.h"
 
+// GetAirPropagationPar / MinimizeforLaunchAngle on a wave: each layer's two ends on two lanes
+#ifndef AIRICE_RTF_SIDES
+#define AIRICE_RTF_SIDES 1
+#endif
+
 namespace airice {
 
 namespace {
@@ -544,6 +549,37 @@ __device__ LayerLane air_prop_lane(const DevMedium& M, double LaunchAngleAir, do
   const double A = ice ? M.A_ice : M.A_air;
   const double Rx = ice ? AntennaDepth : StopH, Tx = ice ? 0.0 : StartH;
   const int air = ice ? 0 : 1;
+#if AIRICE_RTF_SIDES
+  // the layer's two ends on two lanes (lane j: Rx, lane j + 8: Tx; the partner's values come back
+  // by shuffle): each antiderivative of GetRayOpticalPath / GetRayPropagationTime /
+  // GetRayGeometricPath once per lane, differenced in the reference's order (+Rx - Tx, sign flip
+  // in air)
+  const bool tx_side = (threadIdx.x & 8) != 0;
+  const double h = tx_side ? Tx : Rx;
+  const double fD = rtf_fDnfR(h, A, rtf_B(M, h, air), -rtf_C(M, h, air), L);
+  const double fD_tx = __shfl_down(fD, 8);
+  double x1 = +fD - fD_tx;
+  if (air) x1 *= -1;
+  R.o[0] = x1;
+  if (full) {
+    const double nzStopHeight = rtf_nz_air(M, StopH);
+    R.o[1] = (j == 0) ? Recv0 * M.r2d : asin(L / nzStopHeight) * M.r2d;
+    R.o[2] = L;
+    const double ft = rtf_ftimeD(M, h, A, -rtf_C(M, h, air), kSpeedC, L, air);
+    double fp = 0.0;
+    if (W == 5) fp = mr_fpathD(h, A, rtf_B(M, h, air), -rtf_C(M, h, air), L);
+    const double ft_tx = __shfl_down(ft, 8);
+    double t = +ft - ft_tx;
+    if (air) t *= -1;
+    R.o[3] = t;
+    if (W == 5) {
+      const double fp_tx = __shfl_down(fp, 8);
+      double g = fp - fp_tx;
+      if (air) g *= -1;
+      R.o[4] = g;
+    }
+  }
+#else
   R.o[0] = rtf_optical_path(M, A, Rx, Tx, L, air);
   if (full) {
     const double nzStopHeight = rtf_nz_air(M, StopH);
@@ -552,6 +588,7 @@ __device__ LayerLane air_prop_lane(const DevMedium& M, double LaunchAngleAir, do
     R.o[3] = rtf_prop_time(M, A, Rx, Tx, L, air);
     if (W == 5) R.o[4] = mr_geo_path(M, A, Rx, Tx, L, air);
   }
+#endif
   return R;
 }
 
@@ -561,8 +598,8 @@ template <int W>
 __device__ void air_prop_wave(const DevMedium& M, double LaunchAngleAir, double AirTxHeight,
                               double IceLayerHeight, double* __restrict__ out) {
   const int lane = (int)(threadIdx.x & 63);
-  const LayerLane R = air_prop_lane<W>(M, LaunchAngleAir, AirTxHeight, IceLayerHeight, lane, true,
-                                       -1, 0.0);
+  const LayerLane R = air_prop_lane<W>(M, LaunchAngleAir, AirTxHeight, IceLayerHeight,
+                                       AIRICE_RTF_SIDES ? (lane & 7) : lane, true, -1, 0.0);
   if (lane < M.ml)
     for (int k = 0; k < W; k++) out[W * lane + k] = lane < R.nf ? R.o[k] : 0.0;
   if (lane == 0) {
@@ -578,8 +615,8 @@ template <int W>
 __device__ double min_launch_wave(const DevMedium& M, double x, double AirTxHeight,
                                   double IceLayerHeight, double AntennaDepth, double D) {
   const int lane = (int)(threadIdx.x & 63);
-  const LayerLane R = air_prop_lane<W>(M, x, AirTxHeight, IceLayerHeight, lane, false, 4,
-                                       AntennaDepth);
+  const LayerLane R = air_prop_lane<W>(M, x, AirTxHeight, IceLayerHeight,
+                                       AIRICE_RTF_SIDES ? (lane & 7) : lane, false, 4, AntennaDepth);
   double thd_air = 0;
   for (int i = 0; i < kMaxLayers; i++) {
     const double a = __shfl(R.o[0], i);
