@@ -67,6 +67,11 @@ constexpr int kTableBlock = AIRICE_TABLE_BS;
 #ifndef AIRICE_PAIR_ENDS
 #define AIRICE_PAIR_ENDS 1
 #endif
+// the secant search's later steps by inverse quadratic interpolation from its AIRICE_IQI-th step
+// (0: secant only; 1: from the second point on, with f(lo); 2: on three search points)
+#ifndef AIRICE_IQI
+#define AIRICE_IQI 1
+#endif
 // ... and both guards of a lane in one pass
 #ifndef AIRICE_PAIR_GUARDS
 #define AIRICE_PAIR_GUARDS 0
@@ -1014,7 +1019,9 @@ __device__ __forceinline__ SolveResult solve_root(const DevMedium& M, const IceC
   {
     const double e = exp(M.negC_ice * g.depth_pos);
     const double y = M.A_ice + M.B_ice * e;
-    q.rx = Slim{y * y, M.A_ice * y, M.negC_ice * g.depth_pos, 1.0 / M.negC_ice};
+    // 1/C of the ice from the host-folded surface endpoint (the same IEEE quotient): a kernel
+    // argument, so it occupies no VGPRs across the loop
+    q.rx = Slim{y * y, M.A_ice * y, M.negC_ice * g.depth_pos, I.ice0.invC};
   }
 
   double lo = thR - 16;
@@ -1079,6 +1086,11 @@ __device__ __forceinline__ SolveResult solve_root(const DevMedium& M, const IceC
   // linear (a straight ray's is exactly H u; single precision is plenty for a first guess), then
   // secant steps in theta on the last two points (x1, f1), (x2, f2)
   double x1 = 0.0, f1 = 0.0, x2 = 0.0, f2 = 0.0;
+#if AIRICE_IQI
+  // the point before (x1, f1): the search steps by inverse quadratic interpolation on the last
+  // three points (the secant step plus a curvature term) once it has three
+  double x0 = 0.0, f0 = 0.0;
+#endif
   // PH_G1/G2: guards at x2 -/+ dlt, where x2 is the secant search's last point (it stays put after
   // the search) and dlt lives in x1 (dead once the search ends)
   double& dlt = x1;
@@ -1140,6 +1152,10 @@ __device__ __forceinline__ SolveResult solve_root(const DevMedium& M, const IceC
             const float un = uh - (float)fR * ((uh - ul) / (float)(fR - fL));
             x1 = hi;
             f1 = fR;
+#if AIRICE_IQI
+            x0 = lo;
+            f0 = fL;
+#endif
             x2 = 180 - (double)atanf(un) * M.r2d;  // first guess, evaluated first
             phase = PH_EST;
           }
@@ -1256,6 +1272,16 @@ __device__ __forceinline__ SolveResult solve_root(const DevMedium& M, const IceC
       // the secant point only steers the search (the root comes from GSL's bisection replay), so
       // its quotient takes v_rcp_f64 (~2^-24 relative) instead of the IEEE division
       x = (est == 0) ? x2 : x2 - f2 * ((x2 - x1) * __builtin_amdgcn_rcp(f2 - f1));
+#if AIRICE_IQI
+      // theta(f) through (x0, f0), (x1, f1), (x2, f2) in Newton form, at f = 0: the secant step
+      // minus f1 f2 times the second divided difference (the search only steers; a point outside
+      // the guards falls back to their midpoint below)
+      if (est >= AIRICE_IQI) {
+        const double d1 = (x2 - x1) * __builtin_amdgcn_rcp(f2 - f1);
+        const double d0 = (x1 - x0) * __builtin_amdgcn_rcp(f1 - f0);
+        x += f1 * f2 * ((d1 - d0) * __builtin_amdgcn_rcp(f2 - f0));
+      }
+#endif
 #if AIRICE_OVERSHOOT
       // near convergence (the step is under a quarter of GSL's final bracket width W and x2 is
       // a guard), aim W/8 past the predicted root: the new point and x2 then straddle the root
@@ -1346,6 +1372,10 @@ __device__ __forceinline__ SolveResult solve_root(const DevMedium& M, const IceC
       on_fhi(f);
     } else if (phase == PH_EST) {
       if (est > 0) {
+#if AIRICE_IQI
+        x0 = x1;
+        f0 = f1;
+#endif
         x1 = x2;
         f1 = f2;
       }
