@@ -72,6 +72,10 @@ constexpr int kTableBlock = AIRICE_TABLE_BS;
 #ifndef AIRICE_IQI
 #define AIRICE_IQI 1
 #endif
+// one phase of the root finder's state machine per loop trip (solve_root, the per-lane form)
+#ifndef AIRICE_UNIFORM_PHASE
+#define AIRICE_UNIFORM_PHASE 0
+#endif
 // ... and both guards of a lane in one pass
 #ifndef AIRICE_PAIR_GUARDS
 #define AIRICE_PAIR_GUARDS 0
@@ -1199,6 +1203,23 @@ __device__ __forceinline__ SolveResult solve_root(const DevMedium& M, const IceC
       est = __builtin_amdgcn_readfirstlane(est);
       iter = __builtin_amdgcn_readfirstlane(iter);
     }
+#if AIRICE_UNIFORM_PHASE
+    if constexpr (!WAVE) {
+      // one phase per trip: the wave's lowest phase (a lane's phase never decreases), the lanes in
+      // other phases idle under EXEC, so each trip runs one phase body instead of every body some
+      // lane is in.  A lane's own sequence of points and updates is unchanged.  Probing lanes
+      // (up to ~300 steps) always take part, so that the others do not wait for them.
+      int ph = PH_BISECT;
+#pragma unroll
+      for (int p = PH_FLO; p < PH_BISECT; ++p) {
+        if (__ballot(phase == p) != 0) {
+          ph = p;
+          break;
+        }
+      }
+      if (phase != ph && phase != PH_PROBE) continue;
+    }
+#endif
     if (phase == PH_BISECT) {
       // steps that need no evaluation: an exact zero at a bracket end (GSL returns that end),
       // or a midpoint inside a guard region, whose sign is the region's: lo (left) or hi

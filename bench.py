@@ -737,19 +737,26 @@ def table_cfg4(args, solver, world, rank, dev, stream, distributed, coll_dev, pm
     host_tab = None
     if distributed:
         mode = "host" if want_host else "rccl"
-        path = [f"/dev/shm/airice_cfg4_{os.getpid()}_{int(time.time())}"]
-        dist.broadcast_object_list(path, src=0)
-        try:
-            r = run_sharded_table(g, compute, args.cfg4_reps, 1, device=dev, coll_device=coll_dev,
-                                  sync=torch.cuda.synchronize, gather_reps=1, assemble=mode,
-                                  host_path=path[0], host_copy=host_copy,
-                                  host_register=register, host_unregister=unregister)
-        except OSError as e:  # no room for the shared host table: assemble on the root's GPU
-            rep["host_assembly_error"] = str(e)
-            st["i"] = 0
-            mode = "rccl"
-            r = run_sharded_table(g, compute, args.cfg4_reps, 1, device=dev, coll_device=coll_dev,
-                                  sync=torch.cuda.synchronize, gather_reps=1, assemble="rccl")
+        # every rank takes the same assembly path: rank 0 checks that /dev/shm can hold the shared
+        # host table and broadcasts the decision with the file name (a rank failing alone inside
+        # the collective sequence would leave the others waiting)
+        plan = [f"/dev/shm/airice_cfg4_{os.getpid()}_{int(time.time())}", mode, None]
+        if rank == 0 and mode == "host":
+            try:
+                fs = os.statvfs("/dev/shm")
+                free = fs.f_bavail * fs.f_frsize
+                if free < 44 * n * 1.05:
+                    plan[1], plan[2] = "rccl", f"/dev/shm has {free / 1e9:.1f} GB free"
+            except OSError as e:
+                plan[1], plan[2] = "rccl", str(e)
+        dist.broadcast_object_list(plan, src=0)
+        mode = plan[1]
+        if plan[2] is not None:  # no room for the shared host table: assemble on the root's GPU
+            rep["host_assembly_error"] = plan[2]
+        r = run_sharded_table(g, compute, args.cfg4_reps, 1, device=dev, coll_device=coll_dev,
+                              sync=torch.cuda.synchronize, gather_reps=1, assemble=mode,
+                              host_path=plan[0], host_copy=host_copy,
+                              host_register=register, host_unregister=unregister)
         torch.cuda.synchronize()
         build_s = r["elapsed_s"] / args.cfg4_reps
         rep.update({"value": n / build_s, "ms_per_build": build_s * 1e3,
