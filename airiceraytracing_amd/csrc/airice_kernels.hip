@@ -57,6 +57,13 @@ constexpr int kTableBlock = AIRICE_TABLE_BS;
 #ifndef AIRICE_SCALAR_STAMP
 #define AIRICE_SCALAR_STAMP 0
 #endif
+#ifndef AIRICE_RAY_STAMP
+#define AIRICE_RAY_STAMP 0
+#endif
+// the one-wave kernels touch their argument block's lines at entry (prefetch_kernargs)
+#ifndef AIRICE_KARG_PREFETCH
+#define AIRICE_KARG_PREFETCH 1
+#endif
 #ifndef AIRICE_OVERSHOOT
 #define AIRICE_OVERSHOOT 0
 #endif
@@ -543,9 +550,13 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(AIRICE_TABLE
 // one segment.
 __device__ __forceinline__ void ray_solution_wave(const DevMedium& M, const IceConsts& I,
                                                   double theta, double H, bool in_ice, double* d,
-                                                  const double* tab) {
+                                                  const double* tab,
+                                                  unsigned long long* ts = nullptr) {
   const int lane = (int)(threadIdx.x & 63);
   const RowConst rc = row_const(M, I, H);
+#if AIRICE_RAY_STAMP
+  ts[1] = __builtin_amdgcn_s_memtime() + (unsigned long long)(0.0 * rc.seg.ratio);
+#endif
   const int top = rc.top, bot = I.bot;
   const bool any = rc.any != 0;
   const double A2 = M.A_air * M.A_air, A2i = M.A_ice * M.A_ice;
@@ -571,6 +582,9 @@ __device__ __forceinline__ void ray_solution_wave(const DevMedium& M, const IceC
   const double u_ice = sin_asin(I.n_ratio * vinc);
   sin_in[4] = u_ice;
   on[4] = in_ice;
+#if AIRICE_RAY_STAMP
+  ts[2] = __builtin_amdgcn_s_memtime() + (unsigned long long)(0.0 * u_ice);
+#endif
   // this lane's segment
   const int j = lane < 5 ? lane : 0;
   SegConst S = rc.seg;
@@ -602,6 +616,9 @@ __device__ __forceinline__ void ray_solution_wave(const DevMedium& M, const IceC
   double v_unused;
   const Segment sg = segment_const(S, air ? M.A_air : M.A_ice, air ? A2 : A2i, sj, air, v_unused,
                                    tab);
+#if AIRICE_RAY_STAMP
+  ts[3] = __builtin_amdgcn_s_memtime() + (unsigned long long)(0.0 * (sg.thd + sg.t + sg.geo));
+#endif
   // outputs that are functions of the chain's sines (every lane; lane 0 writes)
   const double inc = any ? k_asin(vinc) * M.r2d : 0.0;
   const double recv_ice = k_asin(sin_asin(I.iceseg.ratio * u_ice)) * M.r2d;
@@ -626,6 +643,11 @@ __device__ __forceinline__ void ray_solution_wave(const DevMedium& M, const IceC
       geo_ice += c;
     }
   }
+#if AIRICE_RAY_STAMP
+  ts[4] = __builtin_amdgcn_s_memtime() +
+          (unsigned long long)(0.0 * (thd_air + thd_ice + t_air + t_ice + geo_air + geo_ice + tS +
+                                      tP + inc + recv_ice));
+#endif
   if (lane != 0) return;
   d[0] = 0;
   d[1] = H;
@@ -653,13 +675,26 @@ __global__ __launch_bounds__(64) void scalar_ray_kernel(DevMedium M, IceConsts I
                                                         const double* __restrict__ txh, int in_ice,
                                                         double* __restrict__ out, size_t ld,
                                                         Signal sig) {
+#if AIRICE_KARG_PREFETCH
+  prefetch_kernargs<sizeof(DevMedium) + sizeof(IceConsts)>();
+#endif
+  unsigned long long ts[6] = {0, 0, 0, 0, 0, 0};
+#if AIRICE_RAY_STAMP
+  // debug: shader-clock stamps (entry, row constants, sine chain, segment, sums, stores) in
+  // out[18..23], deltas from entry
+  ts[0] = __builtin_amdgcn_s_memtime();
+#endif
   const bool inl = sig.n_in >= 2;  // the inputs in the kernel arguments
   double d[18];
   ray_solution_wave(M, I, inl ? sig.in[0] : launch[0], inl ? sig.in[1] : txh[0], in_ice != 0, d,
-                    &kLogTable[0][0]);
+                    &kLogTable[0][0], ts);
   if (threadIdx.x != 0) return;
 #pragma unroll
   for (int c = 0; c < 18; ++c) out[c * ld] = d[c];
+#if AIRICE_RAY_STAMP
+  ts[5] = __builtin_amdgcn_s_memtime();
+  for (int c = 1; c < 6; ++c) out[(17 + c) * ld] = (double)(ts[c] - ts[0]);
+#endif
   signal_done(sig);
 }
 
@@ -2202,6 +2237,9 @@ template <int IN, int OUT>
 __global__ __launch_bounds__(64) void scalar_solve_kernel(DevMedium M, IceConsts I, QueryArgs Q,
                                                           Park park, double* out, size_t ld,
                                                           uint8_t* flag, Signal sig) {
+#if AIRICE_KARG_PREFETCH
+  prefetch_kernargs<sizeof(DevMedium) + sizeof(IceConsts)>();
+#endif
 #if AIRICE_SCALAR_STAMP
   const unsigned long long c0 = __builtin_amdgcn_s_memtime(), w0 = __builtin_amdgcn_s_memrealtime();
 #endif

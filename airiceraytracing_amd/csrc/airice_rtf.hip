@@ -20,6 +20,9 @@
 #ifndef AIRICE_RTF_SIDES
 #define AIRICE_RTF_SIDES 1
 #endif
+#ifndef AIRICE_KARG_PREFETCH
+#define AIRICE_KARG_PREFETCH 1
+#endif
 
 namespace airice {
 
@@ -647,6 +650,9 @@ struct RtfCall {
 };
 
 __global__ void rtf_kernel(DevMedium M, RtfCall c, double* __restrict__ out, Signal sig) {
+#if AIRICE_KARG_PREFETCH
+  prefetch_kernargs<sizeof(DevMedium) + sizeof(RtfCall)>();
+#endif
   // the layer-loop ops run on the whole wave (air_prop_wave, min_launch_wave); the rest on lane 0
   if (c.op == AIRICE_RTF_AIR_PROPAGATION || c.op == AIRICE_MR_AIR_PROPAGATION) {
     if (c.op == AIRICE_RTF_AIR_PROPAGATION)
