@@ -64,6 +64,10 @@ constexpr int kTableBlock = AIRICE_TABLE_BS;
 #ifndef AIRICE_KARG_PREFETCH
 #define AIRICE_KARG_PREFETCH 1
 #endif
+// the table lookup's minimizer fallback as one fused pass (roots_kernel<IN_CM100, 256, true>)
+#ifndef AIRICE_FALLBACK_FUSED
+#define AIRICE_FALLBACK_FUSED 1
+#endif
 #ifndef AIRICE_OVERSHOOT
 #define AIRICE_OVERSHOOT 0
 #endif
@@ -1781,11 +1785,24 @@ constexpr int kRootsBlock = AIRICE_ROOTS_BS;
 #define AIRICE_SORTED_WAVES AIRICE_ROOTS_WAVES
 #endif
 
-template <int IN>
-__global__ __launch_bounds__(kRootsBlock, AIRICE_ROOTS_WAVES) void roots_kernel(DevMedium M,
-                                                                                IceConsts I,
-                                                                                QueryArgs Q,
-                                                                                Park park) {
+// Stage 2 of the lookup fallback with the root handed over in registers (roots_kernel<IN_CM100>,
+// fused): defined below.
+__device__ __forceinline__ void fallback_out_direct(const DevMedium& M, const IceConsts& I,
+                                                    const QueryArgs& Q, double* __restrict__ out,
+                                                    size_t ld, uint8_t* __restrict__ ok,
+                                                    long long k, const double* tab,
+                                                    const Geometry& g, double root, int status);
+
+// BS: threads per block (the lookup fallback pass uses 256: its few active lanes per block then
+// fill more, shorter-lived blocks, all resident at once).  FUSED (IN_CM100 only): the block also
+// runs the fallback's stage 2 for its lanes, with the root in registers (out / ld / ok).
+template <int IN, int BS = kRootsBlock, bool FUSED = false>
+__global__ __launch_bounds__(BS, AIRICE_ROOTS_WAVES) void roots_kernel(DevMedium M, IceConsts I,
+                                                                       QueryArgs Q, Park park,
+                                                                       double* __restrict__ out,
+                                                                       size_t ld,
+                                                                       uint8_t* __restrict__ ok) {
+  constexpr int kRootsBlock = BS;
   __shared__ int s_count[kSortBuckets + 1];
   __shared__ int s_slot[kRootsBlock];
   // the log table in LDS (one 16-byte entry per thread), as in table_kernel: every evaluation's
@@ -1826,6 +1843,10 @@ __global__ __launch_bounds__(kRootsBlock, AIRICE_ROOTS_WAVES) void roots_kernel(
   double thR;
   const Geometry g = load_query<IN>(M, Q, k, thR);
   const SolveResult r = solve_root(M, I, g, thR, park.exact != 0, &s_logtab[0][0]);
+  if constexpr (FUSED) {
+    fallback_out_direct(M, I, Q, out, ld, ok, k, &s_logtab[0][0], g, r.root, r.status);
+    return;
+  }
   park.root[k * park.stride] = r.root;
   park.status[k * park.stride] = (double)r.status;
   if (park.stats != nullptr) {
@@ -2142,7 +2163,9 @@ __global__ __launch_bounds__(kBlock) void hdtip_out_kernel(DevMedium M, IceConst
 // (geoIce, geoAir, optIce, optAir, ...), so the optical and geometric slots trade places;
 // `ok` arrives holding the lookup's checks and is completed with CheckSolBool and
 // launchAngle < 0, then the four zeroed slots of .cc:1451-1456.
-template <bool WAVE = false>
+// DIRECT (lane form): the query and its root arrive in wr (the fused fallback pass) instead of
+// being reloaded and read back from the parked slots.
+template <bool WAVE = false, bool DIRECT = false>
 __device__ __forceinline__ void lookup_fallback_out_body(const DevMedium& M, const IceConsts& I,
                                                          const QueryArgs& Q,
                                                          double* __restrict__ out, size_t ld,
@@ -2151,9 +2174,9 @@ __device__ __forceinline__ void lookup_fallback_out_body(const DevMedium& M, con
                                                          WaveRoot wr = WaveRoot{0.0, 0}) {
   if (!(Q.mask[k] & AIRICE_LOOKUP_FALLBACK)) return;
   double thR;
-  const Geometry g = WAVE ? wr.g : load_query<IN_CM100>(M, Q, k, thR);
-  const double x = WAVE ? wr.root : out[4 * ld + k];
-  const int st = WAVE ? wr.status : (int)out[0 * ld + k];
+  const Geometry g = (WAVE || DIRECT) ? wr.g : load_query<IN_CM100>(M, Q, k, thR);
+  const double x = (WAVE || DIRECT) ? wr.root : out[4 * ld + k];
+  const int st = (WAVE || DIRECT) ? wr.status : (int)out[0 * ld + k];
   const Solved S = WAVE ? evaluate_root_wave(M, I, g, x, st, tab) : evaluate_root(M, I, g, x, st, tab);
   if (WAVE && threadIdx.x != 0) return;
   const double thd = S.thd_ice + S.thd_air;
@@ -2171,6 +2194,14 @@ __device__ __forceinline__ void lookup_fallback_out_body(const DevMedium& M, con
   out[7 * ld + k] = tP;
   out[8 * ld + k] = S.ant * M.d2r;
   ok[k] = good ? 1 : 0;
+}
+
+__device__ __forceinline__ void fallback_out_direct(const DevMedium& M, const IceConsts& I,
+                                                    const QueryArgs& Q, double* __restrict__ out,
+                                                    size_t ld, uint8_t* __restrict__ ok,
+                                                    long long k, const double* tab,
+                                                    const Geometry& g, double root, int status) {
+  lookup_fallback_out_body<false, true>(M, I, Q, out, ld, ok, k, tab, WaveRoot{root, status, g});
 }
 
 __global__ __launch_bounds__(kBlock) void lookup_fallback_out_kernel(
@@ -2356,7 +2387,8 @@ static int launch_roots(const DevMedium& M, const IceConsts& I, const QueryArgs&
   if (IN == IN_CM100 || group_min == 0 || n < group_min || park.stats != nullptr ||
       n >= (1ull << 31)) {
     ktimer_begin(KT_ROOTS, st);
-    hipLaunchKernelGGL(roots_kernel<IN>, roots_grid(n), dim3(kRootsBlock), 0, st, M, I, Q, park);
+    hipLaunchKernelGGL((roots_kernel<IN>), roots_grid(n), dim3(kRootsBlock), 0, st, M, I, Q, park,
+                       nullptr, (size_t)0, nullptr);
     ktimer_end(KT_ROOTS, st);
     return launch_ok();
   }
@@ -2685,12 +2717,22 @@ int launch_lookup_fallback(const DevMedium& M, const IceConsts& I, const double*
                        I, Q, park, out, ld, ok, take_scalar_signal());
     return launch_ok();
   }
+#if AIRICE_FALLBACK_FUSED
+  // one pass: 256-lane blocks group their few fallback lanes into their first wave, solve them and
+  // write their outputs (stage 2 with the root in registers)
+  (void)grid;
+  (void)block;
+  hipLaunchKernelGGL((roots_kernel<IN_CM100, 256, true>), dim3((unsigned)((n + 255) / 256)),
+                     dim3(256), 0, st, M, I, Q, park, out, ld, ok);
+  return launch_ok();
+#else
   SortedPark sp;  // the fallback pass is never grouped (launch_roots): the parked slots
   void* ws;
   if (int rc = launch_roots<IN_CM100>(M, I, Q, park, n, st, sp, ws)) return rc;
   if (sp.rec != nullptr) return AIRICE_EINVAL;
   hipLaunchKernelGGL(lookup_fallback_out_kernel, grid, block, 0, st, M, I, Q, out, ld, ok);
   return launch_ok();
+#endif
 }
 
 int launch_trace(const DevMedium& M, const IceConsts& I, const double* depth, const double* ice,
