@@ -74,6 +74,15 @@ constexpr int kTableBlock = AIRICE_TABLE_BS;
 #ifndef AIRICE_GUARD_SKIP
 #define AIRICE_GUARD_SKIP 0
 #endif
+// the per-lane root finder's evaluation-free bisection steps as selects, four per loop trip (the
+// one-query form's code) instead of a loop with a divergent exit per step
+#ifndef AIRICE_LEAN_SELECTS
+#define AIRICE_LEAN_SELECTS 1
+#endif
+// steps per trip of those selects
+#ifndef AIRICE_LEAN_UNROLL
+#define AIRICE_LEAN_UNROLL 4
+#endif
 // the root finder evaluates f(lo) and f(hi) together, before its loop (solve_root)
 #ifndef AIRICE_PAIR_ENDS
 #define AIRICE_PAIR_ENDS 1
@@ -1280,13 +1289,13 @@ __device__ __forceinline__ SolveResult solve_root(const DevMedium& M, const IceC
         const double gl = okL ? gL : -1.0, gr = okR ? gR : __builtin_inf();
         const double lo0 = lo, hi0 = hi;
         bool done = false;
-        if constexpr (WAVE) {
+        if constexpr (WAVE || AIRICE_LEAN_SELECTS) {
           // one query per wave: the same steps as selects, four per trip, so that the chain is
           // midpoint -> compare -> select without a branch per step
           bool stop = false;
           while (!stop) {
 #pragma unroll
-            for (int u = 0; u < 4; ++u) {
+            for (int u = 0; u < AIRICE_LEAN_UNROLL; ++u) {
               const double xm = (lo + hi) / 2.0;
               const bool inL = xm <= gl, inR = !inL && xm >= gr;
               const bool mv = !stop && (inL || inR);  // otherwise: evaluate this midpoint
