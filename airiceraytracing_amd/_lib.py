@@ -115,6 +115,15 @@ class SingleRayInfo(ctypes.Structure):
                 ("n_air", ctypes.c_int64), ("n_ice", ctypes.c_int64)]
 
 
+class TableFileInfo(ctypes.Structure):
+    """airice_table_file_info (include/airice.h): the header of a table file."""
+
+    _fields_ = [("medium", Medium), ("grid", Grid), ("n_rays", ctypes.c_uint64),
+                ("checksum", ctypes.c_uint64)]
+
+
+TABLE_FILE_HEADER = 512  # AIRICE_TABLE_FILE_HEADER
+
 SINGLE_RAY_FIELDS = 6  # AIRICE_SINGLE_RAY_FIELDS
 SINGLE_RAY_WORK = 32   # AIRICE_SINGLE_RAY_WORK
 
@@ -137,7 +146,8 @@ EXPORTED_SYMBOLS = (
     "airice_rtf_eval_variant", "Py_TraceIceToAir", "airice_device_count", "airice_set_device", "airice_malloc",
     "airice_free", "airice_memcpy_h2d", "airice_memcpy_d2h", "airice_synchronize",
     "airice_kernel_timing", "airice_kernel_time", "airice_table_to_host",
-    "airice_host_register", "airice_host_unregister",
+    "airice_host_register", "airice_host_unregister", "airice_table_checksum",
+    "airice_table_save", "airice_table_file_read_info", "airice_table_load",
 )
 
 
@@ -202,6 +212,10 @@ def lib() -> ctypes.CDLL:
         "airice_table_to_host": ([P, S, S, P, S, P], I),
         "airice_host_register": ([P, S], I),
         "airice_host_unregister": ([P], I),
+        "airice_table_checksum": ([P, S, S], ctypes.c_uint64),
+        "airice_table_save": ([ctypes.c_char_p, M, G, P, S, S], I),
+        "airice_table_file_read_info": ([ctypes.c_char_p, ctypes.POINTER(TableFileInfo)], I),
+        "airice_table_load": ([ctypes.c_char_p, M, P, S, ctypes.POINTER(TableFileInfo)], I),
         "airice_trace_ice_to_air_launch": ([M, P, P, P, P, S, P, P], I),
         "airice_trace_ice_to_air_host": ([M, P, P, P, P, S, P], I),
         "Py_TraceIceToAir": ([D, D, D, D, ctypes.POINTER(D)], None),

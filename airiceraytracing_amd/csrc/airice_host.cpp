@@ -145,6 +145,112 @@ int parse_gdas(const std::string& text, airice_medium* m) {
   return AIRICE_OK;
 }
 
+// ---- table files (airice_table_save / _load) --------------------------------------------------
+// The header is serialised field by field at fixed offsets (little-endian host), so that struct
+// padding never reaches the file and the layout does not depend on the compiler.
+namespace {
+
+constexpr char kTableMagic[8] = {'A', 'I', 'R', 'T', 'B', 'L', '0', '1'};
+constexpr uint32_t kTableVersion = 1;
+
+struct HeaderIO {
+  unsigned char* buf;
+  size_t off;
+  bool store;
+  template <class T>
+  void f(T& v) {
+    if (store) std::memcpy(buf + off, &v, sizeof(T));
+    else std::memcpy(&v, buf + off, sizeof(T));
+    off += sizeof(T);
+  }
+  void skip(size_t n) { off += n; }
+};
+
+void medium_io(HeaderIO& io, airice_medium& m) {
+  for (double& v : m.atmlay_cm) io.f(v);
+  for (auto& row : m.abc)
+    for (double& v : row) io.f(v);
+  for (double& v : m.B_air) io.f(v);
+  for (double& v : m.C_air) io.f(v);
+  io.f(m.N0);
+  io.f(m.max_layers);
+  io.f(m.n_points);
+  io.f(m.A_air);
+  io.f(m.A_ice);
+  io.f(m.B_ice);
+  io.f(m.C_ice);
+  io.f(m.pi);
+  io.f(m.h_top);
+  io.f(m.constant_air_index);
+  io.skip(4);
+  io.f(m.A_const);
+}
+
+void grid_io(HeaderIO& io, airice_grid& g) {
+  io.f(g.start_height);
+  io.f(g.stop_height);
+  io.f(g.height_step);
+  io.f(g.height_steps);
+  io.skip(4);
+  io.f(g.start_angle);
+  io.f(g.stop_angle);
+  io.f(g.angle_step);
+  io.f(g.angle_steps);
+  io.skip(4);
+  io.f(g.depth_m);
+  io.f(g.ice_m);
+  io.f(g.in_ice);
+  io.f(g.table_rows);
+}
+
+// the parsed fields of two media, bit for bit (the variant's pi included)
+bool same_medium(const airice_medium& a, const airice_medium& b) {
+  unsigned char x[AIRICE_TABLE_FILE_HEADER] = {}, y[AIRICE_TABLE_FILE_HEADER] = {};
+  airice_medium ca = a, cb = b;
+  HeaderIO ia{x, 0, true}, ib{y, 0, true};
+  medium_io(ia, ca);
+  medium_io(ib, cb);
+  return std::memcmp(x, y, ia.off) == 0;
+}
+
+inline uint64_t rotl64(uint64_t v, int r) { return (v << r) | (v >> (64 - r)); }
+
+// four independent multiply-rotate lanes over 8-byte words (a non-cryptographic integrity check:
+// catches truncation, bit rot and a file mixed up with another table)
+uint64_t bytes_hash(const unsigned char* p, size_t n, uint64_t seed) {
+  constexpr uint64_t P1 = 0x9E3779B185EBCA87ull, P2 = 0xC2B2AE3D27D4EB4Full;
+  uint64_t h[4] = {seed ^ P1, seed ^ P2, seed + P1, seed - P2};
+  size_t i = 0;
+  for (; i + 32 <= n; i += 32) {
+    for (int k = 0; k < 4; ++k) {
+      uint64_t w;
+      std::memcpy(&w, p + i + 8 * k, 8);
+      h[k] = rotl64(h[k] + w * P2, 31) * P1;
+    }
+  }
+  unsigned char tail[32] = {};
+  std::memcpy(tail, p + i, n - i);
+  for (int k = 0; k < 4; ++k) {
+    uint64_t w;
+    std::memcpy(&w, tail + 8 * k, 8);
+    h[k] = rotl64(h[k] + w * P2, 31) * P1;
+  }
+  uint64_t r = rotl64(h[0], 1) + rotl64(h[1], 7) + rotl64(h[2], 12) + rotl64(h[3], 18) + n;
+  r ^= r >> 33;
+  r *= P2;
+  r ^= r >> 29;
+  return r;
+}
+
+struct FileCloser {
+  FILE* f;
+  ~FileCloser() {
+    if (f) std::fclose(f);
+  }
+};
+
+}  // namespace
+
 }  // namespace airice
 
 using namespace airice;
@@ -215,6 +321,142 @@ int airice_grid_init(airice_grid* g, double depth_cm, double ice_cm, double heig
   int32_t rows = g->height_steps;
   while (rows > 0 && !(g->start_height - g->height_step * (rows - 1) > 0)) --rows;
   g->table_rows = rows;
+  return AIRICE_OK;
+}
+
+uint64_t airice_table_checksum(const float* h_table, size_t ld, size_t n_rays) {
+  uint64_t r = 0x5DEECE66Dull ^ n_rays;
+  if (h_table == nullptr) return r;
+  for (int c = 0; c < AIRICE_TABLE_COLUMNS; ++c)
+    r = bytes_hash(reinterpret_cast<const unsigned char*>(h_table + (size_t)c * ld),
+                   n_rays * sizeof(float), r + (uint64_t)c);
+  return r;
+}
+
+int airice_table_save(const char* path, const airice_medium* m, const airice_grid* g,
+                      const float* h_table, size_t ld, size_t n_rays) {
+  if (path == nullptr || m == nullptr || g == nullptr || (h_table == nullptr && n_rays > 0) ||
+      ld < n_rays) {
+    set_error("table_save: null argument or column stride < n_rays");
+    return AIRICE_EINVAL;
+  }
+  unsigned char hdr[AIRICE_TABLE_FILE_HEADER] = {};
+  std::memcpy(hdr, kTableMagic, 8);
+  uint32_t version = kTableVersion, hbytes = AIRICE_TABLE_FILE_HEADER,
+           cols = AIRICE_TABLE_COLUMNS;
+  uint64_t n = n_rays, sum = airice_table_checksum(h_table, ld, n_rays);
+  HeaderIO io{hdr, 8, true};
+  io.f(version);
+  io.f(hbytes);
+  io.f(cols);
+  io.skip(12);
+  io.f(n);
+  io.f(sum);
+  airice_medium mc = *m;
+  airice_grid gc = *g;
+  medium_io(io, mc);
+  grid_io(io, gc);
+  // write a sibling temporary and rename it into place: a reader never sees a half-written file
+  const std::string tmp = std::string(path) + ".part";
+  FileCloser fc{std::fopen(tmp.c_str(), "wb")};
+  if (fc.f == nullptr) {
+    set_error("table_save: cannot create '%s'", tmp.c_str());
+    return AIRICE_EIO;
+  }
+  bool ok = std::fwrite(hdr, 1, sizeof(hdr), fc.f) == sizeof(hdr);
+  for (int c = 0; ok && c < AIRICE_TABLE_COLUMNS && n_rays > 0; ++c)
+    ok = std::fwrite(h_table + (size_t)c * ld, sizeof(float), n_rays, fc.f) == n_rays;
+  ok = (std::fclose(fc.f) == 0) && ok;
+  fc.f = nullptr;
+  if (!ok || std::rename(tmp.c_str(), path) != 0) {
+    std::remove(tmp.c_str());
+    set_error("table_save: writing '%s' failed", path);
+    return AIRICE_EIO;
+  }
+  return AIRICE_OK;
+}
+
+int airice_table_file_read_info(const char* path, airice_table_file_info* info) {
+  if (path == nullptr || info == nullptr) {
+    set_error("table_file_read_info: null argument");
+    return AIRICE_EINVAL;
+  }
+  FileCloser fc{std::fopen(path, "rb")};
+  if (fc.f == nullptr) {
+    set_error("table file: cannot open '%s'", path);
+    return AIRICE_EIO;
+  }
+  unsigned char hdr[AIRICE_TABLE_FILE_HEADER];
+  if (std::fread(hdr, 1, sizeof(hdr), fc.f) != sizeof(hdr) || std::memcmp(hdr, kTableMagic, 8)) {
+    set_error("table file '%s': not an airice table file", path);
+    return AIRICE_EINVAL;
+  }
+  uint32_t version = 0, hbytes = 0, cols = 0;
+  uint64_t n = 0, sum = 0;
+  HeaderIO io{hdr, 8, false};
+  io.f(version);
+  io.f(hbytes);
+  io.f(cols);
+  io.skip(12);
+  io.f(n);
+  io.f(sum);
+  if (version != kTableVersion || hbytes != AIRICE_TABLE_FILE_HEADER ||
+      cols != AIRICE_TABLE_COLUMNS) {
+    set_error("table file '%s': unsupported version %u / header %u / columns %u", path, version,
+              hbytes, cols);
+    return AIRICE_EINVAL;
+  }
+  std::memset(info, 0, sizeof(*info));
+  medium_io(io, info->medium);
+  grid_io(io, info->grid);
+  info->n_rays = n;
+  info->checksum = sum;
+  // the body must hold exactly the 11 columns the header announces
+  if (std::fseek(fc.f, 0, SEEK_END) != 0) {
+    set_error("table file '%s': cannot seek", path);
+    return AIRICE_EIO;
+  }
+  const long long len = (long long)ftello(fc.f);
+  const unsigned long long want =
+      (unsigned long long)AIRICE_TABLE_FILE_HEADER + (unsigned long long)AIRICE_TABLE_COLUMNS * 4ull * n;
+  if (n > (1ull << 56) || len < 0 || (unsigned long long)len != want) {
+    set_error("table file '%s': %lld bytes, the header announces %llu", path, len, want);
+    return AIRICE_EINVAL;
+  }
+  return AIRICE_OK;
+}
+
+int airice_table_load(const char* path, const airice_medium* expect, float* h_table, size_t ld,
+                      airice_table_file_info* info) {
+  airice_table_file_info fi;
+  int rc = airice_table_file_read_info(path, &fi);
+  if (rc != AIRICE_OK) return rc;
+  if (expect != nullptr && !same_medium(*expect, fi.medium)) {
+    set_error("table file '%s' was traced in another medium (atmosphere / ice model / variant)",
+              path);
+    return AIRICE_EINVAL;
+  }
+  const size_t n = (size_t)fi.n_rays;
+  if ((h_table == nullptr && n > 0) || ld < n) {
+    set_error("table_load: null table or column stride %zu < %zu entries", ld, n);
+    return AIRICE_EINVAL;
+  }
+  FileCloser fc{std::fopen(path, "rb")};
+  if (fc.f == nullptr || std::fseek(fc.f, AIRICE_TABLE_FILE_HEADER, SEEK_SET) != 0) {
+    set_error("table file: cannot open '%s'", path);
+    return AIRICE_EIO;
+  }
+  for (int c = 0; c < AIRICE_TABLE_COLUMNS && n > 0; ++c) {
+    if (std::fread(h_table + (size_t)c * ld, sizeof(float), n, fc.f) != n) {
+      set_error("table file '%s': short read in column %d", path, c);
+      return AIRICE_EIO;
+    }
+  }
+  if (airice_table_checksum(h_table, ld, n) != fi.checksum) {
+    set_error("table file '%s': checksum mismatch (corrupt file)", path);
+    return AIRICE_EIO;
+  }
+  if (info != nullptr) *info = fi;
   return AIRICE_OK;
 }
 

@@ -80,6 +80,41 @@ class AirIceSolver:
               "airice_table_host")
         return (table, fullarr) if full else table
 
+    # ------------------------------------------------------------------ table files
+    def save_table(self, path: str, grid: Grid, table) -> None:
+        """airice_table_save: one antenna's table (11 x n float32, numpy or a torch tensor on
+        any device) with this medium and ``grid`` in the header."""
+        if hasattr(table, "detach"):
+            table = table.detach().cpu().numpy()
+        t = np.asarray(table)
+        if t.dtype != np.float32 or t.ndim != 2 or t.shape[0] != _lib.TABLE_COLUMNS:
+            raise ValueError(f"save_table: want an ({_lib.TABLE_COLUMNS}, n) float32 table, "
+                             f"got {t.dtype} {t.shape}")
+        if t.strides[1] != 4:
+            t = np.ascontiguousarray(t)
+        check(lib().airice_table_save(str(path).encode(), ctypes.byref(self.medium),
+                                      ctypes.byref(grid), ptr(t), t.strides[0] // 4, t.shape[1]),
+              "airice_table_save")
+
+    @staticmethod
+    def table_file_info(path: str) -> _lib.TableFileInfo:
+        info = _lib.TableFileInfo()
+        check(lib().airice_table_file_read_info(str(path).encode(), ctypes.byref(info)),
+              "airice_table_file_read_info")
+        return info
+
+    def load_table(self, path: str, check_medium: bool = True):
+        """airice_table_load: (grid, 11 x n float32 numpy table), checksum-verified; with
+        ``check_medium`` a table traced in another medium is refused."""
+        info = self.table_file_info(path)
+        n = int(info.n_rays)
+        table = np.empty((_lib.TABLE_COLUMNS, n), dtype=np.float32)
+        check(lib().airice_table_load(str(path).encode(),
+                                      ctypes.byref(self.medium) if check_medium else None,
+                                      ptr(table), max(n, 1), ctypes.byref(info)),
+              "airice_table_load")
+        return info.grid, table
+
     # ------------------------------------------------------------------ rays
     def rays_device(self, launch_deg, txh, ice_h: float, depth: float, in_ice: bool, out,
                     ld: int | None = None, stream=None) -> None:

@@ -347,6 +347,31 @@ int airice_table_to_host(const float *d_table, size_t d_ld, size_t n_rays, float
 int airice_host_register(void *ptr, size_t bytes);
 int airice_host_unregister(void *ptr);
 
+/* --- table persistence (no reference counterpart: the reference keeps
+ * AllTableAllAntData in memory only, .cc:2101-2136) -------------------------------------------
+ * One antenna's host table in a file: a 512-byte little-endian header (magic "AIRTBL01", the
+ * medium and grid it was traced with, the entry count, a 64-bit checksum of the column bytes),
+ * then the 11 float32 columns of n_rays entries each, column after column.  Host-only (no GPU
+ * needed); a device table goes through airice_table_to_host first. */
+#define AIRICE_TABLE_FILE_HEADER 512
+typedef struct airice_table_file_info {
+  airice_medium medium; /* the medium the table was traced in */
+  airice_grid grid;     /* its grid; n_rays = table_rows x angle_steps for a whole table */
+  uint64_t n_rays;      /* entries per column */
+  uint64_t checksum;    /* of the 11 columns' bytes (airice_table_checksum) */
+} airice_table_file_info;
+/* 64-bit checksum of n_rays entries of the 11 columns (column stride ld). */
+uint64_t airice_table_checksum(const float *h_table, size_t ld, size_t n_rays);
+int airice_table_save(const char *path, const airice_medium *m, const airice_grid *g,
+                      const float *h_table, size_t ld, size_t n_rays);
+/* Header of a table file (validated: magic, version, sizes against the file length). */
+int airice_table_file_read_info(const char *path, airice_table_file_info *info);
+/* Load a table file into h_table (column stride ld >= the file's n_rays), verifying its checksum.
+ * expect (nullable): the medium the caller traces with -- a file traced in another medium (any
+ * parsed field differs) is rejected with AIRICE_EINVAL.  info (nullable) receives the header. */
+int airice_table_load(const char *path, const airice_medium *expect, float *h_table, size_t ld,
+                      airice_table_file_info *info);
+
 /* Kernel timing (bench.py's roofline legs; no reference counterpart).  When on, each launch
  * of a timed kernel is bracketed by a hipEvent pair on its own stream.  Names:
  * "table_kernel", "roots_kernel" (roots_kernel / roots_sorted_kernel, the minimizer's root

@@ -231,6 +231,60 @@ int main(int argc, char** argv) {
               "\"unpinned\": %d, \"col_vs_packed_mismatch\": %d, \"vs_oracle_mismatch\": %d},\n",
               qs.size(), n_checked, n_fallback, n_unpinned, n_col_vs_packed, n_vs_oracle);
 
+  // ---- table files: save / load round trip, then damaged files ------------------------------
+  {
+    airice_medium med;
+    airice_atmosphere_parse(atm.data(), atm.size(), AIRICE_VARIANT_MULTIRAY, &med);
+    airice_grid g;
+    airice_grid_init(&g, -20000.0, 300000.0, step_h, 92.0, 180.0, 1.0);
+    const std::string path = std::string(argv[2]) + ".airtbl";
+    int rc_save = airice_table_save(path.c_str(), &med, &g, cols.data(), (size_t)n, (size_t)n);
+    const size_t ld = (size_t)n + 7;  // a wider destination stride
+    std::vector<float> back(ld * AIRICE_TABLE_COLUMNS, -1.0f);
+    airice_table_file_info info;
+    int rc_load = airice_table_load(path.c_str(), &med, back.data(), ld, &info);
+    bool same = rc_save == 0 && rc_load == 0 && info.n_rays == (uint64_t)n &&
+                info.grid.angle_steps == g.angle_steps && info.medium.max_layers == med.max_layers;
+    for (int c = 0; same && c < AIRICE_TABLE_COLUMNS; ++c)
+      same = std::memcmp(back.data() + (size_t)c * ld, cols.data() + (size_t)c * n,
+                         sizeof(float) * (size_t)n) == 0;
+    // another medium (the pythonwrapper's pi) is refused
+    airice_medium other = med;
+    other.pi = 4.0 * std::atan(1.0);
+    const int rc_other = airice_table_load(path.c_str(), &other, back.data(), ld, nullptr);
+    // damaged copies: truncated at several lengths, a flipped body byte, a flipped magic byte, an
+    // inflated entry count, another version; every one must be refused without a fault
+    const std::string img = read_file(path.c_str());
+    std::vector<std::string> bad;
+    for (size_t cut : {(size_t)0, (size_t)7, (size_t)100, (size_t)511, (size_t)512,
+                       img.size() / 2, img.size() - 1})
+      bad.push_back(img.substr(0, cut));
+    std::string b = img;
+    b[AIRICE_TABLE_FILE_HEADER + 4 * (size_t)n + 3] ^= 0x10;
+    bad.push_back(b);
+    b = img;
+    b[0] ^= 1;
+    bad.push_back(b);
+    b = img;
+    b[32 + 7] = 0x7f;  // n_rays: ~2^62 entries
+    bad.push_back(b);
+    b = img;
+    b[8] = 2;  // version
+    bad.push_back(b);
+    b = img + "x";  // trailing byte
+    bad.push_back(b);
+    int rejected = 0;
+    const std::string bpath = path + ".bad";
+    for (const auto& s : bad) {
+      std::ofstream(bpath, std::ios::binary).write(s.data(), (std::streamsize)s.size());
+      rejected += airice_table_load(bpath.c_str(), nullptr, back.data(), ld, nullptr) != 0;
+    }
+    std::remove(bpath.c_str());
+    std::remove(path.c_str());
+    std::printf("\"table_file\": [%d, %d, %zu, %d],\n", same ? 1 : 0, rc_other != 0 ? 1 : 0,
+                bad.size(), rejected);
+  }
+
   // ---- the oracle's own ray / solve paths on edge geometries ---------------------------------
   {
     double d[18], dm[17], dp[15], a10[10];

@@ -53,4 +53,7 @@ def test_host_code_and_oracle_run_clean_under_asan_ubsan(tmp_path):
     lk = r["lookup"]
     assert lk["checked"] > 2500 and lk["col_vs_packed_mismatch"] == 0
     assert lk["vs_oracle_mismatch"] == 0
+    # table files: the round trip is exact, another medium and every damaged copy are refused
+    same, other_refused, n_bad, n_rejected = r["table_file"]
+    assert same == 1 and other_refused == 1 and n_bad == n_rejected == 12
     assert r["oracle_paths"] == 1

@@ -122,6 +122,33 @@ def test_lookup_rx_in_air(solver, oracle_medium):
     _run_case(solver, oracle_medium, 5000.0, 100.0, 90.1, 180.0, 0.3, 30000, 5)
 
 
+def test_lookup_on_saved_table(solver, tmp_path):
+    """Table persistence (f2): a GPU-built cfg2 table saved from the host copy, loaded back and
+    uploaded gives bit-identical lookups to the table it was saved from."""
+    import torch
+    g, table = _device_table(solver, -20000.0, 20.0, 92.0, 180.0, 0.5)
+    host = table.cpu().numpy()
+    solver.save_table(str(tmp_path / "cfg2.airtbl"), g, table)
+    g2, loaded = solver.load_table(str(tmp_path / "cfg2.airtbl"))
+    assert loaded.tobytes() == host.tobytes()
+    dev = torch.device("cuda:0")
+    t2 = torch.from_numpy(loaded).to(dev)
+    src, dist = parity.lookup_queries(host, 20000, seed=99)
+    n = src.size
+    ts, td, tp = (torch.from_numpy(a).to(dev) for a in (src, dist, np.full(n, -20000.0)))
+    res = []
+    for tab, grid in ((table, g), (t2, g2)):
+        out = torch.empty((9, n), dtype=torch.float64, device=dev)
+        ok = torch.empty(n, dtype=torch.uint8, device=dev)
+        fl = torch.empty(n, dtype=torch.uint8, device=dev)
+        solver.table_lookup_device(solver.lookup_table(tab, grid), ts, td, tp, ICE_CM, out, ok, fl,
+                                   stream=torch.cuda.current_stream())
+        torch.cuda.synchronize()
+        res.append((out.cpu().numpy(), ok.cpu().numpy(), fl.cpu().numpy()))
+    assert np.array_equal(res[0][0], res[1][0], equal_nan=True)
+    assert np.array_equal(res[0][1], res[1][1]) and np.array_equal(res[0][2], res[1][2])
+
+
 def test_lookup_empty_batch(solver):
     import torch
     g, table = _device_table(solver, -20000.0, 1000.0, 92.0, 180.0, 1.0)
