@@ -97,6 +97,11 @@ constexpr int kTableBlock = AIRICE_TABLE_BS;
 #define AIRICE_UNIFORM_PHASE 0
 #endif
 // ... and both guards of a lane in one pass
+// debug build (tools/solve_stats.py with a -DAIRICE_SORTED_STATS=1 library): AIRICE_SOLVE_STATS
+// keeps the batch-wide grouping and records the counts by sorted position
+#ifndef AIRICE_SORTED_STATS
+#define AIRICE_SORTED_STATS 0
+#endif
 #ifndef AIRICE_PAIR_GUARDS
 #define AIRICE_PAIR_GUARDS 0
 #endif
@@ -2033,6 +2038,14 @@ __global__ __launch_bounds__(kSortedBlock, AIRICE_SORTED_WAVES) void roots_sorte
   const Geometry g = load_rec<IN>(M, Q, recs[ks], thR);
   const SolveResult r = solve_root(M, I, g, thR, park.exact != 0, &s_logtab[0][0]);
   sorted_park[ks] = make_double2(r.root, (double)r.status);
+#if AIRICE_SORTED_STATS
+  // debug build: evaluation counts by sorted position, i.e. in the order the waves run them
+  if (park.stats != nullptr) {
+    park.stats[3 * ks] = r.n_eval;
+    park.stats[3 * ks + 1] = r.n_est;
+    park.stats[3 * ks + 2] = r.n_inside;
+  }
+#endif
 }
 
 // Stage 1's result of query k for stage 2.
@@ -2393,8 +2406,8 @@ static int launch_roots(const DevMedium& M, const IceConsts& I, const QueryArgs&
   const size_t group_min = group_min_batch();
   // (the table lookup's fallback pass stays block-local: its batch is the whole lookup batch,
   // of which typically well under 1 % of lanes are fallback lanes)
-  if (IN == IN_CM100 || group_min == 0 || n < group_min || park.stats != nullptr ||
-      n >= (1ull << 31)) {
+  if (IN == IN_CM100 || group_min == 0 || n < group_min ||
+      (park.stats != nullptr && !AIRICE_SORTED_STATS) || n >= (1ull << 31)) {
     ktimer_begin(KT_ROOTS, st);
     hipLaunchKernelGGL((roots_kernel<IN>), roots_grid(n), dim3(kRootsBlock), 0, st, M, I, Q, park,
                        nullptr, (size_t)0, nullptr);

@@ -771,9 +771,18 @@ int airice_table_to_host(const float* d_table, size_t d_ld, size_t n_rays, float
     set_error("table_to_host: null table or column stride < n_rays");
     return AIRICE_EINVAL;
   }
-  HIP_TRY(hipMemcpy2DAsync(h_table, sizeof(float) * h_ld, d_table, sizeof(float) * d_ld,
-                           sizeof(float) * n_rays, AIRICE_TABLE_COLUMNS, hipMemcpyDeviceToHost,
-                           (hipStream_t)stream));
+  const hipStream_t st = (hipStream_t)stream;
+  if (d_ld == n_rays && h_ld == n_rays) {  // both tables dense: one copy
+    HIP_TRY(hipMemcpyAsync(h_table, d_table, sizeof(float) * n_rays * AIRICE_TABLE_COLUMNS,
+                           hipMemcpyDeviceToHost, st));
+    return AIRICE_OK;
+  }
+  // One copy per column.  (A 2D copy with the host table's pitch fails with "invalid argument"
+  // when the host rows are a slab of a larger table -- the multi-GPU host assembly, where each
+  // rank page-locks only its own rows of each column -- and each column is a contiguous range.)
+  for (int c = 0; c < AIRICE_TABLE_COLUMNS; ++c)
+    HIP_TRY(hipMemcpyAsync(h_table + (size_t)c * h_ld, d_table + (size_t)c * d_ld,
+                           sizeof(float) * n_rays, hipMemcpyDeviceToHost, st));
   return AIRICE_OK;
 }
 int airice_host_register(void* ptr, size_t bytes) {

@@ -47,3 +47,47 @@ def test_multi_antenna_launch_padded_stride_and_empty():
     torch.cuda.synchronize()
     assert torch.equal(wide[:, :g.n_rays].view(torch.int32), ref.view(torch.int32))
     assert np.all(wide[:, g.n_rays:].cpu().numpy() == 0)
+
+
+def test_sharded_host_assembly_with_registered_slabs(tmp_path):
+    """The multi-GPU host assembly (bench --workload cfg4, N > 1) in one process: each "rank"
+    page-locks only its own rows of every column of a shared /dev/shm-style table and copies its
+    device slab there with airice_table_to_host.  The copy must stay inside the registered rows
+    (a 2-D copy over the whole pitch failed with "invalid argument" on the GPU box)."""
+    import ctypes
+    import torch
+    from airiceraytracing_amd import AirIceSolver, _lib, make_grid
+    from airiceraytracing_amd.distributed import SharedHostTable, assemble_to_host, shard_rows
+    L = _lib.lib()
+    s = AirIceSolver()
+    dev = torch.device("cuda:0")
+    g = make_grid(-20000.0, 300000.0, 20.0, 92.0, 180.0, 0.5)
+    whole = torch.empty((11, g.n_rays), dtype=torch.float32, device=dev)
+    s.table_device(g, whole)
+    host = SharedHostTable(str(tmp_path / "table"), 11, g.n_rays, create=True)
+    host.tensor.fill_(float("nan"))
+    world = 3
+    for rank in range(world):
+        begin, count, per = shard_rows(g.table_rows, world, rank)
+        slab = torch.empty((11, per * g.angle_steps + 64), dtype=torch.float32, device=dev)
+        s.table_device(g, slab, None, row_begin=begin, row_count=count, ld=slab.shape[1])
+        torch.cuda.synchronize()
+        first, items = begin * g.angle_steps, count * g.angle_steps
+
+        def reg(ptr, nbytes):
+            _lib.check(L.airice_host_register(ctypes.c_void_p(ptr), nbytes), "register")
+
+        def copy(sl, cnt, h, f):
+            _lib.check(L.airice_table_to_host(ctypes.c_void_p(sl.data_ptr()), sl.stride(0), cnt,
+                                              ctypes.c_void_p(h.data_ptr() + 4 * f), h.stride(0),
+                                              None), "airice_table_to_host")
+
+        host.register_columns(first, items, reg)
+        assemble_to_host(slab, items, first, host.tensor, copy)
+        torch.cuda.synchronize()
+        host.unregister(lambda p: _lib.check(L.airice_host_unregister(ctypes.c_void_p(p)),
+                                             "unregister"))
+    ref = whole.cpu().numpy()
+    got = host.tensor.numpy()
+    assert np.array_equal(ref.view(np.int32), got.view(np.int32))
+    host.close()
