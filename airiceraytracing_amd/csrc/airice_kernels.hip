@@ -2084,6 +2084,19 @@ __device__ __forceinline__ void stage_log_table(double (*s)[2]) {
 // and the one-query fused kernel (scalar_solve_kernel).
 // WAVE (one-query kernel): every lane runs the body with the root in wr; evaluate_root_wave
 // spreads the evaluation over the wave and lane 0 writes the outputs.
+// Stage-2 output stores: written once and not read back by the kernel (AIRICE_NT_OUT: as
+// non-temporal stores)
+#ifndef AIRICE_NT_OUT
+#define AIRICE_NT_OUT 0
+#endif
+__device__ __forceinline__ void put_out(double* p, double v) {
+#if AIRICE_NT_OUT
+  __builtin_nontemporal_store(v, p);
+#else
+  *p = v;
+#endif
+}
+
 template <int VARIANT, bool WAVE = false>
 __device__ __forceinline__ void solve_out_body(const DevMedium& M, const IceConsts& I,
                                                const QueryArgs& Q, double* __restrict__ out,
@@ -2100,37 +2113,45 @@ __device__ __forceinline__ void solve_out_body(const DevMedium& M, const IceCons
   if (WAVE && threadIdx.x != 0) return;
   const double thd = S.thd_ice + S.thd_air;
   const double tt = S.t_ice + S.t_air;
-  out[0 * ld + k] = g.H;
-  out[1 * ld + k] = thd;
-  out[2 * ld + k] = S.thd_air;
-  out[3 * ld + k] = S.thd_ice;
-  out[4 * ld + k] = tt * kSpeedC;
-  out[5 * ld + k] = S.t_ice * kSpeedC;
-  out[6 * ld + k] = S.t_air * kSpeedC;
-  out[7 * ld + k] = tt;
-  out[8 * ld + k] = S.t_ice;
-  out[9 * ld + k] = S.t_air;
-  out[10 * ld + k] = S.launch;
+  put_out(out + 0 * ld + k, g.H);
+  put_out(out + 1 * ld + k, thd);
+  put_out(out + 2 * ld + k, S.thd_air);
+  put_out(out + 3 * ld + k, S.thd_ice);
+  put_out(out + 4 * ld + k, tt * kSpeedC);
+  put_out(out + 5 * ld + k, S.t_ice * kSpeedC);
+  put_out(out + 6 * ld + k, S.t_air * kSpeedC);
+  put_out(out + 7 * ld + k, tt);
+  put_out(out + 8 * ld + k, S.t_ice);
+  put_out(out + 9 * ld + k, S.t_air);
+  put_out(out + 10 * ld + k, S.launch);
   if (VARIANT == AIRICE_VARIANT_MULTIRAY) {
     double tS, tP;
     fresnel_from_sine(S.ice_n, I.ice0.n, S.ice_n / I.ice0.n, sin_start(S.inc * M.d2r), tS, tP);
-    out[11 * ld + k] = S.ant;
-    out[12 * ld + k] = tS;
-    out[13 * ld + k] = tP;
-    out[14 * ld + k] = S.geo_air;
-    out[15 * ld + k] = S.geo_ice;
-    out[16 * ld + k] = S.inc;
+    put_out(out + 11 * ld + k, S.ant);
+    put_out(out + 12 * ld + k, tS);
+    put_out(out + 13 * ld + k, tP);
+    put_out(out + 14 * ld + k, S.geo_air);
+    put_out(out + 15 * ld + k, S.geo_ice);
+    put_out(out + 16 * ld + k, S.inc);
   } else {
-    out[11 * ld + k] = k_asin((S.ice_n / I.ice0.n) * sin_start(S.inc * M.d2r)) * M.r2d;
-    out[12 * ld + k] = S.ant;
-    out[13 * ld + k] = S.geo_air;
-    out[14 * ld + k] = S.geo_ice;
+    put_out(out + 11 * ld + k, k_asin((S.ice_n / I.ice0.n) * sin_start(S.inc * M.d2r)) * M.r2d);
+    put_out(out + 12 * ld + k, S.ant);
+    put_out(out + 13 * ld + k, S.geo_air);
+    put_out(out + 14 * ld + k, S.geo_ice);
   }
   if (status != nullptr) status[k] = (uint8_t)S.status;
 }
 
+// occupancy of the stage-2 kernel (0: the compiler's choice, 80 VGPRs = 6 waves/SIMD)
+#ifndef AIRICE_OUT_WAVES
+#define AIRICE_OUT_WAVES 0
+#endif
 template <int VARIANT>
-__global__ __launch_bounds__(kBlock) void solve_out_kernel(DevMedium M, IceConsts I, QueryArgs Q,
+__global__ __launch_bounds__(kBlock)
+#if AIRICE_OUT_WAVES
+__attribute__((amdgpu_waves_per_eu(AIRICE_OUT_WAVES, AIRICE_OUT_WAVES)))
+#endif
+void solve_out_kernel(DevMedium M, IceConsts I, QueryArgs Q,
                                                            double* __restrict__ out, size_t ld,
                                                            uint8_t* __restrict__ status,
                                                            SortedPark sp) {
