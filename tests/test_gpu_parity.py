@@ -158,6 +158,33 @@ def test_pywrapper_trace_cfg5_sample(solver_py, oracle_medium_py):
     assert rep["ok"], rep
 
 
+def test_pywrapper_trace_cfg5_full_size(solver_py, oracle_medium_py):
+    """BASELINE cfg5 at its full size (1e7 Py_TraceIceToAir queries through the batch entry, as
+    bench.py's pywrapper line runs it): every 97th query against the oracle, and on the whole
+    batch the solved fraction and finite outputs on every solved row."""
+    import torch
+    n = 10_000_000
+    depth, ice, txh, dist = parity.cfg5_queries(n)
+    dev = torch.device("cuda:0")
+    t = [torch.from_numpy(np.ascontiguousarray(a)).to(dev) for a in (depth, ice, txh, dist)]
+    out = torch.empty((n, 10), dtype=torch.float64, device=dev)
+    solver_py.trace_ice_to_air_device(*t, out)
+    torch.cuda.synchronize()
+    out = out.cpu().numpy()
+    del t
+    idx = np.arange(0, n, 97)
+    ref = oracle.py_trace_batch(oracle_medium_py, depth[idx], ice[idx], txh[idx], dist[idx],
+                                nthreads=NTHREADS)
+    got = out[idx]
+    assert np.count_nonzero((got[:, 0] != -1000) != (ref[:, 0] != -1000)) == 0
+    rep = parity.compare_columns(got.T, ref.T, parity.TRACE_FLOORS)
+    _report("trace-cfg5-1e7-stride97", rep)
+    assert rep["ok"], rep
+    solved = out[:, 0] != -1000
+    assert 0.96 < solved.mean() < 0.975  # bench r02/r03: 0.9676
+    assert np.isfinite(out[solved]).all()
+
+
 def test_py_trace_kat_through_ctypes_symbol(tmp_path, monkeypatch, atmosphere_text):
     """Py_TraceIceToAir(-10, 3000, 8050, 10000) KAT through the exported symbol."""
     import ctypes
