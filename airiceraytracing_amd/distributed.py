@@ -125,8 +125,8 @@ class SharedHostTable:
 def assemble_to_host(slab: torch.Tensor, count_items: int, first_item: int, host: torch.Tensor,
                      copy=None) -> None:
     """This rank's part of the host-assembled table: host[:, first:first+count] = slab[:, :count].
-    ``copy(slab, count, host, first)`` performs it (the GPU path: one 2-D DMA per rank,
-    airice_table_to_host); default: a torch copy (CPU ranks)."""
+    ``copy(slab, count, host, first)`` performs it (the GPU path: airice_table_to_host, one D2H
+    copy per column into this rank's page-locked rows); default: a torch copy (CPU ranks)."""
     if count_items == 0:
         return
     if copy is not None:
