@@ -23,13 +23,13 @@ def main():
     s = AirIceSolver()
     dev = torch.device("cuda:0")
     txh, dist, dep = [torch.from_numpy(a).to(dev) for a in parity.cfg3_queries(n)]
-    out = torch.zeros((26, 1), dtype=torch.float64, device=dev)
+    out = torch.zeros((28, 1), dtype=torch.float64, device=dev)
     st = torch.empty(1, dtype=torch.uint8, device=dev)
     rows = []
     for i in range(n):
         s.solve_device(txh[i:i + 1], dist[i:i + 1], dep[i:i + 1], 3000.0, out, st, ld=1)
         torch.cuda.synchronize()
-        rows.append(out[17:26, 0].cpu().numpy().copy())
+        rows.append(out[17:28, 0].cpu().numpy().copy())
     a = np.array(rows)
     ghz = a[:, 3] / (a[:, 4] * 10.0)  # ticks per 10 ns
     names = ["setup", "roots", "stage2", "total"]
@@ -39,7 +39,9 @@ def main():
            "evals_mean": float(a[:, 5].mean()),
            "eval_us_median": float(np.median(a[:, 6] / ghz / 1e3)),
            "solve_setup_us_median": float(np.median(a[:, 7] / ghz / 1e3)),
-           "lean_bisect_us_median": float(np.median(a[:, 8] / ghz / 1e3))})
+           "lean_bisect_us_median": float(np.median(a[:, 8] / ghz / 1e3)),
+           "pre_eval_us_median": float(np.median(a[:, 9] / ghz / 1e3)),
+           "post_eval_us_median": float(np.median(a[:, 10] / ghz / 1e3))})
 
 
 if __name__ == "__main__":
