@@ -105,6 +105,11 @@ constexpr int kTableBlock = AIRICE_TABLE_BS;
 #ifndef AIRICE_PAIR_GUARDS
 #define AIRICE_PAIR_GUARDS 0
 #endif
+// the table launch reads its rows' constants from a per-(medium, grid) device cache instead of
+// computing them in each block's prologue
+#ifndef AIRICE_ROWCONST_CACHE
+#define AIRICE_ROWCONST_CACHE 1
+#endif
 #ifndef AIRICE_ROWCONST_ALIGN16
 #define AIRICE_ROWCONST_ALIGN16 0
 #endif
@@ -377,6 +382,8 @@ struct TableArgs {
   int rows_per_block; // LDS rows a block's set of rays may span
   int half;           // rays per set (R = 2: ceil(n / 2); R = 1: n)
   size_t ld;
+  const struct RowConst* rc;  // AIRICE_ROWCONST_CACHE: the grid's row constants (all hsteps
+                              // rows, computed once per medium and grid), else nullptr
 };
 
 // Debug timeline (AIRICE_TABLE_TRACE=<file>, tools/wave_timeline.py): per wave, the 100 MHz
@@ -498,7 +505,12 @@ __device__ __forceinline__ void table_block(const DevMedium& M, const IceConsts&
     r0[j] = kb < ke ? ray_row(G, kb) : 0;
     const int nrows = kb < ke ? ray_row(G, ke - 1) - r0[j] + 1 : 0;
     for (int t = threadIdx.x; t < nrows; t += BS)
+#if AIRICE_ROWCONST_CACHE
+      rows[j * G.rows_per_block + t] = G.rc != nullptr ? G.rc[G.row0 + r0[j] + t]
+                                                       : row_const(M, I, row_height(G, G.row0 + r0[j] + t));
+#else
       rows[j * G.rows_per_block + t] = row_const(M, I, row_height(G, G.row0 + r0[j] + t));
+#endif
   }
   __syncthreads();
   prio_remaining(AIRICE_TABLE_PRIO, 3);
@@ -556,6 +568,14 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(AIRICE_TABLE
   a = __builtin_amdgcn_readfirstlane(a);
   table_block<BS, 1, false>(M, Iv[a], Gv[a], map.table[a], nullptr, nullptr,
                             blockIdx.x - (unsigned)map.begin[a]);
+}
+
+// Row constants of a whole grid (AIRICE_ROWCONST_CACHE): one row per lane, the table block's own
+// row_const on the same heights, so the cached values are the bits the block would compute.
+__global__ __launch_bounds__(256) void rowconst_kernel(DevMedium M, IceConsts I, TableArgs G,
+                                                       RowConst* __restrict__ out) {
+  const int r = (int)(blockIdx.x * 256 + threadIdx.x);
+  if (r < G.hsteps) out[r] = row_const(M, I, row_height(G, r));
 }
 
 // One forward ray spread over a wave (the one-query GetRayTracingSolutions call): the running
@@ -2480,6 +2500,71 @@ static int release_roots(void* ws, hipStream_t st) {
 }
 
 
+#if AIRICE_ROWCONST_CACHE
+// The row constants of a table grid (every Tx-height row: RowConst, 104 B), computed once per
+// (medium, ice constants, grid heights) by rowconst_kernel into a device buffer that is never
+// overwritten: a new key gets a new buffer, and the least recently used of kRowSets is freed
+// (hipFree waits for kernels still reading it).  The caller holds row_cache_mutex() from the
+// lookup until its launches are enqueued, so no other thread can evict a buffer in between; a
+// multi-antenna launch touches at most kMaxAntennas (< kRowSets) sets, so its own are never the
+// least recently used.
+static std::mutex& row_cache_mutex() {
+  static std::mutex mu;
+  return mu;
+}
+static int row_consts_cached(const DevMedium& M, const IceConsts& I, const TableArgs& A,
+                             hipStream_t st, const RowConst** out) {
+  struct RowSet {
+    std::vector<unsigned char> key;
+    RowConst* dev = nullptr;
+    unsigned long long used = 0;
+  };
+  constexpr size_t kRowSets = 64;
+  static std::vector<std::vector<RowSet>> caches;
+  static unsigned long long tick = 0;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return AIRICE_EHIP;
+  const double gk[3] = {A.start_h, A.stop_h, A.step_h};
+  std::vector<unsigned char> key(sizeof(M) + sizeof(I) + sizeof(gk) + sizeof(int));
+  unsigned char* kp = key.data();
+  std::memcpy(kp, &M, sizeof(M));
+  std::memcpy(kp + sizeof(M), &I, sizeof(I));
+  std::memcpy(kp + sizeof(M) + sizeof(I), gk, sizeof(gk));
+  std::memcpy(kp + sizeof(M) + sizeof(I) + sizeof(gk), &A.hsteps, sizeof(int));
+  if (caches.size() <= (size_t)dev) caches.resize(dev + 1);
+  std::vector<RowSet>& sets = caches[dev];
+  RowSet* c = nullptr;
+  for (RowSet& e : sets)
+    if (e.key == key) c = &e;
+  if (c == nullptr) {
+    if (sets.size() >= kRowSets) {
+      size_t old = 0;
+      for (size_t k = 1; k < sets.size(); ++k)
+        if (sets[k].used < sets[old].used) old = k;
+      if (hipFree(sets[old].dev) != hipSuccess) return AIRICE_EHIP;
+      sets.erase(sets.begin() + (long)old);
+    }
+    RowSet e;
+    if (hipMalloc(&e.dev, sizeof(RowConst) * (size_t)std::max(A.hsteps, 1)) != hipSuccess)
+      return AIRICE_EHIP;
+    hipLaunchKernelGGL(rowconst_kernel, dim3((unsigned)((A.hsteps + 255) / 256)), dim3(256), 0, st,
+                       M, I, A, e.dev);
+    // complete before a launch on another stream can read it
+    if (hipGetLastError() != hipSuccess || hipStreamSynchronize(st) != hipSuccess) {
+      (void)hipFree(e.dev);
+      return AIRICE_EHIP;
+    }
+    e.key = std::move(key);
+    sets.push_back(std::move(e));
+    c = &sets.back();
+  }
+  c->used = ++tick;
+  *out = c->dev;
+  return AIRICE_OK;
+}
+static_assert(kMaxAntennas < 64, "a multi-antenna launch never evicts its own row sets");
+#endif
+
 int launch_table(const DevMedium& M, const IceConsts& I, const airice_grid* g, int row_begin,
                  int row_count, float* d_table, double* d_full, size_t ld, hipStream_t st) {
   if (row_count <= 0 || g->angle_steps <= 0) return AIRICE_OK;
@@ -2497,6 +2582,11 @@ int launch_table(const DevMedium& M, const IceConsts& I, const airice_grid* g, i
   A.inv_asteps = 1.0 / (double)g->angle_steps;
   // rows a 256-ray set can touch, for the LDS row constants
   A.rows_per_block = std::min(kTableBlock, (kTableBlock - 1) / g->angle_steps + 2);
+  A.rc = nullptr;
+#if AIRICE_ROWCONST_CACHE
+  std::unique_lock<std::mutex> rs_lock(row_cache_mutex());  // held until the launches are enqueued
+  if (int rc = row_consts_cached(M, I, A, st, &A.rc)) return rc;
+#endif
   static const char* trace_path = getenv("AIRICE_TABLE_TRACE");
   static const int force_r = getenv("AIRICE_TABLE_RPL") ? atoi(getenv("AIRICE_TABLE_RPL")) : 0;
   // ray indices are 32-bit inside a launch: grids of kMaxLaunchRays or more go in row slabs
@@ -2564,6 +2654,9 @@ int launch_table_multi(const DevMedium& M, const IceConsts* Ih, const airice_gri
     return AIRICE_EINVAL;
   }
   std::vector<TableArgs> Ah(n);
+#if AIRICE_ROWCONST_CACHE
+  std::unique_lock<std::mutex> rs_lock(row_cache_mutex());  // held until the launch is enqueued
+#endif
   MultiMap map;
   std::memset(&map, 0, sizeof(map));
   map.n_ant = n;
@@ -2591,6 +2684,10 @@ int launch_table_multi(const DevMedium& M, const IceConsts* Ih, const airice_gri
     A.inv_asteps = 1.0 / (double)g->angle_steps;
     A.rows_per_block = rpb;
     A.row0 = 0;
+    A.rc = nullptr;
+#if AIRICE_ROWCONST_CACHE
+    if (int rc = row_consts_cached(M, Ih[a], A, st, &A.rc)) return rc;
+#endif
     const long long rays = (long long)g->table_rows * g->angle_steps;
     if (rays >= kMaxLaunchRays - 2 * kTableBlock || lds[a] < (size_t)rays) {
       set_error("antenna %d: %lld rays (ld %zu) do not fit one multi-antenna launch", a, rays,

@@ -91,3 +91,34 @@ def test_sharded_host_assembly_with_registered_slabs(tmp_path):
     got = host.tensor.numpy()
     assert np.array_equal(ref.view(np.int32), got.view(np.int32))
     host.close()
+
+
+def test_row_constant_cache_follows_medium_and_grid(oracle_medium):
+    """The table launch reads its row constants from a device cache keyed by the medium, the ice
+    constants and the grid heights (AIRICE_ROWCONST_CACHE): alternating grids, antenna depths and
+    a second medium must each give the tables an uncached build gives (checked against the
+    oracle's float table), including after the first entries are revisited."""
+    import torch
+    import oracle
+    from airiceraytracing_amd import AirIceSolver, make_grid
+    from tests import parity
+    s = AirIceSolver()
+    dev = torch.device("cuda:0")
+    cases = [(-20000.0, 300000.0, 100.0, 92.0, 180.0, 1.0),
+             (-5000.0, 300000.0, 100.0, 92.0, 180.0, 1.0),     # other antenna depth: other I
+             (-20000.0, 310000.0, 100.0, 92.0, 180.0, 1.0),    # other ice height
+             (-20000.0, 300000.0, 70.0, 92.0, 180.0, 1.0)]     # other height step
+    first = {}
+    for rep in range(2):
+        for args in cases:
+            g = make_grid(*args)
+            t = torch.empty((11, g.n_rays), dtype=torch.float32, device=dev)
+            s.table_device(g, t)
+            torch.cuda.synchronize()
+            got = t.cpu().numpy()
+            if rep == 0:
+                ref = oracle.table_rows(oracle_medium, oracle.grid_init(*args), 0, g.table_rows)
+                assert parity.float_ulp_diff(got, ref) <= 1, args
+                first[args] = got
+            else:
+                assert np.array_equal(got.view(np.int32), first[args].view(np.int32)), args
