@@ -110,6 +110,10 @@ constexpr int kTableBlock = AIRICE_TABLE_BS;
 #ifndef AIRICE_ROWCONST_CACHE
 #define AIRICE_ROWCONST_CACHE 1
 #endif
+// ... and the start-angle sine of every grid column from a per-angle-grid device cache
+#ifndef AIRICE_ANGLE_CACHE
+#define AIRICE_ANGLE_CACHE 1
+#endif
 #ifndef AIRICE_ROWCONST_ALIGN16
 #define AIRICE_ROWCONST_ALIGN16 0
 #endif
@@ -284,14 +288,16 @@ __device__ __forceinline__ void ray_solution_row(const DevMedium& M, const IceCo
                                                  const RowConst& rc, double theta, bool in_ice,
                                                  double* d, bool want_inc,
                                                  const double* tab = &kLogTable[0][0],
-                                                 int top_hi = -1, int prio_after = -1) {
+                                                 int top_hi = -1, int prio_after = -1,
+                                                 const double* v_start = nullptr) {
   // prio_after >= 0: table launch; segments of later rays of this lane still to come
   const bool prio = AIRICE_TABLE_PRIO && prio_after >= 0;
   const double H = rc.H;
   const int top = rc.top;
   const int bot = I.bot;
   const double A2 = M.A_air * M.A_air;
-  double v = sin_start((180 - theta) * M.d2r);  // sine of StartAngle (.cc:1863)
+  // sine of StartAngle (.cc:1863); v_start: the same value, formed by the caller
+  double v = v_start != nullptr ? *v_start : sin_start((180 - theta) * M.d2r);
   double thd_air = 0.0, t_air = 0.0, geo_air = 0.0;
   const bool any = rc.any != 0;
   if (any) {
@@ -384,6 +390,7 @@ struct TableArgs {
   size_t ld;
   const struct RowConst* rc;  // AIRICE_ROWCONST_CACHE: the grid's row constants (all hsteps
                               // rows, computed once per medium and grid), else nullptr
+  const double* vs;           // AIRICE_ANGLE_CACHE: sin of the start angle of every column
 };
 
 // Debug timeline (AIRICE_TABLE_TRACE=<file>, tools/wave_timeline.py): per wave, the 100 MHz
@@ -411,16 +418,28 @@ __device__ __forceinline__ int ray_row(const TableArgs& G, int k) {
 }
 
 // One table entry: ray k of the launch (row r, row-major over TxH rows x launch angles).
+// Launch angle of column iang of the grid (.cc:2085, 2092-2094).
+__device__ __forceinline__ double table_angle(const TableArgs& G, int iang) {
+  double th = G.start_a + G.step_a * iang;
+  if (iang == G.asteps - 1) th = G.stop_a;
+  return th;
+}
+
 __device__ __forceinline__ void table_ray(const DevMedium& M, const IceConsts& I,
                                           const TableArgs& G, const RowConst& rc, int r, int k,
                                           float* __restrict__ table, double* __restrict__ full,
                                           const double* tab, int top_hi, int prio_after) {
   const int iang = k - r * G.asteps;
-  // .cc:2085, 2092-2094
-  double th = G.start_a + G.step_a * iang;
-  if (iang == G.asteps - 1) th = G.stop_a;
+  const double th = table_angle(G, iang);
   double d[18];
+#if AIRICE_ANGLE_CACHE
+  // the start-angle sine of every grid column, formed once per angle grid (angle_sines_kernel)
+  const double vs = G.vs[iang];
+  ray_solution_row(M, I, rc, th, G.in_ice != 0, d, full != nullptr, tab, top_hi, prio_after,
+                   &vs);
+#else
   ray_solution_row(M, I, rc, th, G.in_ice != 0, d, full != nullptr, tab, top_hi, prio_after);
+#endif
   const size_t ld = G.ld;
 #if AIRICE_SADDR_STORE
   // AllTableAllAntData columns (.cc:2101-2111): the column base is wave-uniform, the lane's byte
@@ -576,6 +595,13 @@ __global__ __launch_bounds__(256) void rowconst_kernel(DevMedium M, IceConsts I,
                                                        RowConst* __restrict__ out) {
   const int r = (int)(blockIdx.x * 256 + threadIdx.x);
   if (r < G.hsteps) out[r] = row_const(M, I, row_height(G, r));
+}
+
+// Start-angle sines of a grid's columns (AIRICE_ANGLE_CACHE): the table ray's own expression.
+__global__ __launch_bounds__(256) void angle_sines_kernel(DevMedium M, TableArgs G,
+                                                          double* __restrict__ out) {
+  const int a = (int)(blockIdx.x * 256 + threadIdx.x);
+  if (a < G.asteps) out[a] = sin_start((180 - table_angle(G, a)) * M.d2r);
 }
 
 // One forward ray spread over a wave (the one-query GetRayTracingSolutions call): the running
@@ -2564,6 +2590,52 @@ static int row_consts_cached(const DevMedium& M, const IceConsts& I, const Table
 }
 static_assert(kMaxAntennas < 64, "a multi-antenna launch never evicts its own row sets");
 #endif
+#if AIRICE_ANGLE_CACHE
+// The start-angle sines of an angle grid, kept like the row constants (same mutex, same rules).
+static int angle_sines_cached(const DevMedium& M, const TableArgs& A, hipStream_t st,
+                              const double** out) {
+  struct AngleSet {
+    double key[5];
+    double* dev = nullptr;
+    unsigned long long used = 0;
+  };
+  constexpr size_t kAngleSets = 64;
+  static std::vector<std::vector<AngleSet>> caches;
+  static unsigned long long tick = 0;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return AIRICE_EHIP;
+  const double key[5] = {M.d2r, A.start_a, A.stop_a, A.step_a, (double)A.asteps};
+  if (caches.size() <= (size_t)dev) caches.resize(dev + 1);
+  std::vector<AngleSet>& sets = caches[dev];
+  AngleSet* c = nullptr;
+  for (AngleSet& e : sets)
+    if (std::memcmp(e.key, key, sizeof(key)) == 0) c = &e;
+  if (c == nullptr) {
+    if (sets.size() >= kAngleSets) {
+      size_t old = 0;
+      for (size_t k = 1; k < sets.size(); ++k)
+        if (sets[k].used < sets[old].used) old = k;
+      if (hipFree(sets[old].dev) != hipSuccess) return AIRICE_EHIP;
+      sets.erase(sets.begin() + (long)old);
+    }
+    AngleSet e;
+    std::memcpy(e.key, key, sizeof(key));
+    if (hipMalloc(&e.dev, sizeof(double) * (size_t)std::max(A.asteps, 1)) != hipSuccess)
+      return AIRICE_EHIP;
+    hipLaunchKernelGGL(angle_sines_kernel, dim3((unsigned)((A.asteps + 255) / 256)), dim3(256), 0,
+                       st, M, A, e.dev);
+    if (hipGetLastError() != hipSuccess || hipStreamSynchronize(st) != hipSuccess) {
+      (void)hipFree(e.dev);
+      return AIRICE_EHIP;
+    }
+    sets.push_back(e);
+    c = &sets.back();
+  }
+  c->used = ++tick;
+  *out = c->dev;
+  return AIRICE_OK;
+}
+#endif
 
 int launch_table(const DevMedium& M, const IceConsts& I, const airice_grid* g, int row_begin,
                  int row_count, float* d_table, double* d_full, size_t ld, hipStream_t st) {
@@ -2586,6 +2658,10 @@ int launch_table(const DevMedium& M, const IceConsts& I, const airice_grid* g, i
 #if AIRICE_ROWCONST_CACHE
   std::unique_lock<std::mutex> rs_lock(row_cache_mutex());  // held until the launches are enqueued
   if (int rc = row_consts_cached(M, I, A, st, &A.rc)) return rc;
+#endif
+  A.vs = nullptr;
+#if AIRICE_ANGLE_CACHE
+  if (int rc = angle_sines_cached(M, A, st, &A.vs)) return rc;
 #endif
   static const char* trace_path = getenv("AIRICE_TABLE_TRACE");
   static const int force_r = getenv("AIRICE_TABLE_RPL") ? atoi(getenv("AIRICE_TABLE_RPL")) : 0;
@@ -2687,6 +2763,10 @@ int launch_table_multi(const DevMedium& M, const IceConsts* Ih, const airice_gri
     A.rc = nullptr;
 #if AIRICE_ROWCONST_CACHE
     if (int rc = row_consts_cached(M, Ih[a], A, st, &A.rc)) return rc;
+#endif
+    A.vs = nullptr;
+#if AIRICE_ANGLE_CACHE
+    if (int rc = angle_sines_cached(M, A, st, &A.vs)) return rc;
 #endif
     const long long rays = (long long)g->table_rows * g->angle_steps;
     if (rays >= kMaxLaunchRays - 2 * kTableBlock || lds[a] < (size_t)rays) {

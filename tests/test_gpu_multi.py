@@ -95,9 +95,10 @@ def test_sharded_host_assembly_with_registered_slabs(tmp_path):
 
 def test_row_constant_cache_follows_medium_and_grid(oracle_medium):
     """The table launch reads its row constants from a device cache keyed by the medium, the ice
-    constants and the grid heights (AIRICE_ROWCONST_CACHE): alternating grids, antenna depths and
-    a second medium must each give the tables an uncached build gives (checked against the
-    oracle's float table), including after the first entries are revisited."""
+    constants and the grid heights (AIRICE_ROWCONST_CACHE), and its start-angle sines from one
+    keyed by the angle grid and the variant's degree-to-radian factor (AIRICE_ANGLE_CACHE):
+    alternating grids, antenna depths and the two variants must each give the tables an uncached
+    build gives (checked against the oracle's float table), also when entries are revisited."""
     import torch
     import oracle
     from airiceraytracing_amd import AirIceSolver, make_grid
@@ -107,7 +108,8 @@ def test_row_constant_cache_follows_medium_and_grid(oracle_medium):
     cases = [(-20000.0, 300000.0, 100.0, 92.0, 180.0, 1.0),
              (-5000.0, 300000.0, 100.0, 92.0, 180.0, 1.0),     # other antenna depth: other I
              (-20000.0, 310000.0, 100.0, 92.0, 180.0, 1.0),    # other ice height
-             (-20000.0, 300000.0, 70.0, 92.0, 180.0, 1.0)]     # other height step
+             (-20000.0, 300000.0, 70.0, 92.0, 180.0, 1.0),     # other height step
+             (-20000.0, 300000.0, 100.0, 90.1, 180.0, 0.7)]    # other angle grid (AIRICE_ANGLE_CACHE)
     first = {}
     for rep in range(2):
         for args in cases:
@@ -122,3 +124,25 @@ def test_row_constant_cache_follows_medium_and_grid(oracle_medium):
                 first[args] = got
             else:
                 assert np.array_equal(got.view(np.int32), first[args].view(np.int32)), args
+
+
+def test_cached_table_equals_per_lane_rays_in_both_variants():
+    """The table launch's cached row constants and start-angle sines (keyed by the medium, so by
+    the variant's degree-to-radian factor too) against rays_kernel, which forms both per lane:
+    the 18 doubles of every entry bit for bit, for each variant, built alternately."""
+    import torch
+    from airiceraytracing_amd import AirIceSolver, VARIANT_MULTIRAY, VARIANT_PYWRAPPER, make_grid
+    dev = torch.device("cuda:0")
+    g = make_grid(-20000.0, 300000.0, 100.0, 92.0, 180.0, 1.0)
+    n = g.n_rays
+    for rep in range(2):
+        for variant in (VARIANT_MULTIRAY, VARIANT_PYWRAPPER):
+            s = AirIceSolver(variant=variant)
+            t = torch.empty((11, n), dtype=torch.float32, device=dev)
+            full = torch.empty((18, n), dtype=torch.float64, device=dev)
+            s.table_device(g, t, full)
+            rays = torch.empty((18, n), dtype=torch.float64, device=dev)
+            s.rays_device(full[11].contiguous(), full[1].contiguous(), g.stop_height, g.depth_m,
+                          bool(g.in_ice), rays)
+            torch.cuda.synchronize()
+            assert torch.equal(full.view(torch.int64), rays.view(torch.int64)), (rep, variant)
