@@ -126,10 +126,10 @@ def test_row_constant_cache_follows_medium_and_grid(oracle_medium):
                 assert np.array_equal(got.view(np.int32), first[args].view(np.int32)), args
 
 
-def test_cached_table_equals_per_lane_rays_in_both_variants():
-    """The table launch's cached row constants and start-angle sines (keyed by the medium, so by
-    the variant's degree-to-radian factor too) against rays_kernel, which forms both per lane:
-    the 18 doubles of every entry bit for bit, for each variant, built alternately."""
+def test_cached_table_equals_per_lane_rays():
+    """The table launch's cached row constants and start-angle sines against rays_kernel, which
+    forms both per lane: the 18 doubles of every entry bit for bit, for the media of both solver
+    variants, built alternately (MakeRayTracingTable is MultiRay's, so both use its pi)."""
     import torch
     from airiceraytracing_amd import AirIceSolver, VARIANT_MULTIRAY, VARIANT_PYWRAPPER, make_grid
     dev = torch.device("cuda:0")
