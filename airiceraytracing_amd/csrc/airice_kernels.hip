@@ -433,8 +433,13 @@ __device__ __forceinline__ void table_ray(const DevMedium& M, const IceConsts& I
   const double th = table_angle(G, iang);
   double d[18];
 #if AIRICE_ANGLE_CACHE
-  // the start-angle sine of every grid column, formed once per angle grid (angle_sines_kernel)
-  const double vs = G.vs[iang];
+  // the start-angle sine of every grid column, formed once per angle grid (angle_sines_kernel);
+  // launches captured into a graph before their grid was cached form it here
+  double vs;
+  if (G.vs != nullptr)
+    vs = G.vs[iang];
+  else
+    vs = sin_start((180 - th) * M.d2r);
   ray_solution_row(M, I, rc, th, G.in_ice != 0, d, full != nullptr, tab, top_hi, prio_after,
                    &vs);
 #else
@@ -2538,6 +2543,12 @@ static std::mutex& row_cache_mutex() {
   static std::mutex mu;
   return mu;
 }
+// A stream that is being captured into a graph: a new cache entry would need a synchronisation,
+// which capture forbids, so such launches use what is cached and form the rest in the kernel.
+static bool stream_capturing(hipStream_t st) {
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  return hipStreamIsCapturing(st, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone;
+}
 static int row_consts_cached(const DevMedium& M, const IceConsts& I, const TableArgs& A,
                              hipStream_t st, const RowConst** out) {
   struct RowSet {
@@ -2562,6 +2573,10 @@ static int row_consts_cached(const DevMedium& M, const IceConsts& I, const Table
   RowSet* c = nullptr;
   for (RowSet& e : sets)
     if (e.key == key) c = &e;
+  if (c == nullptr && stream_capturing(st)) {
+    *out = nullptr;  // table_block forms the rows itself
+    return AIRICE_OK;
+  }
   if (c == nullptr) {
     if (sets.size() >= kRowSets) {
       size_t old = 0;
@@ -2610,6 +2625,10 @@ static int angle_sines_cached(const DevMedium& M, const TableArgs& A, hipStream_
   AngleSet* c = nullptr;
   for (AngleSet& e : sets)
     if (std::memcmp(e.key, key, sizeof(key)) == 0) c = &e;
+  if (c == nullptr && stream_capturing(st)) {
+    *out = nullptr;  // table_ray forms the sines itself
+    return AIRICE_OK;
+  }
   if (c == nullptr) {
     if (sets.size() >= kAngleSets) {
       size_t old = 0;

@@ -146,3 +146,38 @@ def test_cached_table_equals_per_lane_rays():
                           bool(g.in_ice), rays)
             torch.cuda.synchronize()
             assert torch.equal(full.view(torch.int64), rays.view(torch.int64)), (rep, variant)
+
+
+def test_table_launch_in_a_captured_graph():
+    """Table launches captured into a HIP graph (torch.cuda.graph): one whose grid is already in
+    the row / angle caches and one whose grid is not (capture forbids the synchronisation that
+    building a cache entry needs, so that launch forms its rows and sines in the kernel); each
+    replay gives the uncaptured launch's table bit for bit."""
+    import torch
+    from airiceraytracing_amd import AirIceSolver, make_grid
+    s = AirIceSolver()
+    dev = torch.device("cuda:0")
+    g_hot = make_grid(-20000.0, 300000.0, 100.0, 92.0, 180.0, 1.0)
+    g_new = make_grid(-17000.0, 300000.0, 90.0, 91.0, 180.0, 0.9)  # not built before
+    ref = {}
+    t_hot = torch.empty((11, g_hot.n_rays), dtype=torch.float32, device=dev)
+    s.table_device(g_hot, t_hot)
+    torch.cuda.synchronize()
+    ref["hot"] = t_hot.clone()
+    t_new = torch.full((11, g_new.n_rays), float("nan"), dtype=torch.float32, device=dev)
+    t_hot.fill_(float("nan"))
+    graph = torch.cuda.CUDAGraph()
+    side = torch.cuda.Stream()
+    side.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(side):
+        with torch.cuda.graph(graph, stream=side):
+            s.table_device(g_hot, t_hot, stream=side)
+            s.table_device(g_new, t_new, stream=side)
+    torch.cuda.synchronize()
+    graph.replay()
+    torch.cuda.synchronize()
+    want_new = torch.empty_like(t_new)
+    s.table_device(g_new, want_new)  # uncaptured: builds the cache entries
+    torch.cuda.synchronize()
+    assert torch.equal(t_hot.view(torch.int32), ref["hot"].view(torch.int32))
+    assert torch.equal(t_new.view(torch.int32), want_new.view(torch.int32))
