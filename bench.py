@@ -65,7 +65,7 @@ def parse():
                    help="N>1: one table sharded by TxH rows + RCCL gather (default), or one "
                         "antenna table per GPU")
     p.add_argument("--solve-n", type=int, default=1_000_000)
-    p.add_argument("--solve-steps", type=int, default=5)
+    p.add_argument("--solve-steps", type=int, default=20)
     p.add_argument("--no-cpu", action="store_true", help="skip the CPU legs (baselines, parity)")
     p.add_argument("--no-solve", action="store_true", help="skip the minimizer line item")
     p.add_argument("--no-lookup", action="store_true", help="skip the table-lookup line item")
@@ -335,7 +335,8 @@ def main():
         def solve_call():
             solver.solve_device(tq[0], tq[1], tq[2], 3000.0, out, stt, stream=stream)
 
-        solve_call()
+        for _ in range(2):  # warm-up: code objects, scratch pool
+            solve_call()
         torch.cuda.synchronize()
         barrier()
         torch.cuda.synchronize()
