@@ -114,6 +114,9 @@ constexpr int kTableBlock = AIRICE_TABLE_BS;
 #ifndef AIRICE_ANGLE_CACHE
 #define AIRICE_ANGLE_CACHE 1
 #endif
+#if AIRICE_ANGLE_CACHE && !AIRICE_ROWCONST_CACHE
+#error "AIRICE_ANGLE_CACHE shares the row-constant cache's lock and capture check"
+#endif
 #ifndef AIRICE_ROWCONST_ALIGN16
 #define AIRICE_ROWCONST_ALIGN16 0
 #endif
