@@ -145,7 +145,7 @@ EXPORTED_SYMBOLS = (
     "airice_trace_ice_to_air_host", "airice_rtf_outputs", "airice_rtf_eval",
     "airice_rtf_eval_variant", "Py_TraceIceToAir", "airice_device_count", "airice_set_device", "airice_malloc",
     "airice_free", "airice_memcpy_h2d", "airice_memcpy_d2h", "airice_synchronize",
-    "airice_kernel_timing", "airice_kernel_time", "airice_table_to_host",
+    "airice_kernel_timing", "airice_kernel_time", "airice_table_cache_stats", "airice_table_to_host",
     "airice_host_register", "airice_host_unregister", "airice_table_checksum",
     "airice_table_save", "airice_table_file_read_info", "airice_table_load",
 )
@@ -297,3 +297,15 @@ def kernel_time(name: str, reset: bool = True) -> tuple[float, int]:
     check(lib().airice_kernel_time(name.encode(), ctypes.byref(ms), ctypes.byref(cnt),
                                    1 if reset else 0), "airice_kernel_time")
     return ms.value, cnt.value
+
+
+def table_cache_stats() -> dict:
+    """Entries of the table launch's per-grid caches on the current device
+    (airice_table_cache_stats): keys seen, filled and pinned, for the row constants and the
+    start-angle sines."""
+    out = (ctypes.c_int * 6)()
+    fn = lib().airice_table_cache_stats  # bound here: tools/ab_table.py loads older builds too
+    fn.argtypes, fn.restype = [ctypes.POINTER(ctypes.c_int)], ctypes.c_int
+    check(fn(out), "airice_table_cache_stats")
+    return {"rows": {"keys": out[0], "filled": out[1], "pinned": out[2]},
+            "angles": {"keys": out[3], "filled": out[4], "pinned": out[5]}}

@@ -30,35 +30,6 @@
 
 #include "airice_tlog.hpp"
 
-#ifndef AIRICE_LEAN_LOG
-#define AIRICE_LEAN_LOG 1
-#endif
-#ifndef AIRICE_INT_RANGE
-#define AIRICE_INT_RANGE 1
-#endif
-#ifndef AIRICE_FAST_ASIN
-#define AIRICE_FAST_ASIN 1
-#endif
-#ifndef AIRICE_FAST_FRESNEL
-#define AIRICE_FAST_FRESNEL 1
-#endif
-#ifndef AIRICE_SQRT_FIX
-#define AIRICE_SQRT_FIX 1
-#endif
-#ifndef AIRICE_RCP_NEWTON
-#define AIRICE_RCP_NEWTON 1
-#endif
-// fast_sqrt's q = 0 case without a select: v_rsq_f64(q + 2^-1074) is finite at q = 0 and the
-// added 2^-1074 leaves every q >= 2^-1020 (and every q <= 0, NaN) unchanged
-#ifndef AIRICE_SQRT_TINY
-#define AIRICE_SQRT_TINY 1
-#endif
-// log_ratio's fast-path test as two v_cmp_class (q and b positive normal) instead of the
-// integer range tests on their high words
-#ifndef AIRICE_CLASS_CHECK
-#define AIRICE_CLASS_CHECK 1
-#endif
-
 namespace airice {
 
 constexpr int kMaxLayers = 4;  // ATMLAY has 5 bounds -> at most 4 air layers
@@ -238,36 +209,22 @@ __device__ __forceinline__ void sqrt_rsqrt(double q, double& s, double& rs) {
   g = __builtin_fma(d, h, g);
   e = __builtin_fma(-h, g, 0.5);
   h = __builtin_fma(h, e, h);
-  if (AIRICE_SQRT_FIX > 1) {
-    d = __builtin_fma(-g, g, q);
-    g = __builtin_fma(d, h, g);
-  }
   s = (q == 0.0) ? q : g;
   rs = (q == 0.0) ? __builtin_inf() : 2.0 * h;
 }
 
 // sqrt(q) (same iteration, no reciprocal): within ~1 ulp; q = 0 -> 0, q < 0 / NaN -> NaN.
+// The q = 0 case needs no select: v_rsq_f64(q + 2^-1074) is finite at q = 0, and the added
+// 2^-1074 leaves every q >= 2^-1020 (and every q <= 0, NaN) unchanged.
 __device__ __forceinline__ double fast_sqrt(double q) {
-#if AIRICE_SQRT_TINY
   const double y = __builtin_amdgcn_rsq(q + 0x1p-1074);
-#else
-  const double y = __builtin_amdgcn_rsq(q);
-#endif
   double g = q * y, h = 0.5 * y;
   const double e = __builtin_fma(-h, g, 0.5);
   g = __builtin_fma(g, e, g);
   h = __builtin_fma(h, e, h);
-  double d = __builtin_fma(-g, g, q);
+  const double d = __builtin_fma(-g, g, q);
   g = __builtin_fma(d, h, g);
-  if (AIRICE_SQRT_FIX > 1) {
-    d = __builtin_fma(-g, g, q);
-    g = __builtin_fma(d, h, g);
-  }
-#if AIRICE_SQRT_TINY
   return g;  // q = 0: y finite, so g = 0 * y = 0 through every step
-#else
-  return (q == 0.0) ? q : g;
-#endif
 }
 
 // a / b for b positive and normal (2^-1000 <= b < 2^1000): v_rcp_f64 (24 bits, measured by
@@ -310,14 +267,8 @@ __device__ __forceinline__ double asin_fast(double x) {
   return __builtin_copysign(y, x);
 }
 
-// asin for the kernels' angle outputs (fast form unless AIRICE_FAST_ASIN=0)
-__device__ __forceinline__ double k_asin(double x) {
-#if AIRICE_FAST_ASIN
-  return asin_fast(x);
-#else
-  return asin(x);
-#endif
-}
+// asin for the kernels' angle outputs
+__device__ __forceinline__ double k_asin(double x) { return asin_fast(x); }
 
 __device__ __forceinline__ RayL ray_L(double A2, double L) {
   RayL r;
@@ -347,28 +298,15 @@ __device__ __forceinline__ double fast_log(double x) { return tlog(x); }
 __device__ __forceinline__ double log_ratio_fast(double a, double b, const double* tab, bool& ok) {
   double y = __builtin_amdgcn_rcp(b);
   y = __builtin_fma(y, __builtin_fma(-b, y, 1.0), y);
-  if (AIRICE_RCP_NEWTON > 1) y = __builtin_fma(y, __builtin_fma(-b, y, 1.0), y);
   const double q0 = a * y;
   const double q = __builtin_fma(__builtin_fma(-b, q0, a), y, q0);
   // a > 0 and q in range cover a (a tiny / huge / inf / NaN shows in q or in a > 0); b in range
   // keeps v_rcp_f64 and the Newton steps clear of overflow and denormals
-#if AIRICE_CLASS_CHECK
   // b and q positive normal (class mask 1 << 8): a <= 0 or NaN, b <= 0, NaN, denormal or so
   // large that v_rcp_f64 leaves the normal range, and q zero, denormal, infinite or NaN all fail;
   // with b > 0 and q > 0 also a > 0
   ok = __builtin_amdgcn_class(b, 1 << 8) && __builtin_amdgcn_class(q, 1 << 8);
-#elif AIRICE_INT_RANGE
-  // the same test on the high words: 2^-1000 <= b, q < 2^1000 as unsigned exponent ranges
-  // (a negative, zero, NaN or infinite value falls outside; a <= 0 or NaN makes q so)
-  ok = (hi_word(b) - 0x01700000u < 0x7D000000u) && (hi_word(q) - 0x01700000u < 0x7D000000u);
-#else
-  ok = a > 0.0 && b > 0x1p-1000 && b < 0x1p1000 && q > 0x1p-1000 && q < 0x1p1000;
-#endif
-#if AIRICE_LEAN_LOG
   return tlog_lean(q, tab);  // garbage, and unused, when !ok
-#else
-  return tlog_pos(q, tab);
-#endif
 }
 
 __device__ __forceinline__ double log_ratio_ieee(double a, double b) {

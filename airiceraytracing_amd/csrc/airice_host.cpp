@@ -147,7 +147,12 @@ int parse_gdas(const std::string& text, airice_medium* m) {
 
 // ---- table files (airice_table_save / _load) --------------------------------------------------
 // The header is serialised field by field at fixed offsets (little-endian host), so that struct
-// padding never reaches the file and the layout does not depend on the compiler.
+// padding never reaches the file and the layout does not depend on the compiler.  The fields and
+// columns are copied in host byte order, so the format is little-endian only because every host
+// this library builds for is: a big-endian build is refused here rather than writing files whose
+// magic and checksum would still match after a byte swap.
+static_assert(__BYTE_ORDER__ == __ORDER_LITTLE_ENDIAN__,
+              "table files are little-endian: host byte order is copied as is");
 namespace {
 
 constexpr char kTableMagic[8] = {'A', 'I', 'R', 'T', 'B', 'L', '0', '1'};

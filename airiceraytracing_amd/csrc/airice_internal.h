@@ -24,6 +24,8 @@ int launch_table(const DevMedium& M, const IceConsts& I, const airice_grid* g, i
                  int row_count, float* d_table, double* d_full, size_t ld, hipStream_t st);
 int launch_table_multi(const DevMedium& M, const IceConsts* Ih, const airice_grid* grids, int n,
                        float* const* tables, const size_t* lds, hipStream_t st);
+// entries of the table launch's per-grid caches (airice_table_cache_stats)
+void table_cache_stats(int out[6]);
 int launch_rays(const DevMedium& M, const IceConsts& I, const double* launch, const double* txh,
                 int in_ice, size_t n, double* out, size_t ld, hipStream_t st);
 int launch_solve(const DevMedium& M, const IceConsts& I, int variant, const double* txh,

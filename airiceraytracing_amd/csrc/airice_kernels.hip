@@ -33,110 +33,26 @@ namespace airice {
 
 constexpr double kSpeedC = 299792458.0;  // .h:30
 constexpr int kBlock = 256;
-// table launch shape (tuning knobs for tools/ab_table.py builds; the defaults are the measured best)
-#ifndef AIRICE_TABLE_BS
-#define AIRICE_TABLE_BS 256
-#endif
-#ifndef AIRICE_TABLE_WAVES
-#define AIRICE_TABLE_WAVES 8
-#endif
-#ifndef AIRICE_TABLE_WAVES2
-#define AIRICE_TABLE_WAVES2 7
-#endif
-constexpr int kTableBlock = AIRICE_TABLE_BS;
-// R = 2 window (rays per launch).  Measured on cfg2 (858,627 rays: 1.64 rounds of R = 1 waves,
-// one round at R = 2): 42.4 us at R = 2 against 40.1 us at R = 1 -- the single round's waves run
-// oldest-first, so the SIMDs still drain one wave at a time (tools/wave_timeline.py) -- hence the
-// window is empty by default and R = 2 is reachable only through AIRICE_TABLE_RPL=2 or building
-// with e.g. -DAIRICE_TWO_RAY_MIN=524288 -DAIRICE_TWO_RAY_MAX=917504.
-// AIRICE_TABLE_R2=0 leaves the R = 2 kernel out of the build (co-compiled template variants can
-// perturb each other's register allocation)
-#ifndef AIRICE_SCALAR_LDSLOG
-#define AIRICE_SCALAR_LDSLOG 0
-#endif
+// Table launch shape: 256-thread blocks at 8 waves/SIMD (64 VGPRs), measured best of 64 / 128 /
+// 256 / 512 threads, 7 / 8 waves and 1 / 2 rays per lane.
+constexpr int kTableBlock = 256;
+constexpr int kTableWaves = 8;
+// debug builds: shader-clock stamps of the one-query kernels (tools/scalar_stamps.py,
+// tools/ray_stamps.py) and the minimizer's evaluation counts by sorted position (tools/wave_evals.py)
 #ifndef AIRICE_SCALAR_STAMP
 #define AIRICE_SCALAR_STAMP 0
 #endif
 #ifndef AIRICE_RAY_STAMP
 #define AIRICE_RAY_STAMP 0
 #endif
-// the one-wave kernels touch their argument block's lines at entry (prefetch_kernargs)
-#ifndef AIRICE_KARG_PREFETCH
-#define AIRICE_KARG_PREFETCH 1
-#endif
-// the table lookup's minimizer fallback as one fused pass (roots_kernel<IN_CM100, 256, true>)
-#ifndef AIRICE_FALLBACK_FUSED
-#define AIRICE_FALLBACK_FUSED 1
-#endif
-#ifndef AIRICE_OVERSHOOT
-#define AIRICE_OVERSHOOT 0
-#endif
-#ifndef AIRICE_GUARD_SKIP
-#define AIRICE_GUARD_SKIP 0
-#endif
-// the per-lane root finder's evaluation-free bisection steps as selects, four per loop trip (the
-// one-query form's code) instead of a loop with a divergent exit per step
-#ifndef AIRICE_LEAN_SELECTS
-#define AIRICE_LEAN_SELECTS 1
-#endif
-// steps per trip of those selects
-#ifndef AIRICE_LEAN_UNROLL
-#define AIRICE_LEAN_UNROLL 4
-#endif
-// the root finder evaluates f(lo) and f(hi) together, before its loop (solve_root)
-#ifndef AIRICE_PAIR_ENDS
-#define AIRICE_PAIR_ENDS 1
-#endif
-// the secant search's later steps by inverse quadratic interpolation from its AIRICE_IQI-th step
-// (0: secant only; 1: from the second point on, with f(lo); 2: on three search points)
-#ifndef AIRICE_IQI
-#define AIRICE_IQI 1
-#endif
-// one phase of the root finder's state machine per loop trip (solve_root, the per-lane form)
-#ifndef AIRICE_UNIFORM_PHASE
-#define AIRICE_UNIFORM_PHASE 0
-#endif
-// ... and both guards of a lane in one pass
-// debug build (tools/solve_stats.py with a -DAIRICE_SORTED_STATS=1 library): AIRICE_SOLVE_STATS
-// keeps the batch-wide grouping and records the counts by sorted position
 #ifndef AIRICE_SORTED_STATS
 #define AIRICE_SORTED_STATS 0
 #endif
-#ifndef AIRICE_PAIR_GUARDS
-#define AIRICE_PAIR_GUARDS 0
-#endif
-// the table launch reads its rows' constants from a per-(medium, grid) device cache instead of
-// computing them in each block's prologue
-#ifndef AIRICE_ROWCONST_CACHE
-#define AIRICE_ROWCONST_CACHE 1
-#endif
-// ... and the start-angle sine of every grid column from a per-angle-grid device cache
-#ifndef AIRICE_ANGLE_CACHE
-#define AIRICE_ANGLE_CACHE 1
-#endif
-#if AIRICE_ANGLE_CACHE && !AIRICE_ROWCONST_CACHE
-#error "AIRICE_ANGLE_CACHE shares the row-constant cache's lock and capture check"
-#endif
-#ifndef AIRICE_ROWCONST_ALIGN16
-#define AIRICE_ROWCONST_ALIGN16 0
-#endif
-#ifndef AIRICE_TABLE_R2
-#define AIRICE_TABLE_R2 1
-#endif
-#ifndef AIRICE_TWO_RAY_MIN
-#define AIRICE_TWO_RAY_MIN 0
-#endif
-#ifndef AIRICE_TWO_RAY_MAX
-#define AIRICE_TWO_RAY_MAX 0
-#endif
-// table stores with an SGPR column base and a 32-bit lane byte offset (global_store saddr form):
+// evaluation-free bisection steps of the root finder per loop trip (as compare-and-select)
+constexpr int kLeanUnroll = 4;
+// table stores take an SGPR column base and a 32-bit lane byte offset (global_store saddr form):
 // launches are split at 2^30 rays so that 4 k < 2^32
-#ifndef AIRICE_SADDR_STORE
-#define AIRICE_SADDR_STORE 1
-#endif
-constexpr long long kMaxLaunchRays = AIRICE_SADDR_STORE ? (1LL << 30) : (1LL << 31);
-constexpr int kTwoRayMin = AIRICE_TWO_RAY_MIN;
-constexpr int kTwoRayMax = AIRICE_TWO_RAY_MAX;
+constexpr long long kMaxLaunchRays = 1LL << 30;
 
 // ---------------------------------------------------------------------------
 // Forward ray: GetRayTracingSolutions (.cc:1796-2017).  d[] = dummy[0..17].
@@ -162,19 +78,11 @@ __device__ __forceinline__ void fresnel_from_sine(double n1, double n2, double r
   const double sqterm = fast_sqrt(1 - a * a);
   double num = n1 * ct - n2 * sqterm;
   double den = n1 * ct + n2 * sqterm;
-#if AIRICE_FAST_FRESNEL
   tS = 1 + div_pos(num, den);
-#else
-  tS = 1 + (num / den);
-#endif
   if (isnan(tS)) tS = 0;
   num = n1 * sqterm - n2 * ct;
   den = n1 * sqterm + n2 * ct;
-#if AIRICE_FAST_FRESNEL
   tP = (1 - div_pos(num, den)) * ratio;
-#else
-  tP = (1 - (num / den)) * ratio;
-#endif
   if (isnan(tP)) tP = 0;
 }
 
@@ -198,11 +106,7 @@ __device__ __forceinline__ TopEnd topend_of(const IceConsts& I, int top) {
 // Everything of a ray that depends on its Tx height only: the Tx layer and the Tx layer's
 // segment folded like the lower layers' (Tx endpoint -> the layer's stop end, or the ice).  The
 // table computes it once per row into LDS (a block spans few rows); other launches per lane.
-struct
-#if AIRICE_ROWCONST_ALIGN16
-__attribute__((aligned(16)))
-#endif
-RowConst {
+struct RowConst {
   SegConst seg;  // Tx endpoint -> stop end of the Tx layer (zero-length case resolved)
   double H;
   int top;       // MaxLayers - SkipLayersAbove - 1
@@ -253,26 +157,6 @@ __device__ __forceinline__ double sin_start(double x) {
   return __builtin_fma(x * x2, p, x);
 }
 
-// Wave priority = segments still to trace (capped at 3), lowered at each segment boundary of the
-// table kernel: the arbiter issues from the highest-priority ready wave (oldest first among
-// equals), so waves that are behind catch up and the SIMD keeps many waves until the end instead
-// of running its youngest waves alone (latency-bound) at the tail.  rem must be wave-uniform.
-#ifndef AIRICE_TABLE_PRIO
-#define AIRICE_TABLE_PRIO 0
-#endif
-__device__ __forceinline__ void prio_remaining(bool on, int rem) {
-  if (!on) return;
-  rem = __builtin_amdgcn_readfirstlane(rem);
-  if (rem >= 3)
-    __builtin_amdgcn_s_setprio(3);
-  else if (rem == 2)
-    __builtin_amdgcn_s_setprio(2);
-  else if (rem == 1)
-    __builtin_amdgcn_s_setprio(1);
-  else
-    __builtin_amdgcn_s_setprio(0);
-}
-
 // I.lower[il].ratio for a lane-varying il (selects)
 __device__ __forceinline__ double sel_lower_ratio(const IceConsts& I, int il) {
   double r = I.lower[0].ratio;
@@ -291,10 +175,8 @@ __device__ __forceinline__ void ray_solution_row(const DevMedium& M, const IceCo
                                                  const RowConst& rc, double theta, bool in_ice,
                                                  double* d, bool want_inc,
                                                  const double* tab = &kLogTable[0][0],
-                                                 int top_hi = -1, int prio_after = -1,
+                                                 int top_hi = -1,
                                                  const double* v_start = nullptr) {
-  // prio_after >= 0: table launch; segments of later rays of this lane still to come
-  const bool prio = AIRICE_TABLE_PRIO && prio_after >= 0;
   const double H = rc.H;
   const int top = rc.top;
   const int bot = I.bot;
@@ -312,7 +194,6 @@ __device__ __forceinline__ void ray_solution_row(const DevMedium& M, const IceCo
   }
   // lower layers: both ends folded on the host (I.lower, scalar reads)
   if (top_hi >= 0) {
-    prio_remaining(prio, prio_after + (top_hi - bot) + (in_ice ? 1 : 0));
 #pragma clang loop unroll(disable)
     for (int il = top_hi - 1; il >= bot; --il) {
       if (il < top) {
@@ -322,7 +203,6 @@ __device__ __forceinline__ void ray_solution_row(const DevMedium& M, const IceCo
         t_air += s.t;
         geo_air += s.geo;
       }
-      prio_remaining(prio, prio_after + (il - bot) + (in_ice ? 1 : 0));
     }
   } else {
 #pragma unroll
@@ -349,7 +229,6 @@ __device__ __forceinline__ void ray_solution_row(const DevMedium& M, const IceCo
     t_ice += s.t;
     geo_ice += s.geo;
     recv_ice = k_asin(v2) * M.r2d;
-    prio_remaining(prio, prio_after);
   }
   double tS, tP;
   fresnel_from_sine(I.n_air_ice, I.n_ice0, I.n_ratio, vinc, tS, tP);
@@ -391,9 +270,10 @@ struct TableArgs {
   int rows_per_block; // LDS rows a block's set of rays may span
   int half;           // rays per set (R = 2: ceil(n / 2); R = 1: n)
   size_t ld;
-  const struct RowConst* rc;  // AIRICE_ROWCONST_CACHE: the grid's row constants (all hsteps
-                              // rows, computed once per medium and grid), else nullptr
-  const double* vs;           // AIRICE_ANGLE_CACHE: sin of the start angle of every column
+  const struct RowConst* rc;  // the grid's row constants (all hsteps rows, computed once per
+                              // medium and grid: row_consts_cached), or nullptr
+  const double* vs;           // sin of the start angle of every column (angle_sines_cached), or
+                              // nullptr
 };
 
 // Debug timeline (AIRICE_TABLE_TRACE=<file>, tools/wave_timeline.py): per wave, the 100 MHz
@@ -431,11 +311,10 @@ __device__ __forceinline__ double table_angle(const TableArgs& G, int iang) {
 __device__ __forceinline__ void table_ray(const DevMedium& M, const IceConsts& I,
                                           const TableArgs& G, const RowConst& rc, int r, int k,
                                           float* __restrict__ table, double* __restrict__ full,
-                                          const double* tab, int top_hi, int prio_after) {
+                                          const double* tab, int top_hi) {
   const int iang = k - r * G.asteps;
   const double th = table_angle(G, iang);
   double d[18];
-#if AIRICE_ANGLE_CACHE
   // the start-angle sine of every grid column, formed once per angle grid (angle_sines_kernel);
   // launches captured into a graph before their grid was cached form it here
   double vs;
@@ -443,13 +322,8 @@ __device__ __forceinline__ void table_ray(const DevMedium& M, const IceConsts& I
     vs = G.vs[iang];
   else
     vs = sin_start((180 - th) * M.d2r);
-  ray_solution_row(M, I, rc, th, G.in_ice != 0, d, full != nullptr, tab, top_hi, prio_after,
-                   &vs);
-#else
-  ray_solution_row(M, I, rc, th, G.in_ice != 0, d, full != nullptr, tab, top_hi, prio_after);
-#endif
+  ray_solution_row(M, I, rc, th, G.in_ice != 0, d, full != nullptr, tab, top_hi, &vs);
   const size_t ld = G.ld;
-#if AIRICE_SADDR_STORE
   // AllTableAllAntData columns (.cc:2101-2111): the column base is wave-uniform, the lane's byte
   // offset fits 32 bits (k < 2^30 per launch)
   {
@@ -469,45 +343,28 @@ __device__ __forceinline__ void table_ray(const DevMedium& M, const IceConsts& I
     st(9, d[17]);
     st(10, d[13]);
   }
-  if (false)
-#endif
-  {
-  // AllTableAllAntData columns (.cc:2101-2111)
-  table[0 * ld + k] = (float)d[1];
-  table[1 * ld + k] = (float)d[2];
-  table[2 * ld + k] = (float)d[7];
-  table[3 * ld + k] = (float)d[6];
-  table[4 * ld + k] = (float)d[11];
-  table[5 * ld + k] = (float)d[3];
-  table[6 * ld + k] = (float)d[14];
-  table[7 * ld + k] = (float)d[15];
-  table[8 * ld + k] = (float)d[16];
-  table[9 * ld + k] = (float)d[17];
-  table[10 * ld + k] = (float)d[13];
-  }
   if (full != nullptr) {
 #pragma unroll
     for (int c = 0; c < 18; ++c) full[c * ld + k] = d[c];
   }
 }
 
-// Table launch: R rays per lane, ray k of set j = k0 + j * G.half + threadIdx.x (each set a
-// contiguous range, so every column store of a wave stays one 256 B segment).  The block first
-// evaluates the Tx-height-only constants of the (few) rows each set spans into LDS -- one lane per
-// row, so the exp / layer scans / top-layer folding run once per row instead of once per wave --
-// then every lane traces its rays one after the other.  R = 2 was built for grids that need about
-// 1.6 rounds of resident waves at R = 1 (BASELINE cfg2), so that the whole grid is resident at
-// once; it measured slower (kTwoRayMin/kTwoRayMax above) and is off by default.
-// (Persistent grid-stride and atomic-chunk schedules were measured and rejected: the loop around
-// the inlined ray body raises register pressure to 160 VGPRs, or 330 B/lane of scratch when capped
-// at 64, and runs 2.7x / 7x slower; the R copies here are straight-line code.)
-// The work of one table block (BS rays of one antenna's grid), shared by the single- and the
-// multi-antenna kernels.
-template <int BS, int R, bool TRACE>
+// Table launch: one ray per lane, ray k = block * 256 + threadIdx.x (each wave's column store one
+// contiguous 256 B segment).  The block first stages the Tx-height-only constants of the (few) rows
+// it spans into LDS -- copied from the grid's row-constant cache, or, when the launch has none, one
+// lane per row computes them, so the exp / layer scans / top-layer folding run once per row
+// instead of once per wave -- then every lane traces its ray.
+// (Measured and rejected, DESIGN.md §5: persistent grid-stride and atomic-chunk schedules -- the
+// loop around the inlined ray body raises register pressure to 160 VGPRs, or 330 B/lane of scratch
+// when capped at 64, and runs 2.7x / 7x slower -- and two rays per lane.)
+// The work of one table block (kTableBlock rays of one antenna's grid), shared by the single- and
+// the multi-antenna kernels.
+template <bool TRACE>
 __device__ __forceinline__ void table_block(const DevMedium& M, const IceConsts& I,
                                             const TableArgs& G, float* __restrict__ table,
                                             double* __restrict__ full,
                                             WaveTrace* __restrict__ trace, unsigned block) {
+  constexpr int BS = kTableBlock;
   extern __shared__ __align__(16) unsigned char smem[];
   RowConst* rows = reinterpret_cast<RowConst*>(smem);
   // the log table (16 B x 2^kLogTableBits) staged in LDS: 16-byte entries, (1 << kLogTableBits) / BS per thread
@@ -524,37 +381,24 @@ __device__ __forceinline__ void table_block(const DevMedium& M, const IceConsts&
     trace[wave].c0 = __builtin_amdgcn_s_memtime();
   }
   const int k0 = (int)block * BS;
-  int r0[R];
-#pragma unroll
-  for (int j = 0; j < R; ++j) {
-    const int kb = k0 + j * G.half;                        // first ray of set j
-    const int ke = min(kb + BS, j + 1 < R ? G.half + j * G.half : G.n);  // end of set j
-    r0[j] = kb < ke ? ray_row(G, kb) : 0;
-    const int nrows = kb < ke ? ray_row(G, ke - 1) - r0[j] + 1 : 0;
+  const int ke = min(k0 + BS, G.n);  // end of this block's rays
+  const int r0 = k0 < ke ? ray_row(G, k0) : 0;
+  {
+    const int nrows = k0 < ke ? ray_row(G, ke - 1) - r0 + 1 : 0;
     for (int t = threadIdx.x; t < nrows; t += BS)
-#if AIRICE_ROWCONST_CACHE
-      rows[j * G.rows_per_block + t] = G.rc != nullptr ? G.rc[G.row0 + r0[j] + t]
-                                                       : row_const(M, I, row_height(G, G.row0 + r0[j] + t));
-#else
-      rows[j * G.rows_per_block + t] = row_const(M, I, row_height(G, G.row0 + r0[j] + t));
-#endif
+      rows[t] = G.rc != nullptr ? G.rc[G.row0 + r0 + t]
+                                : row_const(M, I, row_height(G, G.row0 + r0 + t));
   }
   __syncthreads();
-  prio_remaining(AIRICE_TABLE_PRIO, 3);
-#pragma unroll
-  for (int j = 0; j < R; ++j) {
-    const int k = k0 + j * G.half + (int)threadIdx.x;
-    const int ke = j + 1 < R ? G.half + j * G.half : G.n;
-    if (k0 + j * G.half >= ke) break;  // block-uniform: set j of this block is empty
-    // the set's first row has the highest Tx, so its Tx layer bounds every lane's (top_layer is
+  const int k = k0 + (int)threadIdx.x;
+  if (k0 < G.n) {  // block-uniform
+    // the block's first row has the highest Tx, so its Tx layer bounds every lane's (top_layer is
     // monotone in the height)
-    const int top_hi = __builtin_amdgcn_readfirstlane(rows[j * G.rows_per_block].top);
+    const int top_hi = __builtin_amdgcn_readfirstlane(rows[0].top);
     __builtin_assume(top_hi >= 0);
-    if (k < ke) {
+    if (k < G.n) {
       const int r = ray_row(G, k);
-      // later rays of the lane: ~4 segments each
-      table_ray(M, I, G, rows[j * G.rows_per_block + (r - r0[j])], r, k, table, full,
-                &s_logtab[0][0], top_hi, 4 * (R - 1 - j));
+      table_ray(M, I, G, rows[r - r0], r, k, table, full, &s_logtab[0][0], top_hi);
     }
   }
   if (TRACE && lane == 0) {
@@ -565,15 +409,14 @@ __device__ __forceinline__ void table_block(const DevMedium& M, const IceConsts&
   }
 }
 
-template <int BS, int R, bool TRACE = false>
-// waves_per_eu(8) at R = 1: 64 VGPRs (12 B/lane spilled) at 8 waves/SIMD measured on par or
-// slightly ahead of 67 VGPRs at 7 (bench 42.0 vs 42.9 us for cfg2).  R = 2 needs <= 7 waves/SIMD.
-__global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(R == 1 ? AIRICE_TABLE_WAVES : AIRICE_TABLE_WAVES2, R == 1 ? AIRICE_TABLE_WAVES : AIRICE_TABLE_WAVES2))) void table_kernel(
+// waves_per_eu(8): 64 VGPRs at 8 waves/SIMD, measured on par or slightly ahead of 67 VGPRs at 7.
+template <bool TRACE = false>
+__global__ __launch_bounds__(kTableBlock) __attribute__((amdgpu_waves_per_eu(kTableWaves, kTableWaves))) void table_kernel(
                                                    DevMedium M, IceConsts I, TableArgs G,
                                                    float* __restrict__ table,
                                                    double* __restrict__ full,
                                                    WaveTrace* __restrict__ trace) {
-  table_block<BS, R, TRACE>(M, I, G, table, full, trace, blockIdx.x);
+  table_block<TRACE>(M, I, G, table, full, trace, blockIdx.x);
 }
 
 // Several antennas' tables in one grid (airice_table_launch_multi): the blocks of antenna a are
@@ -587,17 +430,16 @@ struct MultiMap {
   float* table[kMaxAntennas];
 };
 
-template <int BS>
-__global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(AIRICE_TABLE_WAVES, AIRICE_TABLE_WAVES))) void table_multi_kernel(
+__global__ __launch_bounds__(kTableBlock) __attribute__((amdgpu_waves_per_eu(kTableWaves, kTableWaves))) void table_multi_kernel(
     DevMedium M, const IceConsts* __restrict__ Iv, const TableArgs* __restrict__ Gv, MultiMap map) {
   int a = 0;
   for (int j = 1; j < map.n_ant; ++j) a += (int)blockIdx.x >= map.begin[j];
   a = __builtin_amdgcn_readfirstlane(a);
-  table_block<BS, 1, false>(M, Iv[a], Gv[a], map.table[a], nullptr, nullptr,
-                            blockIdx.x - (unsigned)map.begin[a]);
+  table_block<false>(M, Iv[a], Gv[a], map.table[a], nullptr, nullptr,
+                     blockIdx.x - (unsigned)map.begin[a]);
 }
 
-// Row constants of a whole grid (AIRICE_ROWCONST_CACHE): one row per lane, the table block's own
+// Row constants of a whole grid (row_consts_cached): one row per lane, the table block's own
 // row_const on the same heights, so the cached values are the bits the block would compute.
 __global__ __launch_bounds__(256) void rowconst_kernel(DevMedium M, IceConsts I, TableArgs G,
                                                        RowConst* __restrict__ out) {
@@ -605,7 +447,7 @@ __global__ __launch_bounds__(256) void rowconst_kernel(DevMedium M, IceConsts I,
   if (r < G.hsteps) out[r] = row_const(M, I, row_height(G, r));
 }
 
-// Start-angle sines of a grid's columns (AIRICE_ANGLE_CACHE): the table ray's own expression.
+// Start-angle sines of a grid's columns (angle_sines_cached): the table ray's own expression.
 __global__ __launch_bounds__(256) void angle_sines_kernel(DevMedium M, TableArgs G,
                                                           double* __restrict__ out) {
   const int a = (int)(blockIdx.x * 256 + threadIdx.x);
@@ -747,9 +589,7 @@ __global__ __launch_bounds__(64) void scalar_ray_kernel(DevMedium M, IceConsts I
                                                         const double* __restrict__ txh, int in_ice,
                                                         double* __restrict__ out, size_t ld,
                                                         Signal sig) {
-#if AIRICE_KARG_PREFETCH
   prefetch_kernargs<sizeof(DevMedium) + sizeof(IceConsts)>();
-#endif
   unsigned long long ts[6] = {0, 0, 0, 0, 0, 0};
 #if AIRICE_RAY_STAMP
   // debug: shader-clock stamps (entry, row constants, sine chain, segment, sums, stores) in
@@ -1197,11 +1037,9 @@ __device__ __forceinline__ SolveResult solve_root(const DevMedium& M, const IceC
   // linear (a straight ray's is exactly H u; single precision is plenty for a first guess), then
   // secant steps in theta on the last two points (x1, f1), (x2, f2)
   double x1 = 0.0, f1 = 0.0, x2 = 0.0, f2 = 0.0;
-#if AIRICE_IQI
-  // the point before (x1, f1): the search steps by inverse quadratic interpolation on the last
-  // three points (the secant step plus a curvature term) once it has three
+  // the point before (x1, f1): from the second search point on the search steps by inverse
+  // quadratic interpolation on the last three points (the secant step plus a curvature term)
   double x0 = 0.0, f0 = 0.0;
-#endif
   // PH_G1/G2: guards at x2 -/+ dlt, where x2 is the secant search's last point (it stays put after
   // the search) and dlt lives in x1 (dead once the search ends)
   double& dlt = x1;
@@ -1211,9 +1049,6 @@ __device__ __forceinline__ SolveResult solve_root(const DevMedium& M, const IceC
   // bits, two sequential evaluations fewer)
   bool have_next = false;
   double next_air = 0.0, next_ice = 0.0;
-#if AIRICE_PAIR_GUARDS
-  double f_g2 = 0.0;  // f at the second guard, from the first guard's trip
-#endif
   auto guard = [&](double x, double f) {
     if (!(fabs(f) >= tau) || !(x > gL && x < gR)) return;
     if ((f < 0.0) == (fL < 0.0)) {
@@ -1263,10 +1098,8 @@ __device__ __forceinline__ SolveResult solve_root(const DevMedium& M, const IceC
             const float un = uh - (float)fR * ((uh - ul) / (float)(fR - fL));
             x1 = hi;
             f1 = fR;
-#if AIRICE_IQI
             x0 = lo;
             f0 = fL;
-#endif
             x2 = 180 - (double)atanf(un) * M.r2d;  // first guess, evaluated first
             phase = PH_EST;
           }
@@ -1274,7 +1107,6 @@ __device__ __forceinline__ SolveResult solve_root(const DevMedium& M, const IceC
       }
     }
   };
-#if AIRICE_PAIR_ENDS
   if constexpr (!WAVE) {
     // f(lo) and f(hi) in one pass (eval_thd2: two independent chains per lane, ~1.3x the time of
     // one evaluation instead of 2x) before the loop, so that the loop carries no extra state; the
@@ -1294,7 +1126,6 @@ __device__ __forceinline__ SolveResult solve_root(const DevMedium& M, const IceC
       }
     }
   }
-#endif
 #if AIRICE_SCALAR_STAMP
   const int t_setup = (int)(__builtin_amdgcn_s_memtime() - ts0) + (int)(0.0 * (lo + hi));
 #endif
@@ -1310,23 +1141,6 @@ __device__ __forceinline__ SolveResult solve_root(const DevMedium& M, const IceC
       est = __builtin_amdgcn_readfirstlane(est);
       iter = __builtin_amdgcn_readfirstlane(iter);
     }
-#if AIRICE_UNIFORM_PHASE
-    if constexpr (!WAVE) {
-      // one phase per trip: the wave's lowest phase (a lane's phase never decreases), the lanes in
-      // other phases idle under EXEC, so each trip runs one phase body instead of every body some
-      // lane is in.  A lane's own sequence of points and updates is unchanged.  Probing lanes
-      // (up to ~300 steps) always take part, so that the others do not wait for them.
-      int ph = PH_BISECT;
-#pragma unroll
-      for (int p = PH_FLO; p < PH_BISECT; ++p) {
-        if (__ballot(phase == p) != 0) {
-          ph = p;
-          break;
-        }
-      }
-      if (phase != ph && phase != PH_PROBE) continue;
-    }
-#endif
     if (phase == PH_BISECT) {
       // steps that need no evaluation: an exact zero at a bracket end (GSL returns that end),
       // or a midpoint inside a guard region, whose sign is the region's: lo (left) or hi
@@ -1348,13 +1162,13 @@ __device__ __forceinline__ SolveResult solve_root(const DevMedium& M, const IceC
         const double gl = okL ? gL : -1.0, gr = okR ? gR : __builtin_inf();
         const double lo0 = lo, hi0 = hi;
         bool done = false;
-        if constexpr (WAVE || AIRICE_LEAN_SELECTS) {
-          // one query per wave: the same steps as selects, four per trip, so that the chain is
-          // midpoint -> compare -> select without a branch per step
+        {
+          // the steps as selects, four per trip, so that the chain is midpoint -> compare ->
+          // select without a divergent exit per step
           bool stop = false;
           while (!stop) {
 #pragma unroll
-            for (int u = 0; u < AIRICE_LEAN_UNROLL; ++u) {
+            for (int u = 0; u < kLeanUnroll; ++u) {
               const double xm = (lo + hi) / 2.0;
               const bool inL = xm <= gl, inR = !inL && xm >= gr;
               const bool mv = !stop && (inL || inR);  // otherwise: evaluate this midpoint
@@ -1366,20 +1180,6 @@ __device__ __forceinline__ SolveResult solve_root(const DevMedium& M, const IceC
               status = (fin && cont) ? (status | AIRICE_SOLVE_MAXITER) : status;
               done = done || fin;
               stop = stop || !mv || fin;
-            }
-          }
-        } else {
-          for (;;) {
-            const double xm = (lo + hi) / 2.0;
-            if (xm <= gl) lo = xm;
-            else if (xm >= gr) hi = xm;
-            else break;
-            ++iter;
-            const bool cont = !(fabs(hi - lo) < 0 + tol * lo);
-            if (!cont || iter == 40) {
-              if (cont) status |= AIRICE_SOLVE_MAXITER;
-              done = true;
-              break;
             }
           }
         }
@@ -1400,25 +1200,14 @@ __device__ __forceinline__ SolveResult solve_root(const DevMedium& M, const IceC
       // the secant point only steers the search (the root comes from GSL's bisection replay), so
       // its quotient takes v_rcp_f64 (~2^-24 relative) instead of the IEEE division
       x = (est == 0) ? x2 : x2 - f2 * ((x2 - x1) * __builtin_amdgcn_rcp(f2 - f1));
-#if AIRICE_IQI
       // theta(f) through (x0, f0), (x1, f1), (x2, f2) in Newton form, at f = 0: the secant step
       // minus f1 f2 times the second divided difference (the search only steers; a point outside
       // the guards falls back to their midpoint below)
-      if (est >= AIRICE_IQI) {
+      if (est >= 1) {
         const double d1 = (x2 - x1) * __builtin_amdgcn_rcp(f2 - f1);
         const double d0 = (x1 - x0) * __builtin_amdgcn_rcp(f1 - f0);
         x += f1 * f2 * ((d1 - d0) * __builtin_amdgcn_rcp(f2 - f0));
       }
-#endif
-#if AIRICE_OVERSHOOT
-      // near convergence (the step is under a quarter of GSL's final bracket width W and x2 is
-      // a guard), aim W/8 past the predicted root: the new point and x2 then straddle the root
-      // within W/2, which ends the search without the two guard evaluations below
-      if (est > 0 && fabs(f2) >= tau) {
-        const double W = 1e-9 * gL, step = x - x2;
-        if (fabs(step) < 0.25 * W) x += __builtin_copysign(0.125 * W, step);
-      }
-#endif
       if (!(x > gL && x < gR)) x = 0.5 * (gL + gR);  // safeguard: the guards' midpoint
     } else if (phase == PH_G1) {
       x = x2 - dlt;
@@ -1439,7 +1228,7 @@ __device__ __forceinline__ SolveResult solve_root(const DevMedium& M, const IceC
       } else {
         // the point the next trip evaluates when this one is f(lo) (then f(hi)) or the first guard
         // (then always the second: PH_G1 -> PH_G2)
-        const bool pair = phase == PH_FLO || (phase == PH_G1 && !AIRICE_GUARD_SKIP);
+        const bool pair = phase == PH_FLO || phase == PH_G1;
         const double xb = phase == PH_FLO ? hi : x2 + dlt;
 #if AIRICE_SCALAR_STAMP
         const unsigned long long e0 = __builtin_amdgcn_s_memtime();
@@ -1454,15 +1243,6 @@ __device__ __forceinline__ SolveResult solve_root(const DevMedium& M, const IceC
         have_next = pair;
       }
     } else {
-#if AIRICE_PAIR_GUARDS
-      // a wave with lanes at their first guard evaluates both guards of those lanes in one
-      // interleaved pass (the second, x2 + dlt, is consumed in this trip's update)
-      if (__ballot(phase == PH_G1) != 0) {
-        double air_b, ice_b;
-        eval_thd2(M, I, q, x, phase == PH_G1 ? x2 + dlt : x, tab, thd_air, thd_ice, air_b, ice_b);
-        f_g2 = (q.dist - (ice_b + air_b));
-      } else
-#endif
       {
         double L;
         thd_air = air_thd(M, q, x, L, tab);
@@ -1500,10 +1280,8 @@ __device__ __forceinline__ SolveResult solve_root(const DevMedium& M, const IceC
       on_fhi(f);
     } else if (phase == PH_EST) {
       if (est > 0) {
-#if AIRICE_IQI
         x0 = x1;
         f0 = f1;
-#endif
         x1 = x2;
         f1 = f2;
       }
@@ -1514,31 +1292,19 @@ __device__ __forceinline__ SolveResult solve_root(const DevMedium& M, const IceC
         phase = PH_BISECT;
       } else if (fabs(f) < tau) {
         // at the root: guards a few tau either side, scaled by the local secant slope; a side
-        // whose guard already lies within W/4 of the root needs none
+        // whose guard already lies at the root needs none
         dlt = 4.0 * tau * fabs((x2 - x1) * __builtin_amdgcn_rcp(f2 - f1));
-        const double Wq = AIRICE_GUARD_SKIP ? 0.25e-9 * gL : 0.0;
+        const double Wq = 0.0;
         const bool needL = !(x2 - gL <= Wq), needR = !(gR - x2 <= Wq);
         phase = (dlt > 0.0 && dlt < (gR - gL)) ? (needL ? PH_G1 : (needR ? PH_G2 : PH_BISECT))
                                                : PH_BISECT;
       } else {
         guard(x, f);
         if (est >= 12) phase = PH_BISECT;
-#if AIRICE_GUARD_SKIP
-        // guards on both sides within W/2: the bisection evaluates at most ~1 midpoint
-        if (gR - gL <= 0.5e-9 * gL) phase = PH_BISECT;
-#endif
       }
     } else if (phase == PH_G1 || phase == PH_G2) {
       if (isfinite(f)) guard(x, f);
-      phase = (phase == PH_G1 && !(AIRICE_GUARD_SKIP && gR - x2 <= 0.25e-9 * gL)) ? PH_G2
-                                                                               : PH_BISECT;
-#if AIRICE_PAIR_GUARDS
-      if (!WAVE && phase == PH_G2) {  // the second guard, evaluated with the first
-        ++n_eval;
-        if (isfinite(f_g2)) guard(x2 + dlt, f_g2);
-        phase = PH_BISECT;
-      }
-#endif
+      phase = phase == PH_G1 ? PH_G2 : PH_BISECT;
     } else {  // PH_BISECT: gsl_root_fsolver_iterate at a midpoint between the guards
       if (!exact && isfinite(f)) guard(x, f);
       ++iter;
@@ -1822,36 +1588,12 @@ static inline int bisect_exact() {
 constexpr int kSortBuckets = 16;
 // 1024 queries per block: larger groups sort better, and a 16-wave block runs at 4 waves/SIMD
 // (128 VGPRs, some spilled) -- measured faster than 256 (3 waves, no spills), 512 and 768.
-#ifndef AIRICE_ROOTS_BS
-#define AIRICE_ROOTS_BS 1024
-#endif
-constexpr int kRootsBlock = AIRICE_ROOTS_BS;
-#ifndef AIRICE_ROOTS_WAVES
-#define AIRICE_ROOTS_WAVES 4
-#endif
-// batch-wide grouping: batches of at least AIRICE_GROUP_MIN queries (0: never) are sorted across
-// the whole batch and solved in AIRICE_SORTED_BS-thread blocks (roots_sorted_kernel)
-#ifndef AIRICE_GROUP_MIN
-#define AIRICE_GROUP_MIN 65536
-#endif
-#ifndef AIRICE_SORTED_BS
-#define AIRICE_SORTED_BS 256
-#endif
-#ifndef AIRICE_GROUP_BUCKETS
-#define AIRICE_GROUP_BUCKETS 8
-#endif
-#ifndef AIRICE_GROUP_HBINS
-#define AIRICE_GROUP_HBINS 1
-#endif
-#ifndef AIRICE_GROUP_ITEMS
-#define AIRICE_GROUP_ITEMS 2
-#endif
-#ifndef AIRICE_GROUP_THREADS
-#define AIRICE_GROUP_THREADS 1024
-#endif
-#ifndef AIRICE_SORTED_WAVES
-#define AIRICE_SORTED_WAVES AIRICE_ROOTS_WAVES
-#endif
+constexpr int kRootsBlock = 1024;
+constexpr int kRootsWaves = 4;  // 127 VGPRs: 4 waves/SIMD (5 and 6 spill and run slower)
+// batch-wide grouping: batches of at least kGroupMin queries (AIRICE_GROUP_MIN in the environment
+// overrides it; 0: never) are sorted across the whole batch and solved in kSortedBlock-thread
+// blocks (roots_sorted_kernel)
+constexpr long long kGroupMin = 65536;
 
 // Stage 2 of the lookup fallback with the root handed over in registers (roots_kernel<IN_CM100>,
 // fused): defined below.
@@ -1865,7 +1607,7 @@ __device__ __forceinline__ void fallback_out_direct(const DevMedium& M, const Ic
 // fill more, shorter-lived blocks, all resident at once).  FUSED (IN_CM100 only): the block also
 // runs the fallback's stage 2 for its lanes, with the root in registers (out / ld / ok).
 template <int IN, int BS = kRootsBlock, bool FUSED = false>
-__global__ __launch_bounds__(BS, AIRICE_ROOTS_WAVES) void roots_kernel(DevMedium M, IceConsts I,
+__global__ __launch_bounds__(BS, kRootsWaves) void roots_kernel(DevMedium M, IceConsts I,
                                                                        QueryArgs Q, Park park,
                                                                        double* __restrict__ out,
                                                                        size_t ld,
@@ -1932,19 +1674,16 @@ __global__ __launch_bounds__(BS, AIRICE_ROOTS_WAVES) void roots_kernel(DevMedium
 // queries in that order in small blocks that the CU replaces independently.  Each query is still
 // solved on its own and written by its index: results are identical either way.
 // ---------------------------------------------------------------------------
-constexpr int kGroupAngles = AIRICE_GROUP_BUCKETS;   // straight-line-angle classes
-// AIRICE_GROUP_BY_SPAN: the classes within each angle class are the number of air layers the path
-// spans (0-3+): a wave then runs only the middle-layer segments its own queries have
-#ifndef AIRICE_GROUP_BY_SPAN
-#define AIRICE_GROUP_BY_SPAN 1
-#endif
-constexpr int kGroupHeights = AIRICE_GROUP_BY_SPAN ? 4 : AIRICE_GROUP_HBINS;  // classes within each
+constexpr int kGroupAngles = 8;   // straight-line-angle classes (16 measured +0.4 %)
+// the classes within each angle class are the number of air layers the path spans (0-3+): a wave
+// then runs only the middle-layer segments its own queries have
+constexpr int kGroupHeights = 4;  // classes within each
 constexpr int kGroupBuckets = kGroupAngles * kGroupHeights;
-constexpr int kGroupItems = AIRICE_GROUP_ITEMS;  // queries per thread in the sort passes
-constexpr int kGroupThreads = AIRICE_GROUP_THREADS;  // threads per block of the sort passes
+constexpr int kGroupItems = 2;  // queries per thread in the sort passes
+constexpr int kGroupThreads = 1024;  // threads per block of the sort passes
 constexpr int kGroupChunk = kGroupThreads * kGroupItems;  // queries per block and round
 constexpr int kGroupBlocks = 512;                     // blocks of the sort passes (at most)
-constexpr int kSortedBlock = AIRICE_SORTED_BS;
+constexpr int kSortedBlock = 256;
 
 // The sort key is roots_kernel's straight-line-angle bucket, b = floor((thR - 90) * B / 90) with
 // thR = 180 - atan(x) deg, x = D / (H - ice - depth), evaluated without the atan: b >= j exactly
@@ -1968,14 +1707,8 @@ __device__ __forceinline__ int query_bucket(const DevMedium& M, const QueryArgs&
 #pragma unroll
     for (int j = 0; j < kGroupAngles - 1; ++j) b += (g.D <= K.t[j] * den) ? 1 : 0;
   }
-  if (AIRICE_GROUP_BY_SPAN) {
-    const int span = top_layer(M, g.H) - bottom_layer(M, g.ice);
-    b = b * kGroupHeights + (span < 0 ? 0 : (span > 3 ? 3 : span));
-  } else if (kGroupHeights > 1) {  // Tx height between the ice and the top of the atmosphere
-    const double h = (g.H - g.ice) / (M.atm[kMaxLayers] - g.ice) * kGroupHeights;
-    b = b * kGroupHeights + ((h > 0) ? ((h < kGroupHeights) ? (int)h : kGroupHeights - 1) : 0);
-  }
-  return b;
+  const int span = top_layer(M, g.H) - bottom_layer(M, g.ice);
+  return b * kGroupHeights + (span < 0 ? 0 : (span > 3 ? 3 : span));
 }
 
 // Pass 1: the key of every query and each block's bucket counts, bucket-major:
@@ -2077,7 +1810,7 @@ __global__ __launch_bounds__(kGroupThreads) void group_scatter_kernel(
 }
 
 template <int IN>
-__global__ __launch_bounds__(kSortedBlock, AIRICE_SORTED_WAVES) void roots_sorted_kernel(
+__global__ __launch_bounds__(kSortedBlock, kRootsWaves) void roots_sorted_kernel(
     DevMedium M, IceConsts I, QueryArgs Q, Park park, const QueryRec* __restrict__ recs,
     double2* __restrict__ sorted_park, const int* __restrict__ grouped) {
   __shared__ __align__(16) double s_logtab[1 << kLogTableBits][2];
@@ -2138,18 +1871,8 @@ __device__ __forceinline__ void stage_log_table(double (*s)[2]) {
 // and the one-query fused kernel (scalar_solve_kernel).
 // WAVE (one-query kernel): every lane runs the body with the root in wr; evaluate_root_wave
 // spreads the evaluation over the wave and lane 0 writes the outputs.
-// Stage-2 output stores: written once and not read back by the kernel (AIRICE_NT_OUT: as
-// non-temporal stores)
-#ifndef AIRICE_NT_OUT
-#define AIRICE_NT_OUT 0
-#endif
-__device__ __forceinline__ void put_out(double* p, double v) {
-#if AIRICE_NT_OUT
-  __builtin_nontemporal_store(v, p);
-#else
-  *p = v;
-#endif
-}
+// Stage-2 output stores (non-temporal stores measured no faster)
+__device__ __forceinline__ void put_out(double* p, double v) { *p = v; }
 
 template <int VARIANT, bool WAVE = false>
 __device__ __forceinline__ void solve_out_body(const DevMedium& M, const IceConsts& I,
@@ -2196,16 +1919,10 @@ __device__ __forceinline__ void solve_out_body(const DevMedium& M, const IceCons
   if (status != nullptr) status[k] = (uint8_t)S.status;
 }
 
-// occupancy of the stage-2 kernel (0: the compiler's choice, 80 VGPRs = 6 waves/SIMD)
-#ifndef AIRICE_OUT_WAVES
-#define AIRICE_OUT_WAVES 0
-#endif
+// occupancy of the stage-2 kernel: the compiler's choice (80 VGPRs = 6 waves/SIMD; 7 and 8
+// measured slower)
 template <int VARIANT>
-__global__ __launch_bounds__(kBlock)
-#if AIRICE_OUT_WAVES
-__attribute__((amdgpu_waves_per_eu(AIRICE_OUT_WAVES, AIRICE_OUT_WAVES)))
-#endif
-void solve_out_kernel(DevMedium M, IceConsts I, QueryArgs Q,
+__global__ __launch_bounds__(kBlock) void solve_out_kernel(DevMedium M, IceConsts I, QueryArgs Q,
                                                            double* __restrict__ out, size_t ld,
                                                            uint8_t* __restrict__ status,
                                                            SortedPark sp) {
@@ -2301,16 +2018,6 @@ __device__ __forceinline__ void fallback_out_direct(const DevMedium& M, const Ic
   lookup_fallback_out_body<false, true>(M, I, Q, out, ld, ok, k, tab, WaveRoot{root, status, g});
 }
 
-__global__ __launch_bounds__(kBlock) void lookup_fallback_out_kernel(
-    DevMedium M, IceConsts I, QueryArgs Q, double* __restrict__ out, size_t ld,
-    uint8_t* __restrict__ ok) {
-  const long long k = (long long)blockIdx.x * kBlock + threadIdx.x;
-  __shared__ __align__(16) double s_logtab[1 << kLogTableBits][2];
-  stage_log_table(s_logtab);
-  if (k >= Q.n) return;
-  lookup_fallback_out_body(M, I, Q, out, ld, ok, k, &s_logtab[0][0]);
-}
-
 // Stage 2 of the pythonwrapper TraceIceToAir (TraceIceToAir.C:5-73), rows of 10.
 template <bool WAVE = false>
 __device__ __forceinline__ void trace_out_body(const DevMedium& M, const IceConsts& I,
@@ -2365,25 +2072,13 @@ template <int IN, int OUT>
 __global__ __launch_bounds__(64) void scalar_solve_kernel(DevMedium M, IceConsts I, QueryArgs Q,
                                                           Park park, double* out, size_t ld,
                                                           uint8_t* flag, Signal sig) {
-#if AIRICE_KARG_PREFETCH
   prefetch_kernargs<sizeof(DevMedium) + sizeof(IceConsts)>();
-#endif
 #if AIRICE_SCALAR_STAMP
   const unsigned long long c0 = __builtin_amdgcn_s_memtime(), w0 = __builtin_amdgcn_s_memrealtime();
 #endif
-#if AIRICE_SCALAR_LDSLOG
-  __shared__ __align__(16) double s_logtab[1 << kLogTableBits][2];
-  for (int t = threadIdx.x; t < (1 << kLogTableBits); t += 64) {
-    s_logtab[t][0] = kLogTable[t][0];
-    s_logtab[t][1] = kLogTable[t][1];
-  }
-  __syncthreads();
-  const double* tab = &s_logtab[0][0];
-#else
   // one wave and a handful of logarithms per evaluation: the log table is read from global
   // memory (L1 / L2 after the first call) instead of being staged in LDS first
   const double* tab = &kLogTable[0][0];
-#endif
   if (IN == IN_CM100 && !(Q.mask[0] & AIRICE_LOOKUP_FALLBACK)) {
     if (threadIdx.x == 0) signal_done(sig);
     return;
@@ -2465,14 +2160,14 @@ hipError_t scratch_alloc(void** p, size_t bytes, hipStream_t st) {
 
 size_t group_min_batch() {
   static const long long v = getenv("AIRICE_GROUP_MIN") ? atoll(getenv("AIRICE_GROUP_MIN"))
-                                                         : AIRICE_GROUP_MIN;
+                                                         : kGroupMin;
   return v > 0 ? (size_t)v : 0;
 }
 
 // Stage 1 of every minimizer launch: roots_kernel (block-local grouping) for small batches and
 // debug statistics, the batch-wide grouping otherwise (stream-ordered scratch, scratch_alloc).
 // A grouped launch returns the sorted parking (sp) its stage-2 kernel reads, and the scratch
-// block (ws) to release after that kernel: release_roots().
+// block (ws) to release after that kernel (RootsScratch).
 template <int IN>
 static int launch_roots(const DevMedium& M, const IceConsts& I, const QueryArgs& Q,
                         const Park& park, size_t n, hipStream_t st, SortedPark& sp, void*& ws) {
@@ -2527,137 +2222,225 @@ static int launch_roots(const DevMedium& M, const IceConsts& I, const QueryArgs&
   return launch_ok();
 }
 
-// Stream-ordered release of a grouped launch's scratch (after its stage-2 kernel).
-static int release_roots(void* ws, hipStream_t st) {
-  if (ws != nullptr && hipFreeAsync(ws, st) != hipSuccess) return AIRICE_EHIP;
-  return AIRICE_OK;
-}
+// A grouped launch's scratch block, released stream-ordered after its stage-2 kernel
+// (release()), or on any early return by the destructor.
+struct RootsScratch {
+  void* ws = nullptr;
+  hipStream_t st;
+  explicit RootsScratch(hipStream_t s) : st(s) {}
+  RootsScratch(const RootsScratch&) = delete;
+  RootsScratch& operator=(const RootsScratch&) = delete;
+  ~RootsScratch() {
+    if (ws != nullptr) (void)hipFreeAsync(ws, st);
+  }
+  int release() {
+    void* p = ws;
+    ws = nullptr;
+    if (p != nullptr && hipFreeAsync(p, st) != hipSuccess) return AIRICE_EHIP;
+    return AIRICE_OK;
+  }
+};
 
-
-#if AIRICE_ROWCONST_CACHE
-// The row constants of a table grid (every Tx-height row: RowConst, 104 B), computed once per
-// (medium, ice constants, grid heights) by rowconst_kernel into a device buffer that is never
-// overwritten: a new key gets a new buffer, and the least recently used of kRowSets is freed
-// (hipFree waits for kernels still reading it).  The caller holds row_cache_mutex() from the
-// lookup until its launches are enqueued, so no other thread can evict a buffer in between; a
-// multi-antenna launch touches at most kMaxAntennas (< kRowSets) sets, so its own are never the
-// least recently used.
-static std::mutex& row_cache_mutex() {
+// Per-grid device caches of the table launch: the row constants of every Tx-height row
+// (RowConst, 104 B; rowconst_kernel) and the start-angle sine of every grid column (8 B;
+// angle_sines_kernel).  Both are O(rows + columns) work that every block of a launch would
+// otherwise redo for the rows and columns it touches.
+//
+// Life of an entry (GridCache::get):
+//  - the FIRST launch that needs a key records the key only and forms its rows / sines in the
+//    kernel (rc / vs = nullptr): a grid built once -- one table per antenna, RunMultiRayCode.C's
+//    pattern -- pays no fill kernel, no allocation and no synchronisation;
+//  - the SECOND launch with the key allocates the buffer, enqueues the fill kernel on its own
+//    stream ahead of its table kernel (stream order makes the buffer complete for it) and records
+//    an event behind the fill; no host synchronisation;
+//  - later launches use the buffer: on the filling stream directly, on another stream once the
+//    event has completed (hipEventQuery) or behind a hipStreamWaitEvent on it;
+//  - a launch being captured into a graph uses an entry only if its fill is already known to be
+//    complete, and pins it: a pinned buffer is never evicted (its address lives in the graph's
+//    kernel arguments).  Otherwise the captured launch forms its rows / sines in the kernel.  No
+//    allocation, query or fill happens under capture.
+// A buffer is written once and never overwritten.  At most kCacheSets unpinned entries per device;
+// the least recently used is freed with hipFree, which waits for the kernels still reading it.
+// The caller holds grid_cache_mutex() from the lookup until its launches are enqueued, so no other
+// thread can evict a buffer in between; a multi-antenna launch touches at most kMaxAntennas
+// (< kCacheSets) entries, so its own are never the least recently used.
+static std::mutex& grid_cache_mutex() {
   static std::mutex mu;
   return mu;
 }
-// A stream that is being captured into a graph: a new cache entry would need a synchronisation,
-// which capture forbids, so such launches use what is cached and form the rest in the kernel.
+// A stream that is being captured into a graph (no allocation, query or synchronisation then).
 static bool stream_capturing(hipStream_t st) {
   hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
   return hipStreamIsCapturing(st, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone;
 }
+constexpr size_t kCacheSets = 64;
+static_assert(kMaxAntennas < (int)kCacheSets, "a multi-antenna launch never evicts its own entries");
+
+class GridCache {
+ public:
+  // fill(buffer, stream): enqueue the kernel that writes the whole buffer.
+  template <class Fill>
+  int get(const std::vector<unsigned char>& key, size_t bytes, hipStream_t st, Fill fill,
+          const void** out) {
+    *out = nullptr;
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return AIRICE_EHIP;
+    if (per_dev_.size() <= (size_t)dev) per_dev_.resize(dev + 1);
+    Dev& D = per_dev_[dev];
+    Entry* c = nullptr;
+    for (Entry& e : D.entries)
+      if (e.key == key) c = &e;
+    if (stream_capturing(st)) {
+      if (c != nullptr && c->dev != nullptr && c->ready) {
+        c->pinned = true;
+        c->used = ++D.tick;
+        *out = c->dev;
+      }
+      return AIRICE_OK;  // otherwise the captured kernel forms the values itself
+    }
+    if (c == nullptr) {  // first use: remember the key, the kernel forms the values
+      if (int rc = make_room(D)) return rc;
+      Entry e;
+      e.key = key;
+      e.used = ++D.tick;
+      D.entries.push_back(std::move(e));
+      return AIRICE_OK;
+    }
+    c->used = ++D.tick;
+    if (c->dev == nullptr) {  // second use: fill, stream-ordered ahead of this launch
+      void* p = nullptr;
+      if (hipMalloc(&p, std::max<size_t>(bytes, 16)) != hipSuccess) return AIRICE_EHIP;
+      fill(p, st);
+      hipEvent_t ev = nullptr;
+      if (hipGetLastError() != hipSuccess ||
+          hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess ||
+          hipEventRecord(ev, st) != hipSuccess) {
+        if (ev != nullptr) (void)hipEventDestroy(ev);
+        (void)hipFree(p);
+        return AIRICE_EHIP;
+      }
+      c->dev = p;
+      c->ev = ev;
+      c->origin = st;
+      *out = p;
+      return AIRICE_OK;
+    }
+    if (!c->ready) {
+      const hipError_t q = hipEventQuery(c->ev);
+      if (q == hipSuccess) {
+        c->ready = true;
+      } else if (q != hipErrorNotReady) {
+        return AIRICE_EHIP;
+      } else if (st != c->origin && hipStreamWaitEvent(st, c->ev, 0) != hipSuccess) {
+        return AIRICE_EHIP;
+      }
+    }
+    *out = c->dev;
+    return AIRICE_OK;
+  }
+
+  // entries of the current device (tests: airice_table_cache_stats)
+  void stats(int* keys, int* filled, int* pinned) {
+    int dev = 0;
+    *keys = *filled = *pinned = 0;
+    if (hipGetDevice(&dev) != hipSuccess || per_dev_.size() <= (size_t)dev) return;
+    for (const Entry& e : per_dev_[dev].entries) {
+      ++*keys;
+      *filled += e.dev != nullptr;
+      *pinned += e.pinned;
+    }
+  }
+
+ private:
+  struct Entry {
+    std::vector<unsigned char> key;
+    void* dev = nullptr;        // nullptr: seen once, not filled
+    hipEvent_t ev = nullptr;    // recorded behind the fill kernel
+    hipStream_t origin = nullptr;
+    bool ready = false;         // the fill is known complete
+    bool pinned = false;        // handed to a captured launch: never evicted
+    unsigned long long used = 0;
+  };
+  struct Dev {
+    std::vector<Entry> entries;
+    unsigned long long tick = 0;
+  };
+  // evict the least recently used unpinned entry when kCacheSets unpinned entries exist
+  static int make_room(Dev& D) {
+    size_t unpinned = 0, old = D.entries.size();
+    for (size_t k = 0; k < D.entries.size(); ++k) {
+      if (D.entries[k].pinned) continue;
+      ++unpinned;
+      if (old == D.entries.size() || D.entries[k].used < D.entries[old].used) old = k;
+    }
+    if (unpinned < kCacheSets) return AIRICE_OK;
+    Entry& e = D.entries[old];
+    if (e.dev != nullptr && hipFree(e.dev) != hipSuccess) return AIRICE_EHIP;
+    if (e.ev != nullptr) (void)hipEventDestroy(e.ev);
+    D.entries.erase(D.entries.begin() + (long)old);
+    return AIRICE_OK;
+  }
+  std::vector<Dev> per_dev_;
+};
+
+static GridCache& row_cache() {
+  static GridCache c;
+  return c;
+}
+static GridCache& angle_cache() {
+  static GridCache c;
+  return c;
+}
+
+// The row constants of a grid.  row_const reads the medium, the heights and, of the ice constants,
+// only the lowest air layer (bot) and the Tx-layer stop ends (topend): the key holds exactly those,
+// so tables of one grid for antennas at different depths in the ice share one entry.
 static int row_consts_cached(const DevMedium& M, const IceConsts& I, const TableArgs& A,
                              hipStream_t st, const RowConst** out) {
-  struct RowSet {
-    std::vector<unsigned char> key;
-    RowConst* dev = nullptr;
-    unsigned long long used = 0;
-  };
-  constexpr size_t kRowSets = 64;
-  static std::vector<std::vector<RowSet>> caches;
-  static unsigned long long tick = 0;
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess) return AIRICE_EHIP;
   const double gk[3] = {A.start_h, A.stop_h, A.step_h};
-  std::vector<unsigned char> key(sizeof(M) + sizeof(I) + sizeof(gk) + sizeof(int));
+  std::vector<unsigned char> key(sizeof(M) + sizeof(I.bot) + sizeof(I.topend) + sizeof(gk) +
+                                 sizeof(A.hsteps));
   unsigned char* kp = key.data();
   std::memcpy(kp, &M, sizeof(M));
-  std::memcpy(kp + sizeof(M), &I, sizeof(I));
-  std::memcpy(kp + sizeof(M) + sizeof(I), gk, sizeof(gk));
-  std::memcpy(kp + sizeof(M) + sizeof(I) + sizeof(gk), &A.hsteps, sizeof(int));
-  if (caches.size() <= (size_t)dev) caches.resize(dev + 1);
-  std::vector<RowSet>& sets = caches[dev];
-  RowSet* c = nullptr;
-  for (RowSet& e : sets)
-    if (e.key == key) c = &e;
-  if (c == nullptr && stream_capturing(st)) {
-    *out = nullptr;  // table_block forms the rows itself
-    return AIRICE_OK;
-  }
-  if (c == nullptr) {
-    if (sets.size() >= kRowSets) {
-      size_t old = 0;
-      for (size_t k = 1; k < sets.size(); ++k)
-        if (sets[k].used < sets[old].used) old = k;
-      if (hipFree(sets[old].dev) != hipSuccess) return AIRICE_EHIP;
-      sets.erase(sets.begin() + (long)old);
-    }
-    RowSet e;
-    if (hipMalloc(&e.dev, sizeof(RowConst) * (size_t)std::max(A.hsteps, 1)) != hipSuccess)
-      return AIRICE_EHIP;
-    hipLaunchKernelGGL(rowconst_kernel, dim3((unsigned)((A.hsteps + 255) / 256)), dim3(256), 0, st,
-                       M, I, A, e.dev);
-    // complete before a launch on another stream can read it
-    if (hipGetLastError() != hipSuccess || hipStreamSynchronize(st) != hipSuccess) {
-      (void)hipFree(e.dev);
-      return AIRICE_EHIP;
-    }
-    e.key = std::move(key);
-    sets.push_back(std::move(e));
-    c = &sets.back();
-  }
-  c->used = ++tick;
-  *out = c->dev;
-  return AIRICE_OK;
+  kp += sizeof(M);
+  std::memcpy(kp, &I.bot, sizeof(I.bot));
+  kp += sizeof(I.bot);
+  std::memcpy(kp, I.topend, sizeof(I.topend));
+  kp += sizeof(I.topend);
+  std::memcpy(kp, gk, sizeof(gk));
+  kp += sizeof(gk);
+  std::memcpy(kp, &A.hsteps, sizeof(A.hsteps));
+  auto fill = [&](void* p, hipStream_t s) {
+    hipLaunchKernelGGL(rowconst_kernel, dim3((unsigned)((A.hsteps + 255) / 256)), dim3(256), 0, s,
+                       M, I, A, static_cast<RowConst*>(p));
+  };
+  const void* p = nullptr;
+  const int rc = row_cache().get(key, sizeof(RowConst) * (size_t)std::max(A.hsteps, 1), st, fill, &p);
+  *out = static_cast<const RowConst*>(p);
+  return rc;
 }
-static_assert(kMaxAntennas < 64, "a multi-antenna launch never evicts its own row sets");
-#endif
-#if AIRICE_ANGLE_CACHE
-// The start-angle sines of an angle grid, kept like the row constants (same mutex, same rules).
+
+// The start-angle sines of an angle grid (the degree-to-radian factor and the angle grid).
 static int angle_sines_cached(const DevMedium& M, const TableArgs& A, hipStream_t st,
                               const double** out) {
-  struct AngleSet {
-    double key[5];
-    double* dev = nullptr;
-    unsigned long long used = 0;
-  };
-  constexpr size_t kAngleSets = 64;
-  static std::vector<std::vector<AngleSet>> caches;
-  static unsigned long long tick = 0;
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess) return AIRICE_EHIP;
-  const double key[5] = {M.d2r, A.start_a, A.stop_a, A.step_a, (double)A.asteps};
-  if (caches.size() <= (size_t)dev) caches.resize(dev + 1);
-  std::vector<AngleSet>& sets = caches[dev];
-  AngleSet* c = nullptr;
-  for (AngleSet& e : sets)
-    if (std::memcmp(e.key, key, sizeof(key)) == 0) c = &e;
-  if (c == nullptr && stream_capturing(st)) {
-    *out = nullptr;  // table_ray forms the sines itself
-    return AIRICE_OK;
-  }
-  if (c == nullptr) {
-    if (sets.size() >= kAngleSets) {
-      size_t old = 0;
-      for (size_t k = 1; k < sets.size(); ++k)
-        if (sets[k].used < sets[old].used) old = k;
-      if (hipFree(sets[old].dev) != hipSuccess) return AIRICE_EHIP;
-      sets.erase(sets.begin() + (long)old);
-    }
-    AngleSet e;
-    std::memcpy(e.key, key, sizeof(key));
-    if (hipMalloc(&e.dev, sizeof(double) * (size_t)std::max(A.asteps, 1)) != hipSuccess)
-      return AIRICE_EHIP;
+  const double k5[5] = {M.d2r, A.start_a, A.stop_a, A.step_a, (double)A.asteps};
+  std::vector<unsigned char> key(sizeof(k5));
+  std::memcpy(key.data(), k5, sizeof(k5));
+  auto fill = [&](void* p, hipStream_t s) {
     hipLaunchKernelGGL(angle_sines_kernel, dim3((unsigned)((A.asteps + 255) / 256)), dim3(256), 0,
-                       st, M, A, e.dev);
-    if (hipGetLastError() != hipSuccess || hipStreamSynchronize(st) != hipSuccess) {
-      (void)hipFree(e.dev);
-      return AIRICE_EHIP;
-    }
-    sets.push_back(e);
-    c = &sets.back();
-  }
-  c->used = ++tick;
-  *out = c->dev;
-  return AIRICE_OK;
+                       s, M, A, static_cast<double*>(p));
+  };
+  const void* p = nullptr;
+  const int rc = angle_cache().get(key, sizeof(double) * (size_t)std::max(A.asteps, 1), st, fill, &p);
+  *out = static_cast<const double*>(p);
+  return rc;
 }
-#endif
+
+void table_cache_stats(int out[6]) {
+  std::lock_guard<std::mutex> lock(grid_cache_mutex());
+  row_cache().stats(&out[0], &out[1], &out[2]);
+  angle_cache().stats(&out[3], &out[4], &out[5]);
+}
 
 int launch_table(const DevMedium& M, const IceConsts& I, const airice_grid* g, int row_begin,
                  int row_count, float* d_table, double* d_full, size_t ld, hipStream_t st) {
@@ -2677,16 +2460,11 @@ int launch_table(const DevMedium& M, const IceConsts& I, const airice_grid* g, i
   // rows a 256-ray set can touch, for the LDS row constants
   A.rows_per_block = std::min(kTableBlock, (kTableBlock - 1) / g->angle_steps + 2);
   A.rc = nullptr;
-#if AIRICE_ROWCONST_CACHE
-  std::unique_lock<std::mutex> rs_lock(row_cache_mutex());  // held until the launches are enqueued
+  std::unique_lock<std::mutex> rs_lock(grid_cache_mutex());  // held until the launches are enqueued
   if (int rc = row_consts_cached(M, I, A, st, &A.rc)) return rc;
-#endif
   A.vs = nullptr;
-#if AIRICE_ANGLE_CACHE
   if (int rc = angle_sines_cached(M, A, st, &A.vs)) return rc;
-#endif
   static const char* trace_path = getenv("AIRICE_TABLE_TRACE");
-  static const int force_r = getenv("AIRICE_TABLE_RPL") ? atoi(getenv("AIRICE_TABLE_RPL")) : 0;
   // ray indices are 32-bit inside a launch: grids of kMaxLaunchRays or more go in row slabs
   const int max_rows = (int)std::max<long long>(1, (kMaxLaunchRays - 2 * kTableBlock) / g->angle_steps);
   for (int done = 0; done < row_count;) {
@@ -2697,22 +2475,13 @@ int launch_table(const DevMedium& M, const IceConsts& I, const airice_grid* g, i
     float* tab = d_table + off;
     double* full = d_full ? d_full + off : nullptr;
     done += rows;
-    // two rays per lane when one ray per lane would take more than one round of resident waves
-    // but two fit in one (kTwoRayMin..kTwoRayMax rays; the double-output parity launches keep one)
-    const int R = !AIRICE_TABLE_R2 ? 1
-                  : force_r ? force_r
-                            : (full == nullptr && A.n > kTwoRayMin && A.n <= kTwoRayMax ? 2 : 1);
-    A.half = R == 2 ? (A.n + 1) / 2 : A.n;
-    const size_t lds = sizeof(RowConst) * (size_t)A.rows_per_block * R;
-    const unsigned blocks = (unsigned)((A.half + kTableBlock - 1) / kTableBlock);
+    A.half = A.n;
+    const size_t lds = sizeof(RowConst) * (size_t)A.rows_per_block;
+    const unsigned blocks = (unsigned)((A.n + kTableBlock - 1) / kTableBlock);
     if (trace_path == nullptr) {
       ktimer_begin(KT_TABLE, st);
-      if (AIRICE_TABLE_R2 && R == 2)
-        hipLaunchKernelGGL((table_kernel<kTableBlock, 1 + AIRICE_TABLE_R2, false>), dim3(blocks),
-                           dim3(kTableBlock), lds, st, M, I, A, tab, full, nullptr);
-      else
-        hipLaunchKernelGGL((table_kernel<kTableBlock, 1, false>), dim3(blocks), dim3(kTableBlock),
-                           lds, st, M, I, A, tab, full, nullptr);
+      hipLaunchKernelGGL(table_kernel<false>, dim3(blocks), dim3(kTableBlock), lds, st, M, I, A,
+                         tab, full, nullptr);
       ktimer_end(KT_TABLE, st);
       if (hipGetLastError() != hipSuccess) return AIRICE_EHIP;
       continue;
@@ -2721,12 +2490,8 @@ int launch_table(const DevMedium& M, const IceConsts& I, const airice_grid* g, i
     const long long nw = (long long)blocks * (kTableBlock / 64);
     WaveTrace* dtr = nullptr;
     if (hipMalloc(&dtr, sizeof(WaveTrace) * nw) != hipSuccess) return AIRICE_EHIP;
-    if (AIRICE_TABLE_R2 && R == 2)
-      hipLaunchKernelGGL((table_kernel<kTableBlock, 1 + AIRICE_TABLE_R2, true>), dim3(blocks),
-                         dim3(kTableBlock), lds, st, M, I, A, tab, full, dtr);
-    else
-      hipLaunchKernelGGL((table_kernel<kTableBlock, 1, true>), dim3(blocks), dim3(kTableBlock), lds,
-                         st, M, I, A, tab, full, dtr);
+    hipLaunchKernelGGL(table_kernel<true>, dim3(blocks), dim3(kTableBlock), lds, st, M, I, A, tab,
+                       full, dtr);
     std::vector<WaveTrace> h(nw);
     if (hipStreamSynchronize(st) != hipSuccess ||
         hipMemcpy(h.data(), dtr, sizeof(WaveTrace) * nw, hipMemcpyDeviceToHost) != hipSuccess)
@@ -2752,9 +2517,7 @@ int launch_table_multi(const DevMedium& M, const IceConsts* Ih, const airice_gri
     return AIRICE_EINVAL;
   }
   std::vector<TableArgs> Ah(n);
-#if AIRICE_ROWCONST_CACHE
-  std::unique_lock<std::mutex> rs_lock(row_cache_mutex());  // held until the launch is enqueued
-#endif
+  std::unique_lock<std::mutex> rs_lock(grid_cache_mutex());  // held until the launch is enqueued
   MultiMap map;
   std::memset(&map, 0, sizeof(map));
   map.n_ant = n;
@@ -2783,13 +2546,9 @@ int launch_table_multi(const DevMedium& M, const IceConsts* Ih, const airice_gri
     A.rows_per_block = rpb;
     A.row0 = 0;
     A.rc = nullptr;
-#if AIRICE_ROWCONST_CACHE
     if (int rc = row_consts_cached(M, Ih[a], A, st, &A.rc)) return rc;
-#endif
     A.vs = nullptr;
-#if AIRICE_ANGLE_CACHE
     if (int rc = angle_sines_cached(M, A, st, &A.vs)) return rc;
-#endif
     const long long rays = (long long)g->table_rows * g->angle_steps;
     if (rays >= kMaxLaunchRays - 2 * kTableBlock || lds[a] < (size_t)rays) {
       set_error("antenna %d: %lld rays (ld %zu) do not fit one multi-antenna launch", a, rays,
@@ -2808,11 +2567,15 @@ int launch_table_multi(const DevMedium& M, const IceConsts* Ih, const airice_gri
   // (up to kConstSets per device, least recently used evicted).  A buffer is written once, by a
   // synchronous copy before any launch reads it, and never overwritten; eviction frees it with
   // hipFree, which waits for the kernels still reading it, on any stream.  The lock is held until
-  // the launch is enqueued, so no other thread can evict the buffer in between.
+  // the launch is enqueued, so no other thread can evict the buffer in between.  Under graph
+  // capture (no allocation or copy allowed) a launch needs its set to be resident already -- one
+  // uncaptured launch of the same antenna set first -- and pins it: a pinned set is never evicted,
+  // since the graph keeps its address.
   struct ConstSet {
     std::vector<unsigned char> host;
     void* dev = nullptr;
     unsigned long long used = 0;
+    bool pinned = false;
   };
   constexpr size_t kConstSets = 8;
   static std::mutex mu;
@@ -2830,11 +2593,20 @@ int launch_table_multi(const DevMedium& M, const IceConsts* Ih, const airice_gri
   ConstSet* c = nullptr;
   for (ConstSet& e : sets)
     if (e.host == packed) c = &e;
+  const bool capturing = stream_capturing(st);
+  if (c == nullptr && capturing) {
+    set_error("multi-antenna table launch under graph capture: run one uncaptured launch of the "
+              "same antenna set (twice: the grid caches fill on a grid's second launch) first");
+    return AIRICE_EINVAL;
+  }
   if (c == nullptr) {
-    if (sets.size() >= kConstSets) {  // evict the least recently used set
-      size_t old = 0;
-      for (size_t k = 1; k < sets.size(); ++k)
-        if (sets[k].used < sets[old].used) old = k;
+    size_t unpinned = 0, old = sets.size();
+    for (size_t k = 0; k < sets.size(); ++k) {
+      if (sets[k].pinned) continue;
+      ++unpinned;
+      if (old == sets.size() || sets[k].used < sets[old].used) old = k;
+    }
+    if (unpinned >= kConstSets) {  // evict the least recently used unpinned set
       if (hipFree(sets[old].dev) != hipSuccess) return AIRICE_EHIP;
       sets.erase(sets.begin() + (long)old);
     }
@@ -2849,10 +2621,11 @@ int launch_table_multi(const DevMedium& M, const IceConsts* Ih, const airice_gri
     c = &sets.back();
   }
   c->used = ++tick;
+  if (capturing) c->pinned = true;
   void* dconst = c->dev;
   const size_t lds_bytes = sizeof(RowConst) * (size_t)rpb;
   ktimer_begin(KT_TABLE, st);
-  hipLaunchKernelGGL(table_multi_kernel<kTableBlock>, dim3((unsigned)blocks), dim3(kTableBlock),
+  hipLaunchKernelGGL(table_multi_kernel, dim3((unsigned)blocks), dim3(kTableBlock),
                      lds_bytes, st, M, static_cast<const IceConsts*>(dconst),
                      reinterpret_cast<const TableArgs*>(static_cast<unsigned char*>(dconst) +
                                                         bytes_i),
@@ -2895,8 +2668,8 @@ int launch_solve(const DevMedium& M, const IceConsts& I, int variant, const doub
     return launch_ok();
   }
   SortedPark sp;
-  void* ws;
-  if (int rc = launch_roots<IN_M>(M, I, Q, park, n, st, sp, ws)) return rc;
+  RootsScratch scr(st);
+  if (int rc = launch_roots<IN_M>(M, I, Q, park, n, st, sp, scr.ws)) return rc;
   if (park.stats != nullptr) {  // debug: append the per-query counts (synchronous)
     std::vector<int> h(3 * n);
     if (hipStreamSynchronize(st) != hipSuccess ||
@@ -2917,7 +2690,7 @@ int launch_solve(const DevMedium& M, const IceConsts& I, int variant, const doub
                        out, ld, status, sp);
   ktimer_end(KT_OUT, st);
   const int rc = launch_ok();
-  if (int rf = release_roots(ws, st)) return rf;
+  if (int rf = scr.release()) return rf;
   return rc;
 }
 
@@ -2934,13 +2707,13 @@ int launch_hdtip(const DevMedium& M, const IceConsts& I, const double* src, cons
     return launch_ok();
   }
   SortedPark sp;
-  void* ws;
-  if (int rc = launch_roots<IN_CM>(M, I, Q, park, n, st, sp, ws)) return rc;
+  RootsScratch scr(st);
+  if (int rc = launch_roots<IN_CM>(M, I, Q, park, n, st, sp, scr.ws)) return rc;
   ktimer_begin(KT_OUT, st);
   hipLaunchKernelGGL(hdtip_out_kernel, grid, block, 0, st, M, I, Q, out, ld, ok, sp);
   ktimer_end(KT_OUT, st);
   const int rc = launch_ok();
-  if (int rf = release_roots(ws, st)) return rf;
+  if (int rf = scr.release()) return rf;
   return rc;
 }
 
@@ -2959,7 +2732,6 @@ int launch_lookup_fallback(const DevMedium& M, const IceConsts& I, const double*
                        I, Q, park, out, ld, ok, take_scalar_signal());
     return launch_ok();
   }
-#if AIRICE_FALLBACK_FUSED
   // one pass: 256-lane blocks group their few fallback lanes into their first wave, solve them and
   // write their outputs (stage 2 with the root in registers)
   (void)grid;
@@ -2967,14 +2739,6 @@ int launch_lookup_fallback(const DevMedium& M, const IceConsts& I, const double*
   hipLaunchKernelGGL((roots_kernel<IN_CM100, 256, true>), dim3((unsigned)((n + 255) / 256)),
                      dim3(256), 0, st, M, I, Q, park, out, ld, ok);
   return launch_ok();
-#else
-  SortedPark sp;  // the fallback pass is never grouped (launch_roots): the parked slots
-  void* ws;
-  if (int rc = launch_roots<IN_CM100>(M, I, Q, park, n, st, sp, ws)) return rc;
-  if (sp.rec != nullptr) return AIRICE_EINVAL;
-  hipLaunchKernelGGL(lookup_fallback_out_kernel, grid, block, 0, st, M, I, Q, out, ld, ok);
-  return launch_ok();
-#endif
 }
 
 int launch_trace(const DevMedium& M, const IceConsts& I, const double* depth, const double* ice,
@@ -2989,13 +2753,13 @@ int launch_trace(const DevMedium& M, const IceConsts& I, const double* depth, co
     return launch_ok();
   }
   SortedPark sp;
-  void* ws;
-  if (int rc = launch_roots<IN_TRACE>(M, I, Q, park, n, st, sp, ws)) return rc;
+  RootsScratch scr(st);
+  if (int rc = launch_roots<IN_TRACE>(M, I, Q, park, n, st, sp, scr.ws)) return rc;
   ktimer_begin(KT_OUT, st);
   hipLaunchKernelGGL(trace_out_kernel, grid, block, 0, st, M, I, Q, out10, sp);
   ktimer_end(KT_OUT, st);
   const int rc = launch_ok();
-  if (int rf = release_roots(ws, st)) return rf;
+  if (int rf = scr.release()) return rf;
   return rc;
 }
 

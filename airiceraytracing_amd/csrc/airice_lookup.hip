@@ -34,19 +34,12 @@ namespace {
 
 constexpr int kLkBlock = 256;
 
-// waves per SIMD the register allocation targets (0: the compiler's choice, 78 VGPRs = 6 waves).
-// Measured (1e6 cfg3 queries, identical outputs): 7 waves (72 VGPRs, 28 B/lane spilled) 166 us and
-// 8 waves (64 VGPRs, 60 B/lane) 175 us against 152 us at 6: more resident waves do not help a
-// kernel bound by the L2 line requests of its 64-lane gathers, and the spills add requests.
-#ifndef AIRICE_LK_WAVES
-#define AIRICE_LK_WAVES 0
-#endif
-#if AIRICE_LK_WAVES > 0
-#define AIRICE_LK_OCC __attribute__((amdgpu_waves_per_eu(AIRICE_LK_WAVES, AIRICE_LK_WAVES)))
-#else
-#define AIRICE_LK_OCC
-#endif
-__global__ __launch_bounds__(kLkBlock) AIRICE_LK_OCC void lookup_kernel(LkTable T, const double* __restrict__ src,
+// Occupancy: the compiler's choice (78 VGPRs = 6 waves/SIMD).  Measured (1e6 cfg3 queries,
+// identical outputs): 7 waves (72 VGPRs, 28 B/lane spilled) 166 us and 8 waves (64 VGPRs,
+// 60 B/lane) 175 us against 152 us at 6: more resident waves do not help a kernel bound by the L2
+// line requests of its 64-lane gathers, and the spills add requests.  (Searching the two rows of
+// GetParValues side by side, each step issuing both rows' reads, measured 163 against 161 us.)
+__global__ __launch_bounds__(kLkBlock) void lookup_kernel(LkTable T, const double* __restrict__ src,
                                                           const double* __restrict__ dist,
                                                           double ice_cm, long long n, double d2r,
                                                           double* __restrict__ out, size_t ld,

@@ -261,158 +261,9 @@ __host__ __device__ __forceinline__ void lk_row_params(const LkTable& T, double 
   }
 }
 
-// ---- the two rows of GetParValues side by side ----------------------------------------------
-// A random query's time is two chains of dependent table reads (row 1, then row 2: bisection
-// steps, the closing scan, the pair record).  The rows are independent, so lk_par_values runs
-// their FindClosestTHD searches in one loop: every step issues both rows' reads before using
-// either.  Each row reads the same entries and takes the same decisions as lk_closest_thd
-// (AIRICE_LOOKUP_UNPINNED is an OR over the reads, so their order does not matter); a row that the
-// reference does not search issues a harmless read of entry 0 whose value is not used.
-// Measured (tools/lookup_order_probe.py, 1e6 cfg3 queries, outputs identical): random order
-// 163.4 us against 160.8 us for the row-after-row form, Tx-height-sorted 78.2 against 79.9,
-// (height class, distance)-sorted 95.0 against 103.4.  Random batches are bound by the L2 line
-// requests of 64-lane gathers (~23 lines per query), not by the chains' latency, so the default
-// stays the row-after-row form.
-#ifndef AIRICE_LK_PAIRED
-#define AIRICE_LK_PAIRED 0
-#endif
-
-// lk_at when `on`; otherwise an unused read of entry 0 and no flag
-__host__ __device__ __forceinline__ double lk_at_if(const LkTable& T, int c, long long i, bool on,
-                                                    int& fl) {
-  const bool oob = i < 0 || i >= T.n;
-  if (on && oob) fl |= AIRICE_LOOKUP_UNPINNED;
-  const double v = (double)T.col[c][(on && !oob) ? i : 0];
-  return oob ? __builtin_nan("") : v;
-}
-
-// lk_closest_thd's end: the pair around index2 and the closest-value test
-__host__ __device__ __forceinline__ LkThdBins lk_thd_close(const LkTable& T, double P,
-                                                           long long index2, int& fl,
-                                                           LkThdPair& pr) {
-  const long long index1 = index2 - 1;
-  pr.have_pair = lk_pair(T, index1, pr.r1, pr.r2);
-  const double v2 = pr.have_pair ? (double)pr.r2.c[0] : lk_at(T, 1, index2, fl);
-  const double v1 = pr.have_pair ? (double)pr.r1.c[0] : lk_at(T, 1, index1, fl);
-  double minimum = fabs(P - v2);
-  if (minimum > fabs(P - v1)) minimum = fabs(P - v1);
-  return LkThdBins{index1, index2, minimum};
-}
-
-// lk_row_params' use of a search result (a: D within the row's THD range)
-__host__ __device__ __forceinline__ void lk_row_fill(const LkTable& T, double D, bool a,
-                                                     const LkThdBins& b, const LkThdPair& pr,
-                                                     double par[10], int& fl) {
-  if (a) {
-    if (b.c != 0) {
-      const LkRec rs = pr.have_pair ? pr.r1 : lk_rec(T, b.s, fl);
-      const LkRec re = pr.have_pair ? pr.r2 : lk_rec(T, b.e, fl);
-      const double x1 = pr.have_pair ? (double)pr.r1.c[0] : lk_at(T, 1, b.s, fl);
-      const double x2 = pr.have_pair ? (double)pr.r2.c[0] : lk_at(T, 1, b.e, fl);
-#pragma unroll
-      for (int ip = 0; ip < 10; ++ip)
-        par[ip] = lk_interp(D, x1, (double)rs.c[ip], x2, (double)re.c[ip]);
-    } else {
-      const LkRec r = pr.have_pair ? pr.r2 : lk_rec(T, b.s + 1, fl);
-#pragma unroll
-      for (int ip = 0; ip < 10; ++ip) par[ip] = (double)r.c[ip];
-    }
-  } else {
-#pragma unroll
-    for (int ip = 0; ip < 10; ++ip) par[ip] = -1e9;
-  }
-}
-
-// FindClosestTHD on two rows at once (a1 / a2: the row is searched)
-__host__ __device__ __forceinline__ void lk_closest_thd_2(const LkTable& T, double P, long long s1,
-                                                          long long e1, bool a1, long long s2,
-                                                          long long e2, bool a2, int& fl,
-                                                          LkThdBins& b1, LkThdPair& p1,
-                                                          LkThdBins& b2, LkThdPair& p2) {
-#pragma unroll 1
-  for (int i = 0; i < 8; ++i) {
-    const bool d1 = a1 && e1 - s1 >= 3, d2 = a2 && e2 - s2 >= 3;
-    const long long m1 = (s1 + e1) / 2, m2 = (s2 + e2) / 2;
-    const double v1 = lk_at_if(T, 1, m1, d1, fl), v2 = lk_at_if(T, 1, m2, d2, fl);
-    if (d1) {
-      if (v1 - P > 0) s1 = m1;
-      if (v1 - P < 0) e1 = m1;
-    }
-    if (d2) {
-      if (v2 - P > 0) s2 = m2;
-      if (v2 - P < 0) e2 = m2;
-    }
-  }
-  // the scans from s to e + 1 until an entry is not above P (index2; 0 if none)
-  double mn1 = 100000000000.0, mn2 = 100000000000.0;
-  long long i1 = s1, i2 = s2, x1 = 0, x2 = 0;
-  bool r1 = a1, r2 = a2;
-#pragma unroll 1
-  while (r1 || r2) {
-    const bool g1 = r1 && i1 < e1 + 1, g2 = r2 && i2 < e2 + 1;
-    const double v1 = lk_at_if(T, 1, i1, g1, fl), v2 = lk_at_if(T, 1, i2, g2, fl);
-    if (g1) {
-      const double minval = fabs(v1 - P);
-      if (minval < mn1 && v1 > P) {
-        mn1 = minval;
-        ++i1;
-      } else {
-        x1 = i1;
-        r1 = false;
-      }
-    } else {
-      r1 = false;
-    }
-    if (g2) {
-      const double minval = fabs(v2 - P);
-      if (minval < mn2 && v2 > P) {
-        mn2 = minval;
-        ++i2;
-      } else {
-        x2 = i2;
-        r2 = false;
-      }
-    } else {
-      r2 = false;
-    }
-  }
-  if (a1) b1 = lk_thd_close(T, P, x1, fl, p1);
-  if (a2) b2 = lk_thd_close(T, P, x2, fl, p2);
-}
-
 // GetParValues (.cc:1172-1302) for a Tx height inside the table's range
 __host__ __device__ __forceinline__ void lk_par_values(const LkTable& T, double H, double D, double* h1,
                                        double par1[10], double* h2, double par2[10], int& fl) {
-#if AIRICE_LK_PAIRED
-  const double min_h = lk_at(T, 0, T.n - 1, fl);
-  LkRow R;
-  const bool fast = lk_row(T, lk_txh_index(T, H), R);
-  LkTxhBins b;
-  if (fast) {
-    b = R.b;
-    b.c1 = fabs(R.c1v - H);
-    b.c2 = b.c1;
-  } else {
-    b = lk_closest_txh(T, H, fl);
-  }
-  *h1 = fast ? R.h1 : lk_at(T, 0, b.s1, fl);
-  const bool two = b.c1 != 0 && H > min_h && b.s2 < T.n - 1;  // the second row is read
-  *h2 = two ? (fast ? R.h2 : lk_at(T, 0, b.s2, fl)) : *h1;
-  // lk_row_params: each row is searched when D is within its largest THD
-  const double mx1 = fast ? R.mt1 : lk_at(T, 1, b.s1, fl);
-  const double mx2 = two ? (fast ? R.mt2 : lk_at(T, 1, b.s2, fl)) : 0.0;
-  const bool a1 = D <= mx1, a2 = two && D <= mx2;
-  LkThdBins t1{0, 0, 0}, t2{0, 0, 0};
-  LkThdPair p1, p2;
-  lk_closest_thd_2(T, D, b.s1, b.e1, a1, b.s2, b.e2, a2, fl, t1, p1, t2, p2);
-  lk_row_fill(T, D, a1, t1, p1, par1, fl);
-  if (two) {
-    lk_row_fill(T, D, a2, t2, p2, par2, fl);
-  } else {
-#pragma unroll
-    for (int ip = 0; ip < 10; ++ip) par2[ip] = par1[ip];
-  }
-#else
   const double min_h = lk_at(T, 0, T.n - 1, fl);
   LkRow R;  // packed row record: the span and its end values without the scans
   const bool fast = lk_row(T, lk_txh_index(T, H), R);
@@ -436,7 +287,6 @@ __host__ __device__ __forceinline__ void lk_par_values(const LkTable& T, double 
 #pragma unroll
     for (int ip = 0; ip < 10; ++ip) par2[ip] = par1[ip];
   }
-#endif
 }
 
 // GetHorizontalDistanceToIntersectionPoint_Table (.cc:1305-1462) for one query (metres): out9

@@ -16,13 +16,6 @@
 #include "airice.h"
 #include "airice_internal.h"
 
-// GetAirPropagationPar / MinimizeforLaunchAngle on a wave: each layer's two ends on two lanes
-#ifndef AIRICE_RTF_SIDES
-#define AIRICE_RTF_SIDES 1
-#endif
-#ifndef AIRICE_KARG_PREFETCH
-#define AIRICE_KARG_PREFETCH 1
-#endif
 
 namespace airice {
 
@@ -552,7 +545,6 @@ __device__ LayerLane air_prop_lane(const DevMedium& M, double LaunchAngleAir, do
   const double A = ice ? M.A_ice : M.A_air;
   const double Rx = ice ? AntennaDepth : StopH, Tx = ice ? 0.0 : StartH;
   const int air = ice ? 0 : 1;
-#if AIRICE_RTF_SIDES
   // the layer's two ends on two lanes (lane j: Rx, lane j + 8: Tx; the partner's values come back
   // by shuffle): each antiderivative of GetRayOpticalPath / GetRayPropagationTime /
   // GetRayGeometricPath once per lane, differenced in the reference's order (+Rx - Tx, sign flip
@@ -582,16 +574,6 @@ __device__ LayerLane air_prop_lane(const DevMedium& M, double LaunchAngleAir, do
       R.o[4] = g;
     }
   }
-#else
-  R.o[0] = rtf_optical_path(M, A, Rx, Tx, L, air);
-  if (full) {
-    const double nzStopHeight = rtf_nz_air(M, StopH);
-    R.o[1] = (j == 0) ? Recv0 * M.r2d : asin(L / nzStopHeight) * M.r2d;
-    R.o[2] = L;
-    R.o[3] = rtf_prop_time(M, A, Rx, Tx, L, air);
-    if (W == 5) R.o[4] = mr_geo_path(M, A, Rx, Tx, L, air);
-  }
-#endif
   return R;
 }
 
@@ -602,7 +584,7 @@ __device__ void air_prop_wave(const DevMedium& M, double LaunchAngleAir, double 
                               double IceLayerHeight, double* __restrict__ out) {
   const int lane = (int)(threadIdx.x & 63);
   const LayerLane R = air_prop_lane<W>(M, LaunchAngleAir, AirTxHeight, IceLayerHeight,
-                                       AIRICE_RTF_SIDES ? (lane & 7) : lane, true, -1, 0.0);
+                                       (lane & 7), true, -1, 0.0);
   if (lane < M.ml)
     for (int k = 0; k < W; k++) out[W * lane + k] = lane < R.nf ? R.o[k] : 0.0;
   if (lane == 0) {
@@ -619,7 +601,7 @@ __device__ double min_launch_wave(const DevMedium& M, double x, double AirTxHeig
                                   double IceLayerHeight, double AntennaDepth, double D) {
   const int lane = (int)(threadIdx.x & 63);
   const LayerLane R = air_prop_lane<W>(M, x, AirTxHeight, IceLayerHeight,
-                                       AIRICE_RTF_SIDES ? (lane & 7) : lane, false, 4, AntennaDepth);
+                                       (lane & 7), false, 4, AntennaDepth);
   double thd_air = 0;
   for (int i = 0; i < kMaxLayers; i++) {
     const double a = __shfl(R.o[0], i);
@@ -650,9 +632,7 @@ struct RtfCall {
 };
 
 __global__ void rtf_kernel(DevMedium M, RtfCall c, double* __restrict__ out, Signal sig) {
-#if AIRICE_KARG_PREFETCH
   prefetch_kernargs<sizeof(DevMedium) + sizeof(RtfCall)>();
-#endif
   // the layer-loop ops run on the whole wave (air_prop_wave, min_launch_wave); the rest on lane 0
   if (c.op == AIRICE_RTF_AIR_PROPAGATION || c.op == AIRICE_MR_AIR_PROPAGATION) {
     if (c.op == AIRICE_RTF_AIR_PROPAGATION)

@@ -303,6 +303,15 @@ int lookup_fallback_one(const airice_medium* m, double src_cm, double dist_cm, d
 
 using namespace airice;
 
+extern "C" int airice_table_cache_stats(int out[6]) {
+  if (out == nullptr) {
+    set_error("airice_table_cache_stats: out is null");
+    return AIRICE_EINVAL;
+  }
+  table_cache_stats(out);
+  return AIRICE_OK;
+}
+
 extern "C" int airice_kernel_timing(int on) {
   g_ktimer_on.store(on != 0, std::memory_order_relaxed);
   return AIRICE_OK;

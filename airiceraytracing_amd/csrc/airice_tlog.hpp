@@ -26,21 +26,6 @@
 
 #include "airice_logtab.h"
 
-#ifndef AIRICE_LEAN_ESTRIN
-#define AIRICE_LEAN_ESTRIN 0  // measured: no faster than Horner
-#endif
-// Degree of tlog_lean's log1p(r) polynomial: 5 (default; truncation <= 2^-50.6 absolute) or
-// 6 / 7 (the full form).  Degree 5 vs 7: cfg2 table 2.8 % and cfg3 solves 2 % faster, float
-// table bit-identical (tools/ab_table.py, tools/gpu_ab_solve.sh).
-#ifndef AIRICE_LEAN_DEG
-#define AIRICE_LEAN_DEG 5
-#endif
-// tlog_lean's table address as one shift and one mask of the high word (the byte offset of
-// entry i) instead of the entry index scaled afterwards
-#ifndef AIRICE_TLOG_IDX2
-#define AIRICE_TLOG_IDX2 1
-#endif
-
 namespace airice {
 
 // A polynomial coefficient held in an SGPR pair: the fma then issues as one VOP3 v_fma_f64 with the
@@ -103,7 +88,7 @@ __host__ __device__ AIRICE_INLINE double tlog_pos(double x, const double* tab = 
 }
 
 // log(x) for x positive, normal and finite, without the hi + lo bookkeeping: w = k ln2 + log c_i
-// by one fma, then w + (r + r^2 q) with q of degree AIRICE_LEAN_DEG - 2 in r.  ~8 FP64 ops
+// by one fma, then w + (r + r^2 q) with q of degree 3 in r.  ~8 FP64 ops
 // instead of ~19.  Error bounded in ABSOLUTE terms: <= ~3 ulp of max(|log x|, 1) at degree 5
 // (truncation |r|^6/6 <= 2^-50.6 for |r| <= 2^-8, plus the roundings of w and the final sum;
 // 2 ulp at degree 7), measured in tests/test_tlog.py.  The ray kernels' log ratios use this
@@ -111,52 +96,24 @@ __host__ __device__ AIRICE_INLINE double tlog_pos(double x, const double* tab = 
 // logarithm is what reaches them.
 __host__ __device__ AIRICE_INLINE double tlog_lean(double x, const double* tab = &kLogTable[0][0]) {
   const double Ln2 = 0x1.62e42fefa39efp-1;
-  const double A0 = -0x1p-1, A1 = 0x1.5555555555555p-2, A2 = -0x1p-2, A3 = 0x1.999999999999ap-3,
-               A4 = -0x1.5555555555555p-3, A5 = 0x1.2492492492492p-3;
+  const double A0 = -0x1p-1, A1 = 0x1.5555555555555p-2, A2 = -0x1p-2, A3 = 0x1.999999999999ap-3;
   const uint64_t ix = dbits(x);
   const uint32_t hx = (uint32_t)(ix >> 32);
   const uint32_t htmp = hx - 0x3fe60000u;
   const int k = (int32_t)htmp >> 20;
   const double z = bitsd(((uint64_t)(hx - (htmp & 0xfff00000u)) << 32) | (ix & 0xffffffffULL));
-#if AIRICE_TLOG_IDX2
+  // the table address as one shift and one mask of the high word (the byte offset of entry i)
   const uint32_t off = (htmp >> (20 - kLogTableBits - 4)) & (((1u << kLogTableBits) - 1) << 4);
   const double* ent = reinterpret_cast<const double*>(reinterpret_cast<const char*>(tab) + off);
   const double invc = ent[0], logc = ent[1];
-#else
-  const int i = (int)((htmp >> (20 - kLogTableBits)) & ((1u << kLogTableBits) - 1));
-  const double invc = tab[2 * i], logc = tab[2 * i + 1];
-#endif
   const double r = AIRICE_FMA(z, invc, -1.0);
   const double w = AIRICE_FMA((double)k, Ln2, logc);
   const double r2 = r * r;
-#if AIRICE_LEAN_ESTRIN
-  // the same polynomial with a 3-deep instead of a 5-deep dependent chain (pairs in r, then r^2)
-  const double p01 = AIRICE_FMA(r, kc(A1), kc(A0));
-  const double p23 = AIRICE_FMA(r, kc(A3), kc(A2));
-  const double p45 = AIRICE_FMA(r, A5, kc(A4));
-  const double q = AIRICE_FMA(r2, AIRICE_FMA(r2, p45, p23), p01);
-#elif AIRICE_LEAN_DEG == 4
-  // through r^4 (for a table of >= 1024 entries, |r| <= 2^-11: truncation <= 2^-57.3 absolute)
-  double q = AIRICE_FMA(r, kc(A2), kc(A1));
-  q = AIRICE_FMA(r, q, kc(A0));
-#elif AIRICE_LEAN_DEG == 5
-  // through r^5: truncation |r|^6 / 6 <= 2^-50.6 absolute
+  // through r^5: truncation |r|^6 / 6 <= 2^-50.6 absolute (degree 7 measured 2.8 % slower on
+  // the cfg2 table with the float table bit-identical; an Estrin form no faster than Horner)
   double q = AIRICE_FMA(r, kc(A3), kc(A2));
   q = AIRICE_FMA(r, q, kc(A1));
   q = AIRICE_FMA(r, q, kc(A0));
-#elif AIRICE_LEAN_DEG == 6
-  // through r^6: truncation |r|^7 / 7 <= 2^-58.8 absolute
-  double q = AIRICE_FMA(r, kc(A4), kc(A3));
-  q = AIRICE_FMA(r, q, kc(A2));
-  q = AIRICE_FMA(r, q, kc(A1));
-  q = AIRICE_FMA(r, q, kc(A0));
-#else
-  double q = AIRICE_FMA(r, A5, kc(A4));
-  q = AIRICE_FMA(r, q, kc(A3));
-  q = AIRICE_FMA(r, q, kc(A2));
-  q = AIRICE_FMA(r, q, kc(A1));
-  q = AIRICE_FMA(r, q, kc(A0));
-#endif
   return AIRICE_FMA(r2, q, r) + w;
 }
 

@@ -135,6 +135,21 @@ def assemble_to_host(slab: torch.Tensor, count_items: int, first_item: int, host
         host[:, first_item:first_item + count_items].copy_(slab[:, :count_items])
 
 
+def _try(make):
+    """(make(), None), or (None, the error's text) when it raises OSError / ValueError."""
+    try:
+        return make(), None
+    except (OSError, ValueError) as e:
+        return None, f"{type(e).__name__}: {e}"
+
+
+def _all_ok(ok: bool, group=None, device=None) -> bool:
+    """True on every rank iff ``ok`` is true on every rank (one all-reduce)."""
+    t = torch.tensor([1 if ok else 0], dtype=torch.int32, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MIN, group=group)
+    return bool(t.item())
+
+
 def table_sharded(grid, compute: Callable[[int, int, torch.Tensor], None], cols: int = 11,
                   dtype=torch.float32, device=None, root: int = 0, group=None):
     """Build the full grid across ranks.  compute(row_begin, row_count, out) fills
@@ -227,18 +242,32 @@ def run_sharded_table(grid, compute: Callable[[int, int, torch.Tensor], None], s
     assembled = None
     gather_s = []
     host = None
+    host_error = None
     if assemble == "host":
         if host_path is None:
             raise ValueError("assemble='host' needs host_path")
+        # the root creates the shared table, then the others map it; a failure on any rank (a full
+        # /dev/shm, permissions) is agreed on by every rank, which then all take the RCCL gather,
+        # instead of the failing rank raising while the others wait in a barrier
         if rank == root:
-            host = SharedHostTable(host_path, cols, n_rays, create=True)
-        dist.barrier(group)
-        if rank != root:
-            host = SharedHostTable(host_path, cols, n_rays, create=False)
-        dist.barrier(group)
-        if rank == root:
+            host, host_error = _try(lambda: SharedHostTable(host_path, cols, n_rays, create=True))
+        if not _all_ok(host_error is None, group, coll_device):
+            host_error = host_error or "the root could not create the shared host table"
+        else:
+            if rank != root:
+                host, host_error = _try(
+                    lambda: SharedHostTable(host_path, cols, n_rays, create=False))
+            if not _all_ok(host_error is None, group, coll_device):
+                host_error = host_error or "a rank could not map the shared host table"
+        if rank == root and host is not None:
             import os
-            os.unlink(host_path)  # every rank has it mapped; it goes with the last process
+            os.unlink(host_path)  # every rank has it mapped (or failed); it goes with the last process
+        if host_error is not None:
+            if host is not None:
+                host.close()
+                host = None
+            assemble = "rccl"
+    if assemble == "host":
         if host_register is not None and count:
             host.register_columns(begin * asteps, count * asteps, host_register)
         for _ in range(max(1, gather_reps)):
@@ -270,6 +299,6 @@ def run_sharded_table(grid, compute: Callable[[int, int, torch.Tensor], None], s
     return {"elapsed_s": float(red[0]), "gather_s": float(red[1]), "row_begin": begin,
             "row_count": count, "rows_per_rank": per, "rays_this_rank": count * asteps,
             "bytes_to_root": moved if assemble == "rccl" else 0,
-            "bytes_assembled": moved, "assemble": assemble,
+            "bytes_assembled": moved, "assemble": assemble, "host_assembly_error": host_error,
             "slab": slab, "assembled": assembled, "host": host,
             "host_unregister": host_unregister}

@@ -73,6 +73,8 @@ def parse():
     p.add_argument("--no-multi", action="store_true",
                    help="skip the several-antenna line item (tables on concurrent streams)")
     p.add_argument("--no-scalar", action="store_true", help="skip the scalar-call latencies")
+    p.add_argument("--no-cold", action="store_true",
+                   help="skip the cold (one table per antenna) line item")
     p.add_argument("--no-default-grid", action="store_true",
                    help="skip the reference default grid line item (8.7M rays)")
     p.add_argument("--no-cfg4", action="store_true", help="skip the cfg4 fine-table line item")
@@ -527,6 +529,8 @@ def main():
                       "RunMultiRayCode.C:29-52): concurrent HIP streams, and one "
                       "airice_table_launch_multi launch (rays/s)",
             **multi}
+    if not args.no_cold and not sharded:
+        extra["table_cold"] = table_cold(solver, grid, table, stream, rank, kern_ms)
     if not args.no_pcie and not sharded:
         # host-buffer callers (AllTableAllAntData is host memory): table build + D2H copy of the
         # 11 float columns into pinned memory, in stream order; never the headline value
@@ -679,6 +683,60 @@ def main():
         dist.destroy_process_group()
 
 
+def table_cold(solver, grid, table, stream, rank, warm_kernel_ms, builds: int = 16) -> dict:
+    """The table build as the reference's callers run it: RunMultiRayCode.C:29-52 builds one
+    table per AntennaDepths entry (MakeRayTracingTable, MultiRayAirIceRefraction.cc:2019-2158),
+    each once.  ``builds`` cfg2-sized tables back to back on one stream, each for a grid key never
+    built before in this process, timed on the wall clock (host launch work included) and by HIP
+    events, beside the same number of repeated (warm) builds of the headline grid timed the same
+    way:
+
+    * ``new_depths``: antennas at new depths in the ice -- the row constants of the grid are shared
+      across depths (their cache key holds only what the rows read), the angle sines too;
+    * ``new_grids``: every build a new ice height and angle grid, so neither per-grid cache has
+      the key: each build forms its rows and sines in the kernel."""
+    import torch
+    from airiceraytracing_amd import _lib, make_grid
+
+    def run(grids) -> tuple[float, float]:
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        t0 = time.perf_counter()
+        e0.record(stream)
+        for g in grids:
+            solver.table_device(g, table, None, stream=stream)
+        e1.record(stream)
+        torch.cuda.synchronize()
+        wall = (time.perf_counter() - t0) / len(grids) * 1e3
+        return wall, e0.elapsed_time(e1) / len(grids)
+
+    warm_wall, warm_ev = run([grid] * builds)
+    base = CFG2["depth_cm"] - 100000.0 * (rank + 1)  # depths this process has not built
+    new_depths = [make_grid(base - 1300.0 * a, CFG2["ice_cm"], CFG2["height_step"],
+                            CFG2["start_angle"], CFG2["stop_angle"], CFG2["angle_step"])
+                  for a in range(builds)]
+    before = _lib.table_cache_stats()
+    d_wall, d_ev = run(new_depths)
+    after = _lib.table_cache_stats()
+    new_grids = [make_grid(CFG2["depth_cm"], CFG2["ice_cm"] + 1.0 * (a + 1 + 100 * rank),
+                           CFG2["height_step"], CFG2["start_angle"] + 1e-7 * (a + 1),
+                           CFG2["stop_angle"], CFG2["angle_step"]) for a in range(builds)]
+    assert all(g.n_rays == grid.n_rays for g in new_grids + new_depths)
+    g_wall, g_ev = run(new_grids)
+    return {
+        "metric": "cfg2-sized tables, each for an antenna / grid not built before "
+                  "(RunMultiRayCode.C:29-52: one MakeRayTracingTable per antenna), ms per build",
+        "builds": builds, "rays_per_build": grid.n_rays,
+        "warm_ms_per_build": warm_wall, "warm_event_ms_per_build": warm_ev,
+        "new_depths_ms_per_build": d_wall, "new_depths_event_ms_per_build": d_ev,
+        "new_depths_vs_warm": d_wall / warm_wall,
+        "new_depths_row_cache_keys_added": after["rows"]["keys"] - before["rows"]["keys"],
+        "new_grids_ms_per_build": g_wall, "new_grids_event_ms_per_build": g_ev,
+        "new_grids_vs_warm": g_wall / warm_wall,
+        "new_grids_rays_per_s": grid.n_rays / (g_wall * 1e-3),
+        "headline_kernel_ms": warm_kernel_ms}
+
+
 def cfg4_check_rows(height_steps: int) -> list[int]:
     """Rows of the cfg4 table checked against the oracle: the first and last rows, the rows on
     either side of each atmosphere-layer bound the Tx heights cross (23141.75, 8363.54 and
@@ -759,6 +817,9 @@ def table_cfg4(args, solver, world, rank, dev, stream, distributed, coll_dev, pm
                               host_path=plan[0], host_copy=host_copy,
                               host_register=register, host_unregister=unregister)
         torch.cuda.synchronize()
+        mode = r["assemble"]  # "rccl" when a rank could not create or map the shared host table
+        if r.get("host_assembly_error"):
+            rep["host_assembly_error"] = r["host_assembly_error"]
         build_s = r["elapsed_s"] / args.cfg4_reps
         rep.update({"value": n / build_s, "ms_per_build": build_s * 1e3,
                     "kernel_ms_rank0": ev0.elapsed_time(ev1) / args.cfg4_reps,

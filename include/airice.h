@@ -381,6 +381,13 @@ int airice_table_load(const char *path, const airice_medium *expect, float *h_ta
 int airice_kernel_timing(int on);
 int airice_kernel_time(const char *name, double *total_ms, int64_t *launches, int reset);
 
+/* The table launch's per-grid caches on the current device (no reference counterpart; tests and
+ * diagnostics).  out[0..2]: row-constant keys seen, of them filled (device buffer resident),
+ * pinned (used by a launch captured into a graph); out[3..5]: the same for the start-angle
+ * sines.  A grid's first launch only records its key; the second fills the buffers, stream-ordered
+ * (INTEGRATION.md §5). */
+int airice_table_cache_stats(int out[6]);
+
 #ifdef __cplusplus
 }
 #endif

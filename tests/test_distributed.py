@@ -157,32 +157,43 @@ def _cfg4_mode_worker(rank, world, port, q, assemble, host_path):
     r = run_sharded_table(g, compute, steps=1, warmup=0, gather_reps=2, assemble=assemble,
                           host_path=host_path)
     if rank == 0:
-        q.put((r["assembled"].clone().numpy(), r["bytes_assembled"], r["assemble"]))
+        q.put((r["assembled"].clone().numpy(), r["bytes_assembled"], r["assemble"],
+               r["host_assembly_error"]))
     dist.barrier()
     if r["host"] is not None:
         r["host"].close()
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("assemble,world", [("host", 2), ("host", 3), ("rccl", 3)])
+@pytest.mark.parametrize("assemble,world", [("host", 2), ("host", 3), ("rccl", 3),
+                                            ("host-fail", 2)])
 def test_gloo_cfg4_mode_assembles_table_bitwise(tmp_path, assemble, world):
+    """host-fail: the root cannot create the shared host table (its directory does not exist):
+    every rank learns it and takes the gather path, instead of the others waiting in a barrier."""
     import oracle
     from tests.conftest import ATMOSPHERE_GZ
     ctx = mp.get_context("spawn")
     q = ctx.SimpleQueue()
     port = _free_port()
-    host_path = str(tmp_path / "airice_host_table")
+    fail = assemble == "host-fail"
+    assemble = "host" if fail else assemble
+    host_path = str(tmp_path / ("no_such_dir" if fail else "") / "airice_host_table")
     procs = [ctx.Process(target=_cfg4_mode_worker, args=(r, world, port, q, assemble, host_path))
              for r in range(world)]
     for p in procs:
         p.start()
-    table, nbytes, mode = q.get()
+    table, nbytes, mode, err = q.get()
     for p in procs:
         p.join(timeout=120)
         assert p.exitcode == 0
     m = oracle.load_atmosphere(ATMOSPHERE_GZ)
     g = oracle.grid_init(-20000.0, 300000.0, 997.0, 90.1, 180.0, 0.37)
     ref = oracle.table_rows(m, g, 0, g.height_steps)
+    if fail:
+        assert mode == "rccl" and err is not None and "FileNotFoundError" in err
+        assemble = "rccl"
+    else:
+        assert err is None
     assert mode == assemble and table.shape == ref.shape
     np.testing.assert_array_equal(table.view(np.int32), ref.view(np.int32))
     if assemble == "host":
