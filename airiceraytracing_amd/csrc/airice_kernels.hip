@@ -28,6 +28,7 @@
 #include "airice.h"
 #include "airice_device.hpp"
 #include "airice_internal.h"
+#include "airice_lean.hpp"
 
 namespace airice {
 
@@ -791,6 +792,69 @@ __device__ __forceinline__ void delta_D2(const Slim& T, const Slim& R, const Ray
   xb = (Rb.L * R.invC) * Rb.rsAL * ((R.Cx - T.Cx) - db);
 }
 
+// delta_D on two segments (T1 -> R1 at ray parameter L1, T2 -> R2 at L2) in one straight-line
+// block, so that each chain hides the other's latency; every value as delta_D forms it.
+__device__ __forceinline__ void delta_D_two(const Slim& T1, const Slim& R1, const RayL& L1,
+                                            const Slim& T2, const Slim& R2, const RayL& L2,
+                                            const double* tab, double& x1, double& x2) {
+  const double syR1 = fast_sqrt(R1.y2 - L1.LL), syT1 = fast_sqrt(T1.y2 - L1.LL);
+  const double syR2 = fast_sqrt(R2.y2 - L2.LL), syT2 = fast_sqrt(T2.y2 - L2.LL);
+  double d1, d2;
+  log_ratio2(R1.Ay - L1.LL + L1.sAL * syR1, T1.Ay - L1.LL + L1.sAL * syT1,
+             R2.Ay - L2.LL + L2.sAL * syR2, T2.Ay - L2.LL + L2.sAL * syT2, tab, d1, d2);
+  x1 = (L1.L * R1.invC) * L1.rsAL * ((R1.Cx - T1.Cx) - d1);
+  x2 = (L2.L * R2.invC) * L2.rsAL * ((R2.Cx - T2.Cx) - d2);
+}
+
+// MinimizeforLaunchAngle's THD in air and in the ice at one angle: air_thd + the ice segment with
+// the segments paired into straight-line blocks -- (Tx layer, ice segment), (ice layer, upper
+// middle layer), (lower middle layer) -- instead of one after the other, and the sums formed in
+// air_thd's order: the same bits with about half the dependent chain.  Which segments a query
+// has is nearly uniform over a wave (the grouping sorts by the layers spanned), so the branches
+// below do not diverge.
+__device__ __forceinline__ void eval_thd_pairs(const DevMedium& M, const IceConsts& I,
+                                               const Query& q, double theta, const double* tab,
+                                               double& thd_air, double& thd_ice) {
+  const bool air = q.top >= q.bot, ice = q.depth_pos != 0;
+  double L = __builtin_nan("");
+  if (air) {
+    const double v1 = sin_start((180 - theta) * M.d2r);
+    L = q.n_rtop * sin_asin(q.ratio * sin_asin(v1));
+  }
+  const RayL RL = ray_L(M.A_air * M.A_air, L);
+  const RayL RLi = ray_L(M.A_ice * M.A_ice, L);
+  double xA = 0.0, xE = 0.0;
+  if (air && ice)
+    delta_D_two(q.tx, q.rtop, RL, slim(I.ice0), q.rx, RLi, tab, xA, xE);
+  else if (air)
+    xA = delta_D(q.tx, q.rtop, RL, tab);
+  else if (ice)
+    xE = delta_D(slim(I.ice0), q.rx, RLi, tab);
+  // layers strictly between (2, then 1; both ends layer bounds) and the ice layer
+  const bool m2 = 2 < q.top && 2 > q.bot, m1 = 1 < q.top && 1 > q.bot, b = q.top > q.bot;
+  double xB = 0.0, x2 = 0.0, x1 = 0.0;
+  if (b) {
+    const Slim Sb = start_slim(M, q.bot);
+    if (m2) {
+      delta_D_two(Sb, q.iceair, RL, slim(M.start[2]), slim(M.stop[2]), RL, tab, xB, x2);
+      if (m1) x1 = delta_D(slim(M.start[1]), slim(M.stop[1]), RL, tab);
+    } else if (m1) {
+      delta_D_two(Sb, q.iceair, RL, slim(M.start[1]), slim(M.stop[1]), RL, tab, xB, x1);
+    } else {
+      xB = delta_D(Sb, q.iceair, RL, tab);
+    }
+  }
+  thd_air = 0.0;
+  if (air) {
+    thd_air += -xA;
+    if (m2) thd_air += -x2;
+    if (m1) thd_air += -x1;
+    if (b) thd_air += -xB;
+  }
+  thd_ice = 0;
+  if (ice) thd_ice += xE;
+}
+
 // MinimizeforLaunchAngle's THD in air and in the ice at two angles (the root finder's bracket
 // ends f(lo), f(hi)), as air_thd + the ice term of solve_root's evaluation site computes each:
 // the same operations in the same order per angle, the two angles' chains interleaved.
@@ -939,6 +1003,21 @@ struct SolveResult {
 
 enum { PH_PROBE = 0, PH_FLO = 1, PH_FHI = 2, PH_EST = 3, PH_G1 = 4, PH_G2 = 5, PH_BISECT = 6,
        PH_DONE = 7 };
+
+#if AIRICE_SORTED_STATS
+// debug build: wave-level executions of the root finder's blocks (tools/solve_blocks.py): the
+// first active lane of each execution counts it, so a block that several lanes of a wave run
+// together counts once -- the count of the wave's instruction streams through it
+__device__ unsigned long long g_dbg_exec[16];
+#define DBG_EXEC(i)                                                                 \
+  do {                                                                              \
+    if ((int)(threadIdx.x & 63) == __builtin_ctzll(__ballot(1))) atomicAdd(&g_dbg_exec[i], 1ull); \
+  } while (0)
+#else
+#define DBG_EXEC(i) \
+  do {              \
+  } while (0)
+#endif
 
 template <bool WAVE = false>
 __device__ __forceinline__ SolveResult solve_root(const DevMedium& M, const IceConsts& I,
@@ -1134,6 +1213,7 @@ __device__ __forceinline__ SolveResult solve_root(const DevMedium& M, const IceC
   unsigned long long tq = __builtin_amdgcn_s_memtime();
 #endif
   while (phase != PH_DONE) {
+    DBG_EXEC(0);
     if constexpr (WAVE) {
       // one query per wave: the phase and the counters are the same on every lane; scalar copies
       // let the phase dispatch branch on SCC instead of exec masks
@@ -1142,6 +1222,7 @@ __device__ __forceinline__ SolveResult solve_root(const DevMedium& M, const IceC
       iter = __builtin_amdgcn_readfirstlane(iter);
     }
     if (phase == PH_BISECT) {
+      DBG_EXEC(1);
       // steps that need no evaluation: an exact zero at a bracket end (GSL returns that end),
       // or a midpoint inside a guard region, whose sign is the region's: lo (left) or hi
       // (right) moves to it, as gsl_root_fsolver_iterate would
@@ -1162,11 +1243,23 @@ __device__ __forceinline__ SolveResult solve_root(const DevMedium& M, const IceC
         const double gl = okL ? gL : -1.0, gr = okR ? gR : __builtin_inf();
         const double lo0 = lo, hi0 = hi;
         bool done = false;
-        {
+        DBG_EXEC(2);
+        // the whole run in closed form when its midpoints are exact (airice_lean.hpp: every
+        // bracket the probe did not move), the same lo, hi, steps and exit as the steps below
+        LeanRun lr;
+        if (lean_closed(lo, hi, iter, gL, gR, okL, okR, tol, lr)) {
+          DBG_EXEC(13);
+          lo = lr.lo;
+          hi = lr.hi;
+          iter += lr.steps;
+          status = lr.maxiter ? (status | AIRICE_SOLVE_MAXITER) : status;
+          done = lr.done;
+        } else {
           // the steps as selects, four per trip, so that the chain is midpoint -> compare ->
           // select without a divergent exit per step
           bool stop = false;
           while (!stop) {
+            DBG_EXEC(3);
 #pragma unroll
             for (int u = 0; u < kLeanUnroll; ++u) {
               const double xm = (lo + hi) / 2.0;
@@ -1197,6 +1290,7 @@ __device__ __forceinline__ SolveResult solve_root(const DevMedium& M, const IceC
     } else if (phase == PH_BISECT) {
       x = (lo + hi) / 2.0;
     } else if (phase == PH_EST) {
+      DBG_EXEC(11);
       // the secant point only steers the search (the root comes from GSL's bisection replay), so
       // its quotient takes v_rcp_f64 (~2^-24 relative) instead of the IEEE division
       x = (est == 0) ? x2 : x2 - f2 * ((x2 - x1) * __builtin_amdgcn_rcp(f2 - f1));
@@ -1217,6 +1311,7 @@ __device__ __forceinline__ SolveResult solve_root(const DevMedium& M, const IceC
       x = lo;
     }
     // the single evaluation site: MinimizeforLaunchAngle (.cc:873-917)
+    DBG_EXEC(4);
     ++n_eval;
     n_inside += (phase == PH_BISECT);
     double thd_air, thd_ice;
@@ -1255,6 +1350,7 @@ __device__ __forceinline__ SolveResult solve_root(const DevMedium& M, const IceC
     }
     const double f = (q.dist - (thd_ice + thd_air));
     if (phase == PH_PROBE) {
+      DBG_EXEC(5);
       if ((!isnan(thd_air) && thd_air > 0) || lo > hi - 0.1) {
         if (hi < 90.001 && hi > 90.00) hi = 90.05;
         phase = PH_FLO;
@@ -1268,6 +1364,7 @@ __device__ __forceinline__ SolveResult solve_root(const DevMedium& M, const IceC
         status |= AIRICE_SOLVE_PROBED;
       }
     } else if (phase == PH_FLO) {
+      DBG_EXEC(6);
       if (!isfinite(f)) {
         status |= AIRICE_SOLVE_NONFINITE_END;
         phase = PH_BISECT;
@@ -1277,8 +1374,10 @@ __device__ __forceinline__ SolveResult solve_root(const DevMedium& M, const IceC
         phase = PH_FHI;
       }
     } else if (phase == PH_FHI) {
+      DBG_EXEC(7);
       on_fhi(f);
     } else if (phase == PH_EST) {
+      DBG_EXEC(8);
       if (est > 0) {
         x0 = x1;
         f0 = f1;
@@ -1303,9 +1402,11 @@ __device__ __forceinline__ SolveResult solve_root(const DevMedium& M, const IceC
         if (est >= 12) phase = PH_BISECT;
       }
     } else if (phase == PH_G1 || phase == PH_G2) {
+      DBG_EXEC(9);
       if (isfinite(f)) guard(x, f);
       phase = phase == PH_G1 ? PH_G2 : PH_BISECT;
     } else {  // PH_BISECT: gsl_root_fsolver_iterate at a midpoint between the guards
+      DBG_EXEC(10);
       if (!exact && isfinite(f)) guard(x, f);
       ++iter;
       bool frozen = false;
@@ -1821,6 +1922,7 @@ __global__ __launch_bounds__(kSortedBlock, kRootsWaves) void roots_sorted_kernel
   __syncthreads();
   const long long ks = (long long)blockIdx.x * kSortedBlock + threadIdx.x;
   if (ks >= *grouped) return;  // past the queries with a bucket
+  DBG_EXEC(12);
   double thR;
   const Geometry g = load_rec<IN>(M, Q, recs[ks], thR);
   const SolveResult r = solve_root(M, I, g, thR, park.exact != 0, &s_logtab[0][0]);
@@ -2435,6 +2537,20 @@ static int angle_sines_cached(const DevMedium& M, const TableArgs& A, hipStream_
   *out = static_cast<const double*>(p);
   return rc;
 }
+
+#if AIRICE_SORTED_STATS
+int debug_exec_counters(unsigned long long* out, int n, int reset) {
+  if (n > 16) n = 16;
+  if (hipDeviceSynchronize() != hipSuccess ||
+      hipMemcpyFromSymbol(out, HIP_SYMBOL(g_dbg_exec), sizeof(unsigned long long) * n) != hipSuccess)
+    return AIRICE_EHIP;
+  if (reset) {
+    static const unsigned long long z[16] = {};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_dbg_exec), z, sizeof(z)) != hipSuccess) return AIRICE_EHIP;
+  }
+  return AIRICE_OK;
+}
+#endif
 
 void table_cache_stats(int out[6]) {
   std::lock_guard<std::mutex> lock(grid_cache_mutex());

@@ -303,6 +303,17 @@ int lookup_fallback_one(const airice_medium* m, double src_cm, double dist_cm, d
 
 using namespace airice;
 
+#if defined(AIRICE_SORTED_STATS) && AIRICE_SORTED_STATS
+// debug build only (-DAIRICE_SORTED_STATS=1, tools/solve_blocks.py): wave-level executions of the
+// root finder's blocks
+namespace airice {
+int debug_exec_counters(unsigned long long* out, int n, int reset);
+}
+extern "C" int airice_debug_exec_counters(unsigned long long* out, int n, int reset) {
+  return airice::debug_exec_counters(out, n, reset);
+}
+#endif
+
 extern "C" int airice_table_cache_stats(int out[6]) {
   if (out == nullptr) {
     set_error("airice_table_cache_stats: out is null");

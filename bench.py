@@ -95,7 +95,17 @@ def parse():
                    help="wall time of each CPU-baseline sample")
     p.add_argument("--parity-stride", type=int, default=97,
                    help="every k-th query of the timed batches is checked against the oracle")
-    return p.parse_args()
+    p.add_argument("--only", choices=("table", "solve", "trace", "lookup", "multi", "cold", "pcie",
+                                      "default-grid", "cfg4", "scalar"), default=None,
+                   help="run the headline table steps and this one line item only, no CPU legs "
+                        "(per-workload rocprofv3 summaries, tools/gpu_profiles.sh)")
+    a = p.parse_args()
+    if a.only is not None:
+        a.no_cpu = True
+        for item in ("solve", "trace", "lookup", "multi", "cold", "pcie", "default-grid", "cfg4",
+                     "scalar"):
+            setattr(a, "no_" + item.replace("-", "_"), item != a.only)
+    return a
 
 
 def load_pmc() -> dict:
@@ -145,7 +155,8 @@ def counter_roofline(kernel_key: str, units: int, kernel_ms: float, pmc: dict,
                        "x 64 lanes) per unit from " + os.path.relpath(PMC_FILE, ROOT),
         "fp64_lane_ops_per_unit": ops_per_unit,
         "valu_insts_per_unit": p.get("valu_insts_per_unit"),
-        "valu_busy_pct": p.get("valu_busy_pct"),
+        "fp64_pipe_busy_pct": p.get("fp64_pipe_busy_pct"),
+        "wave_cycle_shares": p.get("wave_cycle_shares"),
         "units_per_launch": units, "kernel_ms": kernel_ms,
         "hbm_bytes_per_launch_algorithmic": algorithmic_bytes_per_unit * units,
         "hbm_GBps_algorithmic": algorithmic_bytes_per_unit * units / (kernel_ms * 1e-3) / 1e9
@@ -718,8 +729,8 @@ def table_cold(solver, grid, table, stream, rank, warm_kernel_ms, builds: int = 
     before = _lib.table_cache_stats()
     d_wall, d_ev = run(new_depths)
     after = _lib.table_cache_stats()
-    new_grids = [make_grid(CFG2["depth_cm"], CFG2["ice_cm"] + 1.0 * (a + 1 + 100 * rank),
-                           CFG2["height_step"], CFG2["start_angle"] + 1e-7 * (a + 1),
+    new_grids = [make_grid(CFG2["depth_cm"], CFG2["ice_cm"] - 1.0 * (a + 1 + 100 * rank),
+                           CFG2["height_step"], CFG2["start_angle"] - 1e-7 * (a + 1),
                            CFG2["stop_angle"], CFG2["angle_step"]) for a in range(builds)]
     assert all(g.n_rays == grid.n_rays for g in new_grids + new_depths)
     g_wall, g_ev = run(new_grids)

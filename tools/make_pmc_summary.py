@@ -3,7 +3,19 @@
 HBM bytes follow MI355X_MICROARCH.md §HBM: WRITE_SIZE/FETCH_SIZE are KiB (x1024); FETCH_SIZE
 under-reports wide coalesced streaming reads by 2x on gfx950 -- the kernels here read only
 kernel arguments and <=24 B per query, so FETCH is reported both raw and doubled (upper bound).
-VALU busy uses the gfx9 formula 100*SQ_ACTIVE_INST_VALU*4/SIMDs/(GRBM_GUI_ACTIVE/XCDs).
+
+Busy figures, both bounded by construction:
+* fp64_pipe_busy_pct = 100 x (executed FP64 VALU instructions x 4 cycles) / (1024 SIMDs x the
+  launch's cycles, GRBM_GUI_ACTIVE / 8 XCDs): a SIMD completes at most one wave64 FP64
+  instruction every 4 cycles (16 FP64 lanes per clock, the FP64 vector peak), so this cannot
+  exceed 100; it is the roofline fraction at the clock the launch actually ran at.
+* wave_cycle_shares: SQ_ACTIVE_INST_ANY (issuing), SQ_WAIT_INST_ANY (ready to issue but stalled
+  on a dependency or a busy pipe) and SQ_WAIT_ANY (parked on s_waitcnt / barrier) over
+  SQ_WAVE_CYCLES -- disjoint parts of every wave's lifetime (MI355X_MICROARCH.md §rocprofv3).
+(The earlier VALU-busy, 100 x SQ_ACTIVE_INST_VALU x 4 / SIMDs / (GRBM_GUI_ACTIVE / XCDs), priced
+every VALU instruction at 4 cycles -- the FP64 cost -- and read 100.8 % on the cfg4 launch, where
+the cheaper integer / move / select instructions share the SIMD: it is not a bounded busy and is
+no longer reported.)
 """
 import json
 import sys
@@ -26,13 +38,19 @@ def derive(name, c, n_units, kernel_ns=None):
     f64 = sum(c.get(k, 0.0) for k in ("SQ_INSTS_VALU_ADD_F64", "SQ_INSTS_VALU_MUL_F64",
                                        "SQ_INSTS_VALU_FMA_F64", "SQ_INSTS_VALU_TRANS_F64"))
     grbm = c.get("GRBM_GUI_ACTIVE", 0.0)
+    wc = c.get("SQ_WAVE_CYCLES", 0.0)
     d = {
         "units_per_launch": n_units,
         "valu_insts_per_unit": c.get("SQ_INSTS_VALU", 0.0) * 64 / n_units,
         "fp64_valu_insts_per_unit": f64 * 64 / n_units,
         "fp64_fma_share": c.get("SQ_INSTS_VALU_FMA_F64", 0.0) / f64 if f64 else None,
-        "valu_busy_pct": 100 * c.get("SQ_ACTIVE_INST_VALU", 0.0) * 4 / SIMDS / (grbm / XCDS)
-        if grbm else None,
+        "fp64_pipe_busy_pct": 100 * f64 * 4 / SIMDS / (grbm / XCDS) if grbm else None,
+        "wave_cycle_shares": {
+            "issuing": c["SQ_ACTIVE_INST_ANY"] / wc,
+            "stalled_ready": c["SQ_WAIT_INST_ANY"] / wc,
+            "parked_waitcnt_barrier": c["SQ_WAIT_ANY"] / wc,
+        } if wc and "SQ_ACTIVE_INST_ANY" in c and "SQ_WAIT_INST_ANY" in c and "SQ_WAIT_ANY" in c
+        else None,
         "waves": waves,
         "write_bytes_per_launch": c.get("WRITE_SIZE", 0.0) * 1024,
         "fetch_bytes_per_launch_raw": c.get("FETCH_SIZE", 0.0) * 1024,
