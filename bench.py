@@ -56,7 +56,64 @@ SURVEY_REFERENCE_PROBE = {
 PMC_FILE = os.path.join(ROOT, "profiles", "pmc_summary.json")
 
 
-def parse():
+class HipBackend:
+    """Where the table path of the bench runs: libairice.so's kernels on this process's GPU (the
+    product).  The table-path code below (headline steps, the sharded assembly, the cfg4 item)
+    only calls these methods, so tests/bench_rehearsal.py can run the same multi-rank flow on CPU
+    ranks over gloo with a stand-in for the kernels."""
+    is_gpu = True
+
+    def __init__(self, local_rank: int):
+        import torch
+        from airiceraytracing_amd import AirIceSolver
+        ndev = torch.cuda.device_count()
+        self.dev = torch.device(f"cuda:{local_rank % max(1, ndev)}")
+        torch.cuda.set_device(self.dev)
+        self.solver = AirIceSolver()
+        self.stream = torch.cuda.current_stream()
+
+    def event(self):
+        import torch
+        return torch.cuda.Event(enable_timing=True)
+
+    def sync(self) -> None:
+        import torch
+        torch.cuda.synchronize()
+
+    def release(self) -> None:
+        import torch
+        torch.cuda.synchronize()
+        torch.cuda.empty_cache()
+
+    def table(self, grid, out, row_begin: int = 0, row_count=None, ld=None) -> None:
+        self.solver.table_device(grid, out, None, row_begin=row_begin, row_count=row_count, ld=ld,
+                                 stream=self.stream)
+
+    def table_to_host(self, slab, cnt: int, host, first: int) -> None:
+        """host[:, first:first+cnt] = slab[:, :cnt] (airice_table_to_host: one D2H copy per
+        column into page-locked rows)."""
+        import ctypes
+        from airiceraytracing_amd import _lib
+        from airiceraytracing_amd.solver import _stream_handle
+        _lib.check(_lib.lib().airice_table_to_host(
+            ctypes.c_void_p(slab.data_ptr()), slab.stride(0), cnt,
+            ctypes.c_void_p(host.data_ptr() + 4 * first), host.stride(0),
+            _stream_handle(self.stream)), "airice_table_to_host")
+
+    def host_register(self, ptr: int, nbytes: int) -> None:
+        import ctypes
+        from airiceraytracing_amd import _lib
+        _lib.check(_lib.lib().airice_host_register(ctypes.c_void_p(ptr), nbytes),
+                   "airice_host_register")
+
+    def host_unregister(self, ptr: int) -> None:
+        import ctypes
+        from airiceraytracing_amd import _lib
+        _lib.check(_lib.lib().airice_host_unregister(ctypes.c_void_p(ptr)),
+                   "airice_host_unregister")
+
+
+def parse(argv=None):
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=50)
@@ -83,9 +140,15 @@ def parse():
     p.add_argument("--cfg4-reps", type=int, default=3)
     p.add_argument("--cfg4-host", choices=("auto", "none"), default="auto",
                    help="assemble the cfg4 table in host memory (default) or keep it in HBM")
+    p.add_argument("--cfg4-host-path", default=None,
+                   help="N>1: the node-shared host table's file (default: a new file in /dev/shm)")
     p.add_argument("--workload", choices=("cfg2", "cfg4"), default="cfg2",
                    help="N>1 sharded headline: the cfg2 grid refined N-fold (weak scaling, "
                         "default) or the cfg4 fine table split over the N GPUs (strong scaling)")
+    p.add_argument("--height-step", type=float, default=CFG2["height_step"],
+                   help="TxH step (m) of the headline cfg2 grid (BASELINE cfg2: 20)")
+    p.add_argument("--cfg4-height-step", type=float, default=CFG4["height_step"],
+                   help="TxH step (m) of the cfg4 fine table (BASELINE cfg4: 1)")
     p.add_argument("--lookup-n", type=int, default=1_000_000)
     p.add_argument("--trace-n", type=int, default=10_000_000)
     p.add_argument("--no-trace", action="store_true", help="skip the cfg5 pythonwrapper line item")
@@ -99,7 +162,7 @@ def parse():
                                       "default-grid", "cfg4", "scalar"), default=None,
                    help="run the headline table steps and this one line item only, no CPU legs "
                         "(per-workload rocprofv3 summaries, tools/gpu_profiles.sh)")
-    a = p.parse_args()
+    a = p.parse_args(argv)
     if a.only is not None:
         a.no_cpu = True
         for item in ("solve", "trace", "lookup", "multi", "cold", "pcie", "default-grid", "cfg4",
@@ -179,14 +242,20 @@ def ocml_priced(grid, rays: int, kernel_ms: float) -> dict:
             "note": "library-priced work model, not executed instructions"}
 
 
-def main():
-    args = parse()
+def main(argv=None, make_backend=None, json_path=None):
+    """The bench.  argv: command-line arguments (default sys.argv); make_backend(local_rank):
+    where the table path runs (default HipBackend); json_path: write rank 0's JSON line there
+    instead of to stdout."""
+    args = parse(argv)
+    CFG2["height_step"] = args.height_step
+    CFG4["height_step"] = args.cfg4_height_step
     os.environ.setdefault("NCCL_DEBUG", "WARN")
     # stdout carries exactly one JSON line (rank 0): RCCL prints its version banner to fd 1 at
     # communicator init, so fd 1 points at stderr for the whole run and the JSON line goes to the
     # saved descriptor
     sys.stdout.flush()
-    json_fd = os.dup(1)
+    json_fd = os.dup(1) if json_path is None else os.open(json_path, os.O_WRONLY | os.O_CREAT |
+                                                         os.O_TRUNC, 0o644)
     os.dup2(2, 1)
     import torch
     import torch.distributed as dist
@@ -196,9 +265,8 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     distributed = "RANK" in os.environ  # launched by torch.distributed.run (any world size)
     backend = os.environ.get("AIRICE_DIST_BACKEND", "nccl")  # gloo: rehearsal ranks sharing a GPU
-    ndev = torch.cuda.device_count()
-    dev = torch.device(f"cuda:{local % max(1, ndev)}")
-    torch.cuda.set_device(dev)
+    be = (make_backend or HipBackend)(local)
+    dev = be.dev
     if distributed:
         if backend == "nccl":
             dist.init_process_group(backend="nccl", device_id=dev)
@@ -209,9 +277,9 @@ def main():
     from airiceraytracing_amd import AirIceSolver, make_grid
     from airiceraytracing_amd import _lib
     from airiceraytracing_amd.distributed import run_sharded_table, sharded_step_grid_step
-    solver = AirIceSolver()
+    solver = be.solver
     pmc = load_pmc()
-    stream = torch.cuda.current_stream()
+    stream = be.stream
     sharded = world > 1 and args.mode == "sharded"
 
     def barrier():
@@ -219,7 +287,7 @@ def main():
             dist.barrier()
 
     if args.cfg4_only:
-        rep = table_cfg4(args, solver, world, rank, dev, stream, distributed, coll_dev, pmc)
+        rep = table_cfg4(args, be, world, rank, distributed, coll_dev, pmc)
         if rank == 0:
             os.write(json_fd, (json.dumps({"table_cfg4": rep}) + "\n").encode())
         if distributed:
@@ -232,7 +300,7 @@ def main():
         # the cfg4 fine table split over the N GPUs (strong scaling): K builds of every rank's
         # TxH-row slab, then one host assembly (table_cfg4)
         args.cfg4_reps = args.steps
-        rep4 = table_cfg4(args, solver, world, rank, dev, stream, distributed, coll_dev, pmc)
+        rep4 = table_cfg4(args, be, world, rank, distributed, coll_dev, pmc)
         grid = make_grid(CFG4["depth_cm"], CFG4["ice_cm"], CFG4["height_step"],
                          CFG4["start_angle"], CFG4["stop_angle"], CFG4["angle_step"])
         depth_cm = CFG4["depth_cm"]
@@ -252,15 +320,14 @@ def main():
         depth_cm = CFG2["depth_cm"] - 1000.0 * rank  # replicas: rank r's antenna at 200 + 10 r m
         grid = make_grid(depth_cm, CFG2["ice_cm"], CFG2["height_step"], CFG2["start_angle"],
                          CFG2["stop_angle"], CFG2["angle_step"])
-    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    ev0, ev1 = be.event(), be.event()
     if not cfg4_headline:
         shard_rep = None
     if cfg4_headline:
         pass
     elif sharded:
         def compute(begin, count, slab):
-            solver.table_device(grid, slab, None, row_begin=begin, row_count=count,
-                                ld=slab.shape[1], stream=stream)
+            be.table(grid, slab, row_begin=begin, row_count=count, ld=slab.shape[1])
 
         # the kernel time comes from a HIP-event pair around the K launches on the launch
         # stream, recorded inside compute's stream order
@@ -275,7 +342,7 @@ def main():
                 ev1.record(stream)
 
         r = run_sharded_table(grid, timed_compute, args.steps, args.warmup, device=dev,
-                              coll_device=coll_dev, sync=torch.cuda.synchronize, gather_reps=3)
+                              coll_device=coll_dev, sync=be.sync, gather_reps=3)
         elapsed = elapsed_bar = r["elapsed_s"]
         n_local = r["rays_this_rank"]
         total_rays = grid.n_rays * args.steps
@@ -294,8 +361,8 @@ def main():
         if rank == 0:
             # the assembled table equals the whole grid built on one GPU, bit for bit
             full = torch.empty((11, grid.n_rays), dtype=torch.float32, device=dev)
-            solver.table_device(grid, full, None, stream=stream)
-            torch.cuda.synchronize()
+            be.table(grid, full)
+            be.sync()
             shard_rep["assembled_bitwise_equal_single_gpu"] = bool(
                 torch.equal(r["assembled"].to(dev).view(torch.int32), full.view(torch.int32)))
             del full
@@ -305,34 +372,35 @@ def main():
         table = torch.empty((11, n_local), dtype=torch.float32, device=dev)
 
         def step():
-            solver.table_device(grid, table, None, stream=stream)
+            be.table(grid, table)
 
         for _ in range(args.warmup):
             step()
-        torch.cuda.synchronize()
+        be.sync()
         barrier()
-        torch.cuda.synchronize()
+        be.sync()
         t0 = time.perf_counter()
         ev0.record(stream)
         for _ in range(args.steps):
             step()
         ev1.record(stream)
-        torch.cuda.synchronize()
+        be.sync()
         # the clock stops when this rank's K steps are done; the trailing barrier (an RCCL
         # all-reduce, ~0.1-0.3 ms) closes the bracket but is not step work -- the max over ranks
         # below covers rank skew.  Both figures are reported.
         elapsed = time.perf_counter() - t0
         barrier()
-        torch.cuda.synchronize()
+        be.sync()
         elapsed_bar = time.perf_counter() - t0
         el = torch.tensor([elapsed, elapsed_bar], dtype=torch.float64, device=coll_dev)
         if distributed:
             dist.all_reduce(el, op=dist.ReduceOp.MAX)
         elapsed, elapsed_bar = (float(x) for x in el.tolist())
         total_rays = world * n_local * args.steps
-    torch.cuda.synchronize()
+    be.sync()
     if not cfg4_headline:
-        kern_ms = ev0.elapsed_time(ev1) / args.steps
+        # (a rank whose slab is empty recorded no events; only rank 0 reports, and it has rows)
+        kern_ms = ev0.elapsed_time(ev1) / args.steps if n_local > 0 else None
     value = total_rays / elapsed
     extra = {}
 
@@ -585,8 +653,7 @@ def main():
                                        "value": gd.n_rays / (dms * 1e-3), "unit": "rays/s"}
         del td
     if not args.no_cfg4:
-        extra["table_cfg4"] = table_cfg4(args, solver, world, rank, dev, stream, distributed,
-                                         coll_dev, pmc)
+        extra["table_cfg4"] = table_cfg4(args, be, world, rank, distributed, coll_dev, pmc)
     if rank == 0 and not args.no_scalar:
         extra["scalar_latency_us"] = scalar_latencies(args)
 
@@ -649,7 +716,7 @@ def main():
 
     roof = counter_roofline("table_kernel_cfg4" if cfg4_headline else "table_kernel", n_local,
                             kern_ms, pmc, 44.0)
-    roof["ocml_priced"] = ocml_priced(grid, n_local, kern_ms)
+    roof["ocml_priced"] = ocml_priced(grid, n_local, kern_ms) if kern_ms else None
 
     if rank == 0:
         if cfg4_headline:
@@ -748,56 +815,47 @@ def table_cold(solver, grid, table, stream, rank, warm_kernel_ms, builds: int = 
         "headline_kernel_ms": warm_kernel_ms}
 
 
-def cfg4_check_rows(height_steps: int) -> list[int]:
+def cfg4_check_rows(height_steps: int, step: float = 1.0) -> list[int]:
     """Rows of the cfg4 table checked against the oracle: the first and last rows, the rows on
     either side of each atmosphere-layer bound the Tx heights cross (23141.75, 8363.54 and
-    3217.48 m: rows 76858/76859, 91636/91637, 96782/96783), and evenly spaced rows between."""
-    rows = {0, 1, height_steps - 1, 76858, 76859, 91636, 91637, 96782, 96783}
+    3217.48 m: at the 1 m step rows 76858/76859, 91636/91637, 96782/96783), and evenly spaced rows
+    between."""
+    rows = {0, 1, height_steps - 1}
+    for bound in (23141.75, 8363.54, 3217.48):
+        r = int((100000.0 - bound) // step)
+        rows |= {r, r + 1}
     rows |= {int(r) for r in np.linspace(0, height_steps - 1, 6)}
     return sorted(r for r in rows if 0 <= r < height_steps)
 
 
-def table_cfg4(args, solver, world, rank, dev, stream, distributed, coll_dev, pmc) -> dict:
+def table_cfg4(args, be, world, rank, distributed, coll_dev, pmc) -> dict:
     """BASELINE cfg4, the fine table (872,135,991 rays, 38.4 GB): built in HBM (N=1: the whole
     grid on one GPU; N>1: contiguous TxH-row slabs, one per GPU), timed over cfg4_reps builds, then
     assembled in host memory where the reference keeps AllTableAllAntData (.cc:2079-2136): one
     2-D DMA per GPU (airice_table_to_host) into page-locked host pages -- a private buffer at N=1,
     a node-shared mapping (distributed.SharedHostTable) that every rank fills in parallel at N>1.
     Rank 0 checks cfg4_check_rows() of the host table against the oracle."""
-    import ctypes
     import torch
     import torch.distributed as dist
-    from airiceraytracing_amd import _lib, make_grid
+    from airiceraytracing_amd import make_grid
     from airiceraytracing_amd.distributed import run_sharded_table, shard_rows
-    L = _lib.lib()
     g = make_grid(CFG4["depth_cm"], CFG4["ice_cm"], CFG4["height_step"], CFG4["start_angle"],
                   CFG4["stop_angle"], CFG4["angle_step"])
     asteps, n = g.angle_steps, g.n_rays
     begin, count, per = shard_rows(g.table_rows, world, rank)
-    from airiceraytracing_amd.solver import _stream_handle
-    h = _stream_handle(stream)
-    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    dev, stream = be.dev, be.stream
+    ev0, ev1 = be.event(), be.event()
     st = {"i": 0}
 
     def compute(b, c, slab):
         if st["i"] == 1:
             ev0.record(stream)
-        solver.table_device(g, slab, None, row_begin=b, row_count=c, ld=slab.shape[1],
-                            stream=stream)
+        be.table(g, slab, row_begin=b, row_count=c, ld=slab.shape[1])
         st["i"] += 1
         if st["i"] == 1 + args.cfg4_reps:
             ev1.record(stream)
 
-    def host_copy(slab, cnt, host, first):
-        _lib.check(L.airice_table_to_host(ctypes.c_void_p(slab.data_ptr()), slab.stride(0), cnt,
-                                          ctypes.c_void_p(host.data_ptr() + 4 * first),
-                                          host.stride(0), h), "airice_table_to_host")
-
-    def register(ptr, nbytes):
-        _lib.check(L.airice_host_register(ctypes.c_void_p(ptr), nbytes), "airice_host_register")
-
-    def unregister(ptr):
-        _lib.check(L.airice_host_unregister(ctypes.c_void_p(ptr)), "airice_host_unregister")
+    host_copy, register, unregister = be.table_to_host, be.host_register, be.host_unregister
 
     want_host = args.cfg4_host != "none"
     rep = {"metric": "cfg4 fine table rays/s (BASELINE cfg4: MakeRayTracingTable TxH 100000->3000 "
@@ -810,13 +868,15 @@ def table_cfg4(args, solver, world, rank, dev, stream, distributed, coll_dev, pm
         # every rank takes the same assembly path: rank 0 checks that /dev/shm can hold the shared
         # host table and broadcasts the decision with the file name (a rank failing alone inside
         # the collective sequence would leave the others waiting)
-        plan = [f"/dev/shm/airice_cfg4_{os.getpid()}_{int(time.time())}", mode, None]
+        plan = [args.cfg4_host_path or f"/dev/shm/airice_cfg4_{os.getpid()}_{int(time.time())}",
+                mode, None]
         if rank == 0 and mode == "host":
             try:
-                fs = os.statvfs("/dev/shm")
+                fs = os.statvfs(os.path.dirname(plan[0]) or ".")
                 free = fs.f_bavail * fs.f_frsize
                 if free < 44 * n * 1.05:
-                    plan[1], plan[2] = "rccl", f"/dev/shm has {free / 1e9:.1f} GB free"
+                    plan[1], plan[2] = "rccl", (f"{os.path.dirname(plan[0])} has "
+                                                f"{free / 1e9:.1f} GB free")
             except OSError as e:
                 plan[1], plan[2] = "rccl", str(e)
         dist.broadcast_object_list(plan, src=0)
@@ -824,16 +884,17 @@ def table_cfg4(args, solver, world, rank, dev, stream, distributed, coll_dev, pm
         if plan[2] is not None:  # no room for the shared host table: assemble on the root's GPU
             rep["host_assembly_error"] = plan[2]
         r = run_sharded_table(g, compute, args.cfg4_reps, 1, device=dev, coll_device=coll_dev,
-                              sync=torch.cuda.synchronize, gather_reps=1, assemble=mode,
+                              sync=be.sync, gather_reps=1, assemble=mode,
                               host_path=plan[0], host_copy=host_copy,
                               host_register=register, host_unregister=unregister)
-        torch.cuda.synchronize()
+        be.sync()
         mode = r["assemble"]  # "rccl" when a rank could not create or map the shared host table
         if r.get("host_assembly_error"):
             rep["host_assembly_error"] = r["host_assembly_error"]
         build_s = r["elapsed_s"] / args.cfg4_reps
         rep.update({"value": n / build_s, "ms_per_build": build_s * 1e3,
-                    "kernel_ms_rank0": ev0.elapsed_time(ev1) / args.cfg4_reps,
+                    "kernel_ms_rank0": ev0.elapsed_time(ev1) / args.cfg4_reps
+                    if r["rays_this_rank"] > 0 else None,
                     "rows_per_rank": r["rows_per_rank"], "assemble": mode,
                     "assemble_ms": r["gather_s"] * 1e3,
                     "assemble_GBps": r["bytes_assembled"] / r["gather_s"] / 1e9
@@ -849,11 +910,11 @@ def table_cfg4(args, solver, world, rank, dev, stream, distributed, coll_dev, pm
     else:
         slab = torch.empty((11, n), dtype=torch.float32, device=dev)
         compute(0, g.table_rows, slab)  # warm-up (st i: 0 -> 1)
-        torch.cuda.synchronize()
+        be.sync()
         t0 = time.perf_counter()
         for _ in range(args.cfg4_reps):
             compute(0, g.table_rows, slab)
-        torch.cuda.synchronize()
+        be.sync()
         build_s = (time.perf_counter() - t0) / args.cfg4_reps
         kms = ev0.elapsed_time(ev1) / args.cfg4_reps
         rep.update({"value": n / build_s, "ms_per_build": build_s * 1e3, "kernel_ms": kms,
@@ -865,11 +926,11 @@ def table_cfg4(args, solver, world, rank, dev, stream, distributed, coll_dev, pm
             register(host_np.ctypes.data, host_np.nbytes)
             rep["host_alloc_register_s"] = time.perf_counter() - t1
             host_tab = torch.from_numpy(host_np)
-            e2, e3 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e2, e3 = be.event(), be.event()
             e2.record(stream)
             host_copy(slab, n, host_tab, 0)
             e3.record(stream)
-            torch.cuda.synchronize()
+            be.sync()
             d2h_ms = e2.elapsed_time(e3)
             rep.update({"assemble": "host", "assemble_ms": d2h_ms,
                         "assemble_GBps": 44 * n / (d2h_ms * 1e-3) / 1e9,
@@ -887,7 +948,7 @@ def table_cfg4(args, solver, world, rank, dev, stream, distributed, coll_dev, pm
                                                  "Atmosphere.dat.gz"))
         og = oracle.grid_init(CFG4["depth_cm"], CFG4["ice_cm"], CFG4["height_step"],
                               CFG4["start_angle"], CFG4["stop_angle"], CFG4["angle_step"])
-        rows = cfg4_check_rows(g.table_rows)
+        rows = cfg4_check_rows(g.table_rows, CFG4["height_step"])
         worst, nan_ok = 0, True
         for r_ in rows:
             got = host_tab[:, r_ * asteps:(r_ + 1) * asteps].cpu().numpy()
@@ -907,8 +968,7 @@ def table_cfg4(args, solver, world, rank, dev, stream, distributed, coll_dev, pm
     elif want_host:
         unregister(host_np.ctypes.data)
     del host_tab, slab_holder
-    torch.cuda.synchronize()
-    torch.cuda.empty_cache()
+    be.release()
     return rep
 
 
@@ -1004,8 +1064,22 @@ def scalar_cpu_per_call(om, og, ot) -> dict:
     oracle.py_trace_batch(omp, dep, np.full(n, 3000.0), np.minimum(txh, 20000.0), dst * 0.6,
                           nthreads=1)
     res["Py_TraceIceToAir"] = (time.perf_counter() - t0) / n * 1e6
+    # RayTracingFunctions::GetAirPropagationPar (RayTracingFunctions.cc:529-659), the latency
+    # driver's arguments; the oracle's per-call ctypes overhead (~1-2 us) is measured on a no-op op
+    # and subtracted
+    args = [[92 + float(np.fmod(dst[i], 88.0)), float(txh[i]), 3000.0] for i in range(n)]
+    t0 = time.perf_counter()
+    for a in args:
+        oracle.rtf_eval(om, 3, a)  # AIRICE_RTF_AIR_PROPAGATION
+    t_rtf = time.perf_counter() - t0
+    t0 = time.perf_counter()
+    for a in args:
+        oracle.getnz_air(om, a[1])
+    t_call = time.perf_counter() - t0
+    res["RayTracingFunctions::GetAirPropagationPar"] = max(t_rtf - t_call, 0.0) / n * 1e6
     res["note"] = ("oracle restatement, 1 thread, same query distribution; Python loop overhead "
-                   "included only for GetHorizontalDistanceToIntersectionPoint")
+                   "included only for GetHorizontalDistanceToIntersectionPoint; the RTF figure "
+                   "has a ctypes round trip (oracle.getnz_air) subtracted")
     return res
 
 

@@ -199,3 +199,50 @@ def test_gloo_cfg4_mode_assembles_table_bitwise(tmp_path, assemble, world):
     if assemble == "host":
         assert nbytes == ref.size * 4
         assert not os.path.exists(host_path)  # unlinked once every rank had it mapped
+
+
+def _run_bench_ranks(world, argv, json_path, timeout=240):
+    from tests.bench_rehearsal import rank_main
+    ctx = mp.get_context("spawn")
+    port = _free_port()
+    procs = [ctx.Process(target=rank_main, args=(r, world, port, argv, json_path))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=timeout)
+        assert p.exitcode == 0, p.exitcode
+    import json
+    with open(json_path) as f:
+        lines = [ln for ln in f.read().splitlines() if ln.strip()]
+    assert len(lines) == 1
+    return json.loads(lines[0])
+
+
+BENCH8 = ["--gpus", "8", "--steps", "2", "--warmup", "1", "--height-step", "400",
+          "--cfg4-height-step", "2000", "--cfg4-reps", "1", "--no-cpu", "--no-solve", "--no-trace",
+          "--no-lookup", "--no-multi", "--no-scalar", "--no-default-grid", "--no-cold", "--no-pcie"]
+
+
+@pytest.mark.parametrize("cfg4_host", ["shared", "fail"])
+def test_gloo_world8_bench_flow(tmp_path, cfg4_host):
+    """The whole bench.py N>1 flow (bench.main) at world size 8 over gloo, each rank's table slabs
+    from the oracle (tests/bench_rehearsal.py): one JSON line with n_gpus 8, the sharded cfg2-style
+    table assembled bit for bit equal to the whole grid built on one rank, and the cfg4 item sharded
+    over 8 ranks -- assembled in a node-shared host table, or, when that file cannot be created
+    (``fail``: its path is an existing directory), by the gather every rank falls back to."""
+    host_path = tmp_path / "cfg4_host_table"
+    if cfg4_host == "fail":
+        host_path.mkdir()
+    line = _run_bench_ranks(8, BENCH8 + ["--cfg4-host-path", str(host_path)],
+                            str(tmp_path / "bench.json"))
+    assert line["n_gpus"] == 8 and line["steps"] == 2 and line["scaling"] == "weak"
+    assert line["value"] > 0 and line["ms_per_step"] > 0
+    assert line["sharded"]["assembled_bitwise_equal_single_gpu"] is True
+    assert line["sharded"]["rows_per_rank"] == -(-1941 // 8)
+    c4 = line["table_cfg4"]
+    assert c4["n_gpus"] == 8 and c4["rows"] == 49 and c4["value"] > 0
+    if cfg4_host == "fail":
+        assert c4["assemble"] == "rccl" and "IsADirectoryError" in c4["host_assembly_error"]
+    else:
+        assert c4["assemble"] == "host" and "host_assembly_error" not in c4
