@@ -172,6 +172,9 @@ __device__ __forceinline__ double sel_lower_ratio(const IceConsts& I, int il) {
 // the lower layers then run as one loop over a uniform layer index, their SegConst read with
 // scalar loads one layer at a time, instead of one inlined copy per layer.  Same operations in
 // the same order either way.
+// A1: the launch's A_air is exactly 1 (MultiRayAirIceRefraction.h:99, the table's medium), so
+// the products with it are dropped (exact: x * 1.0 == x).
+template <bool A1 = false>
 __device__ __forceinline__ void ray_solution_row(const DevMedium& M, const IceConsts& I,
                                                  const RowConst& rc, double theta, bool in_ice,
                                                  double* d, bool want_inc,
@@ -181,14 +184,15 @@ __device__ __forceinline__ void ray_solution_row(const DevMedium& M, const IceCo
   const double H = rc.H;
   const int top = rc.top;
   const int bot = I.bot;
-  const double A2 = M.A_air * M.A_air;
+  const double Aair = A1 ? 1.0 : M.A_air;
+  const double A2 = Aair * Aair;
   // sine of StartAngle (.cc:1863); v_start: the same value, formed by the caller
   double v = v_start != nullptr ? *v_start : sin_start((180 - theta) * M.d2r);
   double thd_air = 0.0, t_air = 0.0, geo_air = 0.0;
   const bool any = rc.any != 0;
   if (any) {
     // n_layer1 == Getnz_air(StartHeight) == nzTx: Snell into a layer is the identity
-    const Segment s = segment_const(rc.seg, M.A_air, A2, sin_asin(v), true, v, tab);
+    const Segment s = segment_const(rc.seg, Aair, A2, sin_asin(v), true, v, tab);
     thd_air += s.thd;
     t_air += s.t;
     geo_air += s.geo;
@@ -199,7 +203,7 @@ __device__ __forceinline__ void ray_solution_row(const DevMedium& M, const IceCo
     for (int il = top_hi - 1; il >= bot; --il) {
       if (il < top) {
         // v is a segment's output sine here (already sin_asin'd: sin_asin is idempotent)
-        const Segment s = segment_const(I.lower[il], M.A_air, A2, v, true, v, tab);
+        const Segment s = segment_const(I.lower[il], Aair, A2, v, true, v, tab);
         thd_air += s.thd;
         t_air += s.t;
         geo_air += s.geo;
@@ -209,7 +213,7 @@ __device__ __forceinline__ void ray_solution_row(const DevMedium& M, const IceCo
 #pragma unroll
     for (int il = kMaxLayers - 2; il >= 0; --il) {
       if (il >= top || il < bot) continue;
-      const Segment s = segment_const(I.lower[il], M.A_air, A2, v, true, v, tab);
+      const Segment s = segment_const(I.lower[il], Aair, A2, v, true, v, tab);
       thd_air += s.thd;
       t_air += s.t;
       geo_air += s.geo;
@@ -309,6 +313,7 @@ __device__ __forceinline__ double table_angle(const TableArgs& G, int iang) {
   return th;
 }
 
+template <bool A1>
 __device__ __forceinline__ void table_ray(const DevMedium& M, const IceConsts& I,
                                           const TableArgs& G, const RowConst& rc, int r, int k,
                                           float* __restrict__ table, double* __restrict__ full,
@@ -323,7 +328,7 @@ __device__ __forceinline__ void table_ray(const DevMedium& M, const IceConsts& I
     vs = G.vs[iang];
   else
     vs = sin_start((180 - th) * M.d2r);
-  ray_solution_row(M, I, rc, th, G.in_ice != 0, d, full != nullptr, tab, top_hi, &vs);
+  ray_solution_row<A1>(M, I, rc, th, G.in_ice != 0, d, full != nullptr, tab, top_hi, &vs);
   const size_t ld = G.ld;
   // AllTableAllAntData columns (.cc:2101-2111): the column base is wave-uniform, the lane's byte
   // offset fits 32 bits (k < 2^30 per launch)
@@ -360,7 +365,7 @@ __device__ __forceinline__ void table_ray(const DevMedium& M, const IceConsts& I
 // when capped at 64, and runs 2.7x / 7x slower -- and two rays per lane.)
 // The work of one table block (kTableBlock rays of one antenna's grid), shared by the single- and
 // the multi-antenna kernels.
-template <bool TRACE>
+template <bool TRACE, bool A1>
 __device__ __forceinline__ void table_block(const DevMedium& M, const IceConsts& I,
                                             const TableArgs& G, float* __restrict__ table,
                                             double* __restrict__ full,
@@ -399,7 +404,7 @@ __device__ __forceinline__ void table_block(const DevMedium& M, const IceConsts&
     __builtin_assume(top_hi >= 0);
     if (k < G.n) {
       const int r = ray_row(G, k);
-      table_ray(M, I, G, rows[r - r0], r, k, table, full, &s_logtab[0][0], top_hi);
+      table_ray<A1>(M, I, G, rows[r - r0], r, k, table, full, &s_logtab[0][0], top_hi);
     }
   }
   if (TRACE && lane == 0) {
@@ -411,13 +416,13 @@ __device__ __forceinline__ void table_block(const DevMedium& M, const IceConsts&
 }
 
 // waves_per_eu(8): 64 VGPRs at 8 waves/SIMD, measured on par or slightly ahead of 67 VGPRs at 7.
-template <bool TRACE = false>
+template <bool TRACE, bool A1>
 __global__ __launch_bounds__(kTableBlock) __attribute__((amdgpu_waves_per_eu(kTableWaves, kTableWaves))) void table_kernel(
                                                    DevMedium M, IceConsts I, TableArgs G,
                                                    float* __restrict__ table,
                                                    double* __restrict__ full,
                                                    WaveTrace* __restrict__ trace) {
-  table_block<TRACE>(M, I, G, table, full, trace, blockIdx.x);
+  table_block<TRACE, A1>(M, I, G, table, full, trace, blockIdx.x);
 }
 
 // Several antennas' tables in one grid (airice_table_launch_multi): the blocks of antenna a are
@@ -431,13 +436,14 @@ struct MultiMap {
   float* table[kMaxAntennas];
 };
 
+template <bool A1>
 __global__ __launch_bounds__(kTableBlock) __attribute__((amdgpu_waves_per_eu(kTableWaves, kTableWaves))) void table_multi_kernel(
     DevMedium M, const IceConsts* __restrict__ Iv, const TableArgs* __restrict__ Gv, MultiMap map) {
   int a = 0;
   for (int j = 1; j < map.n_ant; ++j) a += (int)blockIdx.x >= map.begin[j];
   a = __builtin_amdgcn_readfirstlane(a);
-  table_block<false>(M, Iv[a], Gv[a], map.table[a], nullptr, nullptr,
-                     blockIdx.x - (unsigned)map.begin[a]);
+  table_block<false, A1>(M, Iv[a], Gv[a], map.table[a], nullptr, nullptr,
+                         blockIdx.x - (unsigned)map.begin[a]);
 }
 
 // Row constants of a whole grid (row_consts_cached): one row per lane, the table block's own
@@ -790,69 +796,6 @@ __device__ __forceinline__ void delta_D2(const Slim& T, const Slim& R, const Ray
              R.Ay - Rb.LL + Rb.sAL * syRb, T.Ay - Rb.LL + Rb.sAL * syTb, tab, da, db);
   xa = (Ra.L * R.invC) * Ra.rsAL * ((R.Cx - T.Cx) - da);
   xb = (Rb.L * R.invC) * Rb.rsAL * ((R.Cx - T.Cx) - db);
-}
-
-// delta_D on two segments (T1 -> R1 at ray parameter L1, T2 -> R2 at L2) in one straight-line
-// block, so that each chain hides the other's latency; every value as delta_D forms it.
-__device__ __forceinline__ void delta_D_two(const Slim& T1, const Slim& R1, const RayL& L1,
-                                            const Slim& T2, const Slim& R2, const RayL& L2,
-                                            const double* tab, double& x1, double& x2) {
-  const double syR1 = fast_sqrt(R1.y2 - L1.LL), syT1 = fast_sqrt(T1.y2 - L1.LL);
-  const double syR2 = fast_sqrt(R2.y2 - L2.LL), syT2 = fast_sqrt(T2.y2 - L2.LL);
-  double d1, d2;
-  log_ratio2(R1.Ay - L1.LL + L1.sAL * syR1, T1.Ay - L1.LL + L1.sAL * syT1,
-             R2.Ay - L2.LL + L2.sAL * syR2, T2.Ay - L2.LL + L2.sAL * syT2, tab, d1, d2);
-  x1 = (L1.L * R1.invC) * L1.rsAL * ((R1.Cx - T1.Cx) - d1);
-  x2 = (L2.L * R2.invC) * L2.rsAL * ((R2.Cx - T2.Cx) - d2);
-}
-
-// MinimizeforLaunchAngle's THD in air and in the ice at one angle: air_thd + the ice segment with
-// the segments paired into straight-line blocks -- (Tx layer, ice segment), (ice layer, upper
-// middle layer), (lower middle layer) -- instead of one after the other, and the sums formed in
-// air_thd's order: the same bits with about half the dependent chain.  Which segments a query
-// has is nearly uniform over a wave (the grouping sorts by the layers spanned), so the branches
-// below do not diverge.
-__device__ __forceinline__ void eval_thd_pairs(const DevMedium& M, const IceConsts& I,
-                                               const Query& q, double theta, const double* tab,
-                                               double& thd_air, double& thd_ice) {
-  const bool air = q.top >= q.bot, ice = q.depth_pos != 0;
-  double L = __builtin_nan("");
-  if (air) {
-    const double v1 = sin_start((180 - theta) * M.d2r);
-    L = q.n_rtop * sin_asin(q.ratio * sin_asin(v1));
-  }
-  const RayL RL = ray_L(M.A_air * M.A_air, L);
-  const RayL RLi = ray_L(M.A_ice * M.A_ice, L);
-  double xA = 0.0, xE = 0.0;
-  if (air && ice)
-    delta_D_two(q.tx, q.rtop, RL, slim(I.ice0), q.rx, RLi, tab, xA, xE);
-  else if (air)
-    xA = delta_D(q.tx, q.rtop, RL, tab);
-  else if (ice)
-    xE = delta_D(slim(I.ice0), q.rx, RLi, tab);
-  // layers strictly between (2, then 1; both ends layer bounds) and the ice layer
-  const bool m2 = 2 < q.top && 2 > q.bot, m1 = 1 < q.top && 1 > q.bot, b = q.top > q.bot;
-  double xB = 0.0, x2 = 0.0, x1 = 0.0;
-  if (b) {
-    const Slim Sb = start_slim(M, q.bot);
-    if (m2) {
-      delta_D_two(Sb, q.iceair, RL, slim(M.start[2]), slim(M.stop[2]), RL, tab, xB, x2);
-      if (m1) x1 = delta_D(slim(M.start[1]), slim(M.stop[1]), RL, tab);
-    } else if (m1) {
-      delta_D_two(Sb, q.iceair, RL, slim(M.start[1]), slim(M.stop[1]), RL, tab, xB, x1);
-    } else {
-      xB = delta_D(Sb, q.iceair, RL, tab);
-    }
-  }
-  thd_air = 0.0;
-  if (air) {
-    thd_air += -xA;
-    if (m2) thd_air += -x2;
-    if (m1) thd_air += -x1;
-    if (b) thd_air += -xB;
-  }
-  thd_ice = 0;
-  if (ice) thd_ice += xE;
 }
 
 // MinimizeforLaunchAngle's THD in air and in the ice at two angles (the root finder's bracket
@@ -1716,6 +1659,12 @@ __global__ __launch_bounds__(BS, kRootsWaves) void roots_kernel(DevMedium M, Ice
   constexpr int kRootsBlock = BS;
   __shared__ int s_count[kSortBuckets + 1];
   __shared__ int s_slot[kRootsBlock];
+  const long long k0 = (long long)blockIdx.x * kRootsBlock;
+  const long long kt = k0 + threadIdx.x;
+  // the table lookup's fallback pass: most blocks hold no fallback lane (well under 1 % of a
+  // batch's queries take it) and leave before staging anything
+  if (IN == IN_CM100 && !__syncthreads_or(kt < Q.n && (Q.mask[kt] & AIRICE_LOOKUP_FALLBACK)))
+    return;
   // the log table in LDS (one 16-byte entry per thread), as in table_kernel: every evaluation's
   // log ratios read it instead of global memory
   __shared__ __align__(16) double s_logtab[1 << kLogTableBits][2];
@@ -1723,8 +1672,6 @@ __global__ __launch_bounds__(BS, kRootsWaves) void roots_kernel(DevMedium M, Ice
     s_logtab[t][0] = kLogTable[t][0];
     s_logtab[t][1] = kLogTable[t][1];
   }
-  const long long k0 = (long long)blockIdx.x * kRootsBlock;
-  const long long kt = k0 + threadIdx.x;
   if (threadIdx.x <= kSortBuckets) s_count[threadIdx.x] = 0;
   __syncthreads();
   // bucket of this lane's own query (unused lanes last)
@@ -2596,8 +2543,12 @@ int launch_table(const DevMedium& M, const IceConsts& I, const airice_grid* g, i
     const unsigned blocks = (unsigned)((A.n + kTableBlock - 1) / kTableBlock);
     if (trace_path == nullptr) {
       ktimer_begin(KT_TABLE, st);
-      hipLaunchKernelGGL(table_kernel<false>, dim3(blocks), dim3(kTableBlock), lds, st, M, I, A,
-                         tab, full, nullptr);
+      if (M.A_air == 1.0)
+        hipLaunchKernelGGL((table_kernel<false, true>), dim3(blocks), dim3(kTableBlock), lds, st,
+                           M, I, A, tab, full, nullptr);
+      else
+        hipLaunchKernelGGL((table_kernel<false, false>), dim3(blocks), dim3(kTableBlock), lds, st,
+                           M, I, A, tab, full, nullptr);
       ktimer_end(KT_TABLE, st);
       if (hipGetLastError() != hipSuccess) return AIRICE_EHIP;
       continue;
@@ -2606,8 +2557,8 @@ int launch_table(const DevMedium& M, const IceConsts& I, const airice_grid* g, i
     const long long nw = (long long)blocks * (kTableBlock / 64);
     WaveTrace* dtr = nullptr;
     if (hipMalloc(&dtr, sizeof(WaveTrace) * nw) != hipSuccess) return AIRICE_EHIP;
-    hipLaunchKernelGGL(table_kernel<true>, dim3(blocks), dim3(kTableBlock), lds, st, M, I, A, tab,
-                       full, dtr);
+    hipLaunchKernelGGL((table_kernel<true, false>), dim3(blocks), dim3(kTableBlock), lds, st, M, I,
+                       A, tab, full, dtr);
     std::vector<WaveTrace> h(nw);
     if (hipStreamSynchronize(st) != hipSuccess ||
         hipMemcpy(h.data(), dtr, sizeof(WaveTrace) * nw, hipMemcpyDeviceToHost) != hipSuccess)
@@ -2741,7 +2692,8 @@ int launch_table_multi(const DevMedium& M, const IceConsts* Ih, const airice_gri
   void* dconst = c->dev;
   const size_t lds_bytes = sizeof(RowConst) * (size_t)rpb;
   ktimer_begin(KT_TABLE, st);
-  hipLaunchKernelGGL(table_multi_kernel, dim3((unsigned)blocks), dim3(kTableBlock),
+  auto multi = M.A_air == 1.0 ? table_multi_kernel<true> : table_multi_kernel<false>;
+  hipLaunchKernelGGL(multi, dim3((unsigned)blocks), dim3(kTableBlock),
                      lds_bytes, st, M, static_cast<const IceConsts*>(dconst),
                      reinterpret_cast<const TableArgs*>(static_cast<unsigned char*>(dconst) +
                                                         bytes_i),

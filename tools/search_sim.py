@@ -1,0 +1,165 @@
+"""CPU simulation of the minimizer's root search (solve_root, airice_kernels.hip) to count
+f-evaluations per solve for alternative search / guard strategies (tools only; the GPU's own counts
+come from tools/solve_stats.py).  f(theta) = D - THD(theta) is taken from the oracle's forward ray
+(GetRayTracingSolutions), a close stand-in for MinimizeforLaunchAngle's f; unprobed cfg3 queries.
+
+    python tools/search_sim.py [n]
+"""
+import math
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import oracle  # noqa: E402
+from tests.parity import cfg3_queries  # noqa: E402
+
+TOL = 1e-9
+D2R, R2D = 3.1415927 / 180.0, 180.0 / 3.1415927
+
+
+def f32(x):
+    return float(np.float32(x))
+
+
+def gsl_midpoint_evals(lo, hi, gl, gr, f, fL_sign, counter):
+    """GSL bisection from [lo, hi]; midpoints in (gl, gr) are evaluated (counted), others take the
+    guard region's sign.  Returns the final bracket."""
+    it = 0
+    f_lower_neg = fL_sign < 0
+    while it < 40:
+        xm = (lo + hi) / 2.0
+        if xm <= gl:
+            lo = xm
+        elif xm >= gr:
+            hi = xm
+        else:
+            counter[0] += 1
+            v = f(xm)
+            if v == 0.0:
+                return xm, xm
+            if (v < 0) != f_lower_neg:
+                hi = xm
+                if abs(v) >= counter[1]:
+                    gr = xm
+            else:
+                lo = xm
+                if abs(v) >= counter[1]:
+                    gl = xm
+        it += 1
+        if abs(hi - lo) < TOL * lo:
+            break
+    return lo, hi
+
+
+def solve(f, lo, hi, tau, strategy):
+    n = 0
+
+    def ev(x):
+        nonlocal n
+        n += 1
+        return f(x)
+
+    fL, fR = ev(lo), ev(hi)
+    if not (math.isfinite(fL) and math.isfinite(fR)):
+        return n, None
+    if (fL < 0) == (fR < 0) or abs(fL) < tau or abs(fR) < tau:
+        return n, None
+    gL, gR = lo, hi
+    ul, uh = f32(math.tan(f32((180 - lo) * D2R))), f32(math.tan(f32((180 - hi) * D2R)))
+    un = f32(uh - f32(fR) * f32(f32(uh - ul) / f32(fR - fL)))
+    x2 = 180 - math.atan(un) * R2D
+    x0, f0, x1, f1 = lo, fL, hi, fR
+    f2 = None
+    est = 0
+    W = 16.0 / 2 ** 27
+    while True:
+        if est > 0:
+            x = x2 - f2 * (x2 - x1) / (f2 - f1)
+            if est >= 1:
+                d1 = (x2 - x1) / (f2 - f1)
+                d0 = (x1 - x0) / (f1 - f0)
+                x += f1 * f2 * ((d1 - d0) / (f2 - f0))
+            if not (gL < x < gR):
+                x = 0.5 * (gL + gR)
+            if strategy == "merge" and abs(x - x2) < W / 16 and abs(f2) >= tau:
+                # x2 is a guard on its side (already recorded); one guard on the other side
+                slope = abs((x2 - x1) / (f2 - f1))
+                dl = 4 * tau * slope
+                xo = x + (dl if (f2 < 0) == (fL < 0) else -dl)
+                v = ev(xo)
+                if math.isfinite(v) and abs(v) >= tau and gL < xo < gR:
+                    if (v < 0) == (fL < 0):
+                        gL = xo
+                    else:
+                        gR = xo
+                break
+        else:
+            x = x2
+        if est > 0:
+            x0, f0, x1, f1 = x1, f1, x2, f2
+        x2 = x
+        f2 = ev(x)
+        est += 1
+        if not math.isfinite(f2):
+            break
+        if abs(f2) < tau:
+            dlt = 4.0 * tau * abs((x2 - x1) / (f2 - f1))
+            if 0 < dlt < gR - gL:
+                for xg in (x2 - dlt, x2 + dlt):
+                    v = ev(xg)
+                    if math.isfinite(v) and abs(v) >= tau and gL < xg < gR:
+                        if (v < 0) == (fL < 0):
+                            gL = xg
+                        else:
+                            gR = xg
+            break
+        if gL < x2 < gR:
+            if (f2 < 0) == (fL < 0):
+                gL = x2
+            else:
+                gR = x2
+        if est >= 12:
+            break
+    cnt = [0, tau]
+    gsl_midpoint_evals(lo, hi, gL, gR, f, fL, cnt)
+    return n + cnt[0], est
+
+
+def main():
+    n = int(sys.argv[1]) if len(sys.argv) > 1 else 300
+    m = oracle.load_atmosphere(os.path.join(ROOT, "airiceraytracing_amd", "data",
+                                            "Atmosphere.dat.gz"))
+    txh, dst, dep = cfg3_queries(4 * n, seed=2024)
+    res = {"base": [], "merge": []}
+    ests = []
+    used = 0
+    for i in range(len(txh)):
+        H, D, d = txh[i], dst[i], dep[i]
+        thR = oracle.straight_angle_of(m, H, D, 3000.0, d)
+        lo, hi = thR - 16, thR
+        if lo < 90.001:
+            continue
+
+        def f(t):
+            return D - oracle.ray_solution(m, t, H, 3000.0, d)[2]
+
+        tau = 1e-6 + 1e-10 * abs(D)
+        for s in res:
+            k, e = solve(f, lo, hi, tau, s)
+            res[s].append(k)
+            if s == "base" and e is not None:
+                ests.append(e)
+        used += 1
+        if used >= n:
+            break
+    for s, v in res.items():
+        print(f"{s}: {np.mean(v):.3f} evaluations per solve over {len(v)} queries")
+    print(f"search steps (base) {np.mean(ests):.3f}")
+
+
+if __name__ == "__main__":
+    main()
