@@ -2327,10 +2327,12 @@ static_assert(kMaxAntennas < (int)kCacheSets, "a multi-antenna launch never evic
 
 class GridCache {
  public:
-  // fill(buffer, stream): enqueue the kernel that writes the whole buffer.
+  // fill(buffer, stream): enqueue the kernel that writes the whole buffer.  fill_first: fill at
+  // the key's first use already (large launches, where forming the values in the kernel costs
+  // more than the fill kernel).
   template <class Fill>
   int get(const std::vector<unsigned char>& key, size_t bytes, hipStream_t st, Fill fill,
-          const void** out) {
+          bool fill_first, const void** out) {
     *out = nullptr;
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess) return AIRICE_EHIP;
@@ -2353,7 +2355,8 @@ class GridCache {
       e.key = key;
       e.used = ++D.tick;
       D.entries.push_back(std::move(e));
-      return AIRICE_OK;
+      if (!fill_first) return AIRICE_OK;
+      c = &D.entries.back();
     }
     c->used = ++D.tick;
     if (c->dev == nullptr) {  // second use: fill, stream-ordered ahead of this launch
@@ -2444,8 +2447,13 @@ static GridCache& angle_cache() {
 // The row constants of a grid.  row_const reads the medium, the heights and, of the ice constants,
 // only the lowest air layer (bot) and the Tx-layer stop ends (topend): the key holds exactly those,
 // so tables of one grid for antennas at different depths in the ice share one entry.
+// Rays of a launch from which a grid's caches are filled at its first use: forming the rows and
+// sines in the kernel costs ~2-5 ps per ray (cfg2: +2 us, 1.07x; cfg4 at 8.7e8 rays: +4.3 ms,
+// 1.21x), the two fill kernels ~10-20 us.
+constexpr long long kFillFirstRays = 1LL << 22;
+
 static int row_consts_cached(const DevMedium& M, const IceConsts& I, const TableArgs& A,
-                             hipStream_t st, const RowConst** out) {
+                             hipStream_t st, bool fill_first, const RowConst** out) {
   const double gk[3] = {A.start_h, A.stop_h, A.step_h};
   std::vector<unsigned char> key(sizeof(M) + sizeof(I.bot) + sizeof(I.topend) + sizeof(gk) +
                                  sizeof(A.hsteps));
@@ -2464,14 +2472,15 @@ static int row_consts_cached(const DevMedium& M, const IceConsts& I, const Table
                        M, I, A, static_cast<RowConst*>(p));
   };
   const void* p = nullptr;
-  const int rc = row_cache().get(key, sizeof(RowConst) * (size_t)std::max(A.hsteps, 1), st, fill, &p);
+  const int rc = row_cache().get(key, sizeof(RowConst) * (size_t)std::max(A.hsteps, 1), st, fill,
+                                 fill_first, &p);
   *out = static_cast<const RowConst*>(p);
   return rc;
 }
 
 // The start-angle sines of an angle grid (the degree-to-radian factor and the angle grid).
 static int angle_sines_cached(const DevMedium& M, const TableArgs& A, hipStream_t st,
-                              const double** out) {
+                              bool fill_first, const double** out) {
   const double k5[5] = {M.d2r, A.start_a, A.stop_a, A.step_a, (double)A.asteps};
   std::vector<unsigned char> key(sizeof(k5));
   std::memcpy(key.data(), k5, sizeof(k5));
@@ -2480,7 +2489,8 @@ static int angle_sines_cached(const DevMedium& M, const TableArgs& A, hipStream_
                        s, M, A, static_cast<double*>(p));
   };
   const void* p = nullptr;
-  const int rc = angle_cache().get(key, sizeof(double) * (size_t)std::max(A.asteps, 1), st, fill, &p);
+  const int rc = angle_cache().get(key, sizeof(double) * (size_t)std::max(A.asteps, 1), st, fill,
+                                   fill_first, &p);
   *out = static_cast<const double*>(p);
   return rc;
 }
@@ -2524,9 +2534,10 @@ int launch_table(const DevMedium& M, const IceConsts& I, const airice_grid* g, i
   A.rows_per_block = std::min(kTableBlock, (kTableBlock - 1) / g->angle_steps + 2);
   A.rc = nullptr;
   std::unique_lock<std::mutex> rs_lock(grid_cache_mutex());  // held until the launches are enqueued
-  if (int rc = row_consts_cached(M, I, A, st, &A.rc)) return rc;
+  const bool fill_first = (long long)row_count * g->angle_steps >= kFillFirstRays;
+  if (int rc = row_consts_cached(M, I, A, st, fill_first, &A.rc)) return rc;
   A.vs = nullptr;
-  if (int rc = angle_sines_cached(M, A, st, &A.vs)) return rc;
+  if (int rc = angle_sines_cached(M, A, st, fill_first, &A.vs)) return rc;
   static const char* trace_path = getenv("AIRICE_TABLE_TRACE");
   // ray indices are 32-bit inside a launch: grids of kMaxLaunchRays or more go in row slabs
   const int max_rows = (int)std::max<long long>(1, (kMaxLaunchRays - 2 * kTableBlock) / g->angle_steps);
@@ -2613,9 +2624,10 @@ int launch_table_multi(const DevMedium& M, const IceConsts* Ih, const airice_gri
     A.rows_per_block = rpb;
     A.row0 = 0;
     A.rc = nullptr;
-    if (int rc = row_consts_cached(M, Ih[a], A, st, &A.rc)) return rc;
+    const bool fill_first = (long long)g->table_rows * g->angle_steps >= kFillFirstRays;
+    if (int rc = row_consts_cached(M, Ih[a], A, st, fill_first, &A.rc)) return rc;
     A.vs = nullptr;
-    if (int rc = angle_sines_cached(M, A, st, &A.vs)) return rc;
+    if (int rc = angle_sines_cached(M, A, st, fill_first, &A.vs)) return rc;
     const long long rays = (long long)g->table_rows * g->angle_steps;
     if (rays >= kMaxLaunchRays - 2 * kTableBlock || lds[a] < (size_t)rays) {
       set_error("antenna %d: %lld rays (ld %zu) do not fit one multi-antenna launch", a, rays,

@@ -71,7 +71,7 @@ def main():
         out = {"kernels": {n: {"calls": int(r["Calls"]), "avg_ms": float(r["AverageNs"]) / 1e6}
                            for n, r in rows.items()}}
         for prefix, path in CHECKS.get(item, []):
-            hit = [r for n, r in rows.items() if n.startswith(prefix)]
+            hit = [r for n, r in rows.items() if n.replace("void ", "", 1).startswith(prefix)]
             if not hit:
                 continue
             ms = float(hit[0]["AverageNs"]) / 1e6

@@ -1,8 +1,6 @@
 set -o pipefail
-O=gpurun_out/r04f; mkdir -p $O
-bash tools/gpu_ab_solve.sh ab/lean1.so ab/bs128.so ab/bs64.so ab/lib_r03.so ab/r03_bs64.so > $O/ab_solve.log 2>&1 || { cat $O/ab_solve.log; exit 1; }
-cat $O/ab_solve.log
-bash tools/gpu_ab_tables.sh ab/lean1.so ab/a1.so > $O/ab_table.log 2>&1 || { cat $O/ab_table.log; exit 1; }
-cat $O/ab_table.log
-bash tools/gpu_ab_lookup.sh ab/lean1.so ab/fb_exit.so > $O/ab_lookup.log 2>&1 || { cat $O/ab_lookup.log; exit 1; }
-cat $O/ab_lookup.log
+O=gpurun_out/r04h; mkdir -p $O
+timeout -k 10 300 python -u -m pytest tests/test_gpu_multi.py tests/test_gpu_cfg4.py -x -q -p no:cacheprovider --timeout 200 --timeout-method thread > $O/tests.log 2>&1; rc=$?
+tail -2 $O/tests.log; [ $rc -eq 0 ] || exit 1
+timeout -k 10 300 python bench.py --only cfg4 > $O/cfg4.json 2>$O/cfg4.err || { tail $O/cfg4.err; exit 1; }
+python -c "import json;d=json.loads(open('$O/cfg4.json').read());c=d['table_cfg4'];print(c['first_build_ms'],c['ms_per_build'],c['kernel_ms'])"
