@@ -19,7 +19,7 @@ for item in table solve trace lookup; do
     || { echo "rocprof $item failed rc=$?"; tail -5 $OUT/prof_$item.err; exit 1; }
 done
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/prof_cfg4 -o cfg4 --output-format csv -- \
-  python $R/bench.py --cfg4-only --cfg4-reps 3 --no-cpu > $OUT/prof_cfg4.json 2> $OUT/prof_cfg4.err \
+  python $R/bench.py --cfg4-only --cfg4-reps 9 --no-cpu > $OUT/prof_cfg4.json 2> $OUT/prof_cfg4.err \
   || { echo "rocprof cfg4 failed rc=$?"; tail -5 $OUT/prof_cfg4.err; exit 1; }
 mkdir -p /tmp/scalar_prof && gunzip -c $R/airiceraytracing_amd/data/Atmosphere.dat.gz > /tmp/scalar_prof/Atmosphere.dat
 cd /tmp/scalar_prof && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/prof_scalar -o scalar --output-format csv -- \

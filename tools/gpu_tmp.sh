@@ -1,5 +1,10 @@
 set -o pipefail
-O=gpurun_out/r04i; mkdir -p $O
-timeout -k 10 300 python bench.py --only cfg4 > $O/cfg4.json 2>$O/cfg4.err || { tail $O/cfg4.err; exit 1; }
-python -c "import json;d=json.loads(open('$O/cfg4.json').read());c=d['table_cfg4'];print(c['first_build_ms'],c['new_key_build_ms'],c['ms_per_build'],c['kernel_ms'])"
-bash tools/gpu_pmc.sh || exit 1
+O=gpurun_out/r04j; mkdir -p $O
+bash tools/gpu_ab_tables.sh ab/base.so ab/s_ilp.so ab/s_memc.so > $O/ab_table.log 2>&1 || { cat $O/ab_table.log; exit 1; }
+bash tools/gpu_ab_solve.sh ab/base.so ab/s_ilp.so ab/s_memc.so > $O/ab_solve.log 2>&1 || { cat $O/ab_solve.log; exit 1; }
+bash tools/gpu_ab_lookup.sh ab/base.so ab/s_ilp.so ab/s_memc.so > $O/ab_lookup.log 2>&1 || { cat $O/ab_lookup.log; exit 1; }
+cat $O/ab_table.log | python3 -c "
+import sys,json
+for l in sys.stdin:
+    d=json.loads(l); print(d['lib'], round(d['ms']*1e3,2), d['sha1'][:10])"
+cat $O/ab_solve.log $O/ab_lookup.log
