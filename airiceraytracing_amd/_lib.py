@@ -104,7 +104,7 @@ class LookupTable(ctypes.Structure):
 
 
 LOOKUP_ENTRY_FLOATS = 32  # AIRICE_LOOKUP_ENTRY_FLOATS
-LOOKUP_ROW_FLOATS = 8  # AIRICE_LOOKUP_ROW_FLOATS
+LOOKUP_ROW_FLOATS = 64  # AIRICE_LOOKUP_ROW_FLOATS
 
 
 class SingleRayInfo(ctypes.Structure):

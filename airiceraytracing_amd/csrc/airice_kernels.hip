@@ -1010,18 +1010,17 @@ __device__ __forceinline__ SolveResult solve_root(const DevMedium& M, const IceC
     // evaluation (.cc:1496-1509 would reject each of them).
     if (q.top >= q.bot) {
       const double thr = 180 - asin((1 + 1e-6) / q.n_tx) * M.r2d;  // NaN if n(Tx) < 1+1e-6
-      while (lo < thr && !(lo > hi - 0.1)) {
-        lo = lo + 0.05;
-        status |= AIRICE_SOLVE_PROBED;
-      }
+      // while (lo < thr && !(lo > hi - 0.1)) lo = lo + 0.05, in closed form (airice_lean.hpp)
+      bool stepped;
+      lo = probe_steps(lo, 0.05, hi - 0.1, thr, true, stepped);
+      if (stepped) status |= AIRICE_SOLVE_PROBED;
     } else {
       // no air layer (Tx above the atmosphere, e.g. the table lookup's x100 fallback): THD in
-      // air is 0 at every angle, so the probe only stops at lo > hi - 0.1 -- up to ~300 steps
-      // whose outcome needs no evaluation
-      while (!(lo > hi - 0.1)) {
-        lo = lo + 0.05;
-        status |= AIRICE_SOLVE_PROBED;
-      }
+      // air is 0 at every angle, so the probe only stops at lo > hi - 0.1 -- up to ~900 steps
+      // whose outcome needs no evaluation, taken in closed form (airice_lean.hpp)
+      bool stepped;
+      lo = probe_steps(lo, 0.05, hi - 0.1, 0.0, false, stepped);
+      if (stepped) status |= AIRICE_SOLVE_PROBED;
       if (hi < 90.001 && hi > 90.00) hi = 90.05;
       phase = PH_FLO;
       if (lo > hi) {
@@ -1639,32 +1638,21 @@ constexpr int kRootsWaves = 4;  // 127 VGPRs: 4 waves/SIMD (5 and 6 spill and ru
 // blocks (roots_sorted_kernel)
 constexpr long long kGroupMin = 65536;
 
-// Stage 2 of the lookup fallback with the root handed over in registers (roots_kernel<IN_CM100>,
-// fused): defined below.
+// Stage 2 of the lookup fallback with the root handed over in registers (lookup_fallback_kernel):
+// defined below.
 __device__ __forceinline__ void fallback_out_direct(const DevMedium& M, const IceConsts& I,
                                                     const QueryArgs& Q, double* __restrict__ out,
                                                     size_t ld, uint8_t* __restrict__ ok,
                                                     long long k, const double* tab,
                                                     const Geometry& g, double root, int status);
 
-// BS: threads per block (the lookup fallback pass uses 256: its few active lanes per block then
-// fill more, shorter-lived blocks, all resident at once).  FUSED (IN_CM100 only): the block also
-// runs the fallback's stage 2 for its lanes, with the root in registers (out / ld / ok).
-template <int IN, int BS = kRootsBlock, bool FUSED = false>
-__global__ __launch_bounds__(BS, kRootsWaves) void roots_kernel(DevMedium M, IceConsts I,
-                                                                       QueryArgs Q, Park park,
-                                                                       double* __restrict__ out,
-                                                                       size_t ld,
-                                                                       uint8_t* __restrict__ ok) {
-  constexpr int kRootsBlock = BS;
+template <int IN>
+__global__ __launch_bounds__(kRootsBlock, kRootsWaves) void roots_kernel(DevMedium M, IceConsts I,
+                                                                         QueryArgs Q, Park park) {
   __shared__ int s_count[kSortBuckets + 1];
   __shared__ int s_slot[kRootsBlock];
   const long long k0 = (long long)blockIdx.x * kRootsBlock;
   const long long kt = k0 + threadIdx.x;
-  // the table lookup's fallback pass: most blocks hold no fallback lane (well under 1 % of a
-  // batch's queries take it) and leave before staging anything
-  if (IN == IN_CM100 && !__syncthreads_or(kt < Q.n && (Q.mask[kt] & AIRICE_LOOKUP_FALLBACK)))
-    return;
   // the log table in LDS (one 16-byte entry per thread), as in table_kernel: every evaluation's
   // log ratios read it instead of global memory
   __shared__ __align__(16) double s_logtab[1 << kLogTableBits][2];
@@ -1676,7 +1664,7 @@ __global__ __launch_bounds__(BS, kRootsWaves) void roots_kernel(DevMedium M, Ice
   __syncthreads();
   // bucket of this lane's own query (unused lanes last)
   int bucket = kSortBuckets;
-  if (kt < Q.n && (IN != IN_CM100 || (Q.mask[kt] & AIRICE_LOOKUP_FALLBACK))) {
+  if (kt < Q.n) {
     double thR0;
     (void)load_query<IN>(M, Q, kt, thR0);
     const double b = (thR0 - 90.0) * (kSortBuckets / 90.0);
@@ -1697,14 +1685,9 @@ __global__ __launch_bounds__(BS, kRootsWaves) void roots_kernel(DevMedium M, Ice
   __syncthreads();
   const long long k = k0 + s_slot[threadIdx.x];
   if (k >= Q.n) return;
-  if (IN == IN_CM100 && !(Q.mask[k] & AIRICE_LOOKUP_FALLBACK)) return;
   double thR;
   const Geometry g = load_query<IN>(M, Q, k, thR);
   const SolveResult r = solve_root(M, I, g, thR, park.exact != 0, &s_logtab[0][0]);
-  if constexpr (FUSED) {
-    fallback_out_direct(M, I, Q, out, ld, ok, k, &s_logtab[0][0], g, r.root, r.status);
-    return;
-  }
   park.root[k * park.stride] = r.root;
   park.status[k * park.stride] = (double)r.status;
   if (park.stats != nullptr) {
@@ -2228,8 +2211,7 @@ static int launch_roots(const DevMedium& M, const IceConsts& I, const QueryArgs&
   if (IN == IN_CM100 || group_min == 0 || n < group_min ||
       (park.stats != nullptr && !AIRICE_SORTED_STATS) || n >= (1ull << 31)) {
     ktimer_begin(KT_ROOTS, st);
-    hipLaunchKernelGGL((roots_kernel<IN>), roots_grid(n), dim3(kRootsBlock), 0, st, M, I, Q, park,
-                       nullptr, (size_t)0, nullptr);
+    hipLaunchKernelGGL((roots_kernel<IN>), roots_grid(n), dim3(kRootsBlock), 0, st, M, I, Q, park);
     ktimer_end(KT_ROOTS, st);
     return launch_ok();
   }
@@ -2797,6 +2779,44 @@ int launch_hdtip(const DevMedium& M, const IceConsts& I, const double* src, cons
   return rc;
 }
 
+// The table lookup's fallback pass: a few hundred of a batch's million queries take it, so a grid
+// over every query would be mostly waves that only read their flag and leave (the dispatch of
+// ~4k empty blocks cost ~10 us).  Each block instead scans a chunk of kFbChunk flags (coalesced
+// byte loads), lists its fallback queries in LDS and solves them, one per lane (stage 2 with the
+// root in registers, as roots_kernel<IN_CM100, 256, true>).
+constexpr int kFbBlock = 256;
+constexpr int kFbChunk = 4096;
+__global__ __launch_bounds__(kFbBlock, kRootsWaves) void lookup_fallback_kernel(
+    DevMedium M, IceConsts I, QueryArgs Q, double* __restrict__ out, size_t ld,
+    uint8_t* __restrict__ ok, int exact) {
+  __shared__ int s_list[kFbChunk];
+  __shared__ int s_n;
+  __shared__ __align__(16) double s_logtab[1 << kLogTableBits][2];
+  if (threadIdx.x == 0) s_n = 0;
+  __syncthreads();
+  const long long c0 = (long long)blockIdx.x * kFbChunk;
+#pragma unroll 4
+  for (int j = threadIdx.x; j < kFbChunk; j += kFbBlock) {
+    const long long k = c0 + j;
+    if (k < Q.n && (Q.mask[k] & AIRICE_LOOKUP_FALLBACK)) s_list[atomicAdd(&s_n, 1)] = j;
+  }
+  __syncthreads();
+  const int cnt = s_n;
+  if (cnt == 0) return;  // block-uniform
+  for (unsigned t = threadIdx.x; t < (1u << kLogTableBits); t += kFbBlock) {
+    s_logtab[t][0] = kLogTable[t][0];
+    s_logtab[t][1] = kLogTable[t][1];
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < cnt; i += kFbBlock) {
+    const long long k = c0 + s_list[i];
+    double thR;
+    const Geometry g = load_query<IN_CM100>(M, Q, k, thR);
+    const SolveResult r = solve_root(M, I, g, thR, exact != 0, &s_logtab[0][0]);
+    fallback_out_direct(M, I, Q, out, ld, ok, k, &s_logtab[0][0], g, r.root, r.status);
+  }
+}
+
 int launch_lookup_fallback(const DevMedium& M, const IceConsts& I, const double* src,
                            const double* dist, const double* depth, double ice_cm, size_t n,
                            double* out, size_t ld, uint8_t* ok, const uint8_t* flags,
@@ -2806,18 +2826,13 @@ int launch_lookup_fallback(const DevMedium& M, const IceConsts& I, const double*
   const double ice_arg = (ice_cm / 100) * 100;
   const QueryArgs Q{src, dist, depth, nullptr, ice_arg, (long long)n, flags};
   const Park park{out + 4 * ld, out, 1, bisect_exact(), nullptr};
-  const dim3 grid(grid_for((long long)n)), block(kBlock);
   if (n == 1) {
     hipLaunchKernelGGL((scalar_solve_kernel<IN_CM100, OUT_FALLBACK>), dim3(1), dim3(64), 0, st, M,
                        I, Q, park, out, ld, ok, take_scalar_signal());
     return launch_ok();
   }
-  // one pass: 256-lane blocks group their few fallback lanes into their first wave, solve them and
-  // write their outputs (stage 2 with the root in registers)
-  (void)grid;
-  (void)block;
-  hipLaunchKernelGGL((roots_kernel<IN_CM100, 256, true>), dim3((unsigned)((n + 255) / 256)),
-                     dim3(256), 0, st, M, I, Q, park, out, ld, ok);
+  hipLaunchKernelGGL(lookup_fallback_kernel, dim3((unsigned)((n + kFbChunk - 1) / kFbChunk)),
+                     dim3(kFbBlock), 0, st, M, I, Q, out, ld, ok, park.exact);
   return launch_ok();
 }
 

@@ -134,4 +134,52 @@ __host__ __device__ AIRICE_INLINE bool lean_closed(double lo, double hi, int ite
   return true;
 }
 
+// The probe's evaluation-free steps (solve_root; Air2IceRayTracing's probe loop,
+// MultiRayAirIceRefraction.cc:1496-1509, where the loop's outcome needs no evaluation):
+//   while ((!use_thr || lo < thr) && !(lo > T)) lo = lo + c;
+// `stepped`: a step was taken.  Inside a binade [2^e, 2^(e+1)) every lo on that binade's grid
+// (spacing u = 2^(e-52)) has lo + c rounded by the same amount, unless c's remainder modulo u is
+// exactly u/2 (a tie, which depends on lo's last bit): there the steps are the exact arithmetic
+// sequence x1 + m d (d = fl(x1 + c) - x1; m d exact while d < 2^(e-10) and m < 2^11), and the
+// stopping step comes from one division, confirmed on exact values (the loop condition is monotone
+// in lo for finite bounds).  A step that leaves the binade, a tie, or non-finite bounds go one step
+// at a time.  The no-air-layer probe of the lookup's x100 fallback runs up to ~900 such steps.
+__host__ __device__ AIRICE_INLINE double probe_steps(double lo, double c, double T, double thr,
+                                                     bool use_thr, bool& stepped) {
+  auto cont = [&](double x) { return (!use_thr || x < thr) && !(x > T); };
+  stepped = false;
+  const bool finite = __builtin_isfinite(T) && (!use_thr || __builtin_isfinite(thr)) && c > 0.0;
+  while (cont(lo)) {
+    lo = lo + c;
+    stepped = true;
+    if (!finite || !cont(lo)) continue;
+    const double x2 = lo + c;
+    const double d = x2 - lo;  // exact (x2 and lo within a factor 2)
+    const int e = lean_exp(lo);
+    if (lean_exp(x2) != e || !(lo > 0.0)) continue;
+    const double u = lean_scale(1.0, e - 52);
+    const double r = c - d;
+    if ((r < 0 ? -r : r) == 0.5 * u || !(d < lean_scale(1.0, e - 10)) || !(d > 0.0)) continue;
+    // steps m = 1 .. mmax stay inside the binade (x1 + m d < 2^(e+1)), m < 2^11
+    const double top = lean_scale(1.0, e + 1);
+    double mmax = floor((top - lo) / d);
+    if (mmax > 2047.0) mmax = 2047.0;
+    while (mmax >= 1.0 && !(lo + mmax * d < top)) mmax -= 1.0;
+    if (mmax < 1.0) continue;
+    // first m with !cont(x1 + m d): from the bounds, then confirmed
+    double m = mmax;
+    const double mT = floor((T - lo) / d) + 1.0;
+    if (mT < m) m = mT;
+    if (use_thr) {
+      const double mthr = ceil((thr - lo) / d);
+      if (mthr < m) m = mthr;
+    }
+    if (m < 1.0) m = 1.0;
+    while (m > 1.0 && !cont(lo + (m - 1.0) * d)) m -= 1.0;
+    while (m < mmax && cont(lo + m * d)) m += 1.0;
+    lo = lo + m * d;
+  }
+  return lo;
+}
+
 }  // namespace airice

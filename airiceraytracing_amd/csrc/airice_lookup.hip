@@ -14,9 +14,12 @@
 //                  finished by the masked minimizer pass (launch_lookup_fallback,
 //                  airice_kernels.hip), which reproduces the reference's fallback call.
 //
-// Cost model: ~20-40 dependent 4-byte gathers per query (2 rows x (bisection over ~900
-// THD entries + 10 columns x 2 entries)), so the kernel is gather-latency bound; the table
-// (11 x 4 B x rays, ~38 MB for the default grid) stays L2/MALL-resident across a batch.
+// Cost model: every lane gathers its own lines, so the kernel is bound by the 128-byte lines it
+// pulls from L2 / the Infinity Cache per query, not by bytes.  With the packed copy a query reads
+// the row record (two lines: the span, its end values and the THD values of the first four
+// bisection steps of both heights), then per height one short window of the THD column (steps 4-7
+// and the scan, 48 B) and one pair record (128 B): ~7 lines, against ~13 when the bisection
+// gathered each midpoint from the THD column.
 // Reads the reference makes outside the table (a row with no valid THD, index -1 in
 // FindClosestTHD) are bounded here and reported as AIRICE_LOOKUP_UNPINNED.
 #include <hip/hip_runtime.h>
@@ -34,11 +37,10 @@ namespace {
 
 constexpr int kLkBlock = 256;
 
-// Occupancy: the compiler's choice (78 VGPRs = 6 waves/SIMD).  Measured (1e6 cfg3 queries,
-// identical outputs): 7 waves (72 VGPRs, 28 B/lane spilled) 166 us and 8 waves (64 VGPRs,
-// 60 B/lane) 175 us against 152 us at 6: more resident waves do not help a kernel bound by the L2
-// line requests of its 64-lane gathers, and the spills add requests.  (Searching the two rows of
-// GetParValues side by side, each step issuing both rows' reads, measured 163 against 161 us.)
+// Occupancy: the compiler's choice (87 VGPRs = 5 waves/SIMD).  Measured (1e6 cfg3 queries,
+// tools/gpu_ab_lookup.sh, identical outputs): 6 waves (80 VGPRs, 36 B/lane spilled) 138 against
+// 124 us.  (Round 3, before the row records' trees: 7 and 8 waves with spills 166 / 175 against
+// 152 us at 6; the two rows of GetParValues searched side by side 163 against 161 us.)
 __global__ __launch_bounds__(kLkBlock) void lookup_kernel(LkTable T, const double* __restrict__ src,
                                                           const double* __restrict__ dist,
                                                           double ice_cm, long long n, double d2r,
@@ -89,8 +91,9 @@ __global__ __launch_bounds__(kLkBlock) void lookup_rows_kernel(LkTable T, float*
   lk_row_fold(T, r, rec);
   float4* p = reinterpret_cast<float4*>(e + T.n * AIRICE_LOOKUP_ENTRY_FLOATS +
                                         r * AIRICE_LOOKUP_ROW_FLOATS);
-  p[0] = make_float4(rec[0], rec[1], rec[2], rec[3]);
-  p[1] = make_float4(rec[4], rec[5], rec[6], rec[7]);
+#pragma unroll
+  for (int q = 0; q < AIRICE_LOOKUP_ROW_FLOATS / 4; ++q)
+    p[q] = make_float4(rec[4 * q], rec[4 * q + 1], rec[4 * q + 2], rec[4 * q + 3]);
 }
 
 LkTable lk_table(const airice_lookup_table* t) {

@@ -140,11 +140,26 @@ __host__ __device__ __forceinline__ LkTxhBins lk_closest_txh(const LkTable& T, d
 // Row record (packed copy, after the entry records): the span of row `index` and the table values
 // the lookup reads at its ends, folded by airice_lookup_pack from the same code as above.  Used
 // only for rows whose scans stay inside the table (ok), so the flags are unchanged.
+//
+// FindClosestTHD's first four bisection steps on a span (s, e) depend on the query only through
+// the comparisons: from a given span the midpoints form a fixed binary tree of depth 4 (15 nodes,
+// breadth-first: node k's successors 2k + 1 after s = mid, 2k + 2 after e = mid).  The record holds
+// the THD value at each node for the row's own span (s1, e1) and for the span the second
+// interpolation height searches (s2, e2): a query then takes its first four steps from two 128-byte
+// lines it reads anyway instead of four dependent gathers into the THD column, and the rest of
+// the search and the linear scan from one short window of that column (lk_closest_thd_tree).
+constexpr int kLkTreeNodes = 15;  // bisection steps 0-3
+constexpr int kLkWindow = 12;     // THD entries the steps 4-7 and the scan may read
+struct LkTree {
+  float v[kLkTreeNodes];
+};
 struct LkRow {
   LkTxhBins b;
   double c1v;      // column 0 at entry `index` (ClosestVal's operand)
   double h1, h2;   // column 0 at s1, at s2 (s2 < n - 1)
   double mt1, mt2; // column 1 (THD) at s1, at s2
+  bool tree1, tree2;  // the node values below are usable (every node's midpoint inside the table)
+  const float* rec;   // the row record: tree 1 at floats 8-22, tree 2 at floats 32-46
 };
 __host__ __device__ __forceinline__ float lk_bits_f(int32_t i) {
   float f;
@@ -156,14 +171,60 @@ __host__ __device__ __forceinline__ int32_t lk_bits_i(float f) {
   std::memcpy(&i, &f, sizeof(i));
   return i;
 }
-// Fold row r (pack time): 8 floats {s1, e1 (int bits), col0[r], col0[s1], col0[s2], col1[s1],
-// col1[s2], ok (int bits)}.
-__host__ __device__ __forceinline__ void lk_row_fold(const LkTable& T, long long r, float rec[8]) {
+// THD values at the 15 nodes of the bisection tree of span (s, e) (pack time).  False when a
+// node's midpoint lies outside the table (the lane then searches the column: lk_closest_thd).
+__host__ __device__ __forceinline__ bool lk_tree_fold(const LkTable& T, long long s, long long e,
+                                                      float* out) {
+  long long ss[kLkTreeNodes], ee[kLkTreeNodes];
+  bool live[kLkTreeNodes];
+  ss[0] = s;
+  ee[0] = e;
+  live[0] = true;
+  bool ok = true;
+  for (int k = 0; k < kLkTreeNodes; ++k) {
+    out[k] = 0.0f;
+    const bool inner = 2 * k + 2 < kLkTreeNodes;
+    bool split = live[k] && ee[k] - ss[k] >= 3;
+    long long mid = 0;
+    if (split) {
+      mid = (ss[k] + ee[k]) / 2;  // FindClosestTHD's midpoint (.cc:1142)
+      if (mid < 0 || mid >= T.n) {
+        ok = false;
+        split = false;
+      } else {
+        out[k] = T.col[1][mid];
+      }
+    }
+    if (inner) {
+      live[2 * k + 1] = live[2 * k + 2] = split;
+      ss[2 * k + 1] = mid;  // v - P > 0: StartIndex = mid
+      ee[2 * k + 1] = ee[k];
+      ss[2 * k + 2] = ss[k];  // v - P < 0: EndIndex = mid
+      ee[2 * k + 2] = mid;
+    }
+  }
+  return ok;
+}
+
+// The search span of the second interpolation height, from the first's (.cc:1118-1121).
+__host__ __device__ __forceinline__ void lk_span2(const LkTable& T, LkTxhBins& b) {
+  b.s2 = b.s1 - T.asteps;
+  b.e2 = b.e1 - T.asteps;
+  if (b.s2 < 0) b.s2 = b.s1 + T.asteps;
+  if (b.e2 < 0) b.e2 = b.e1 + T.asteps;
+}
+
+// Fold row r (pack time), AIRICE_LOOKUP_ROW_FLOATS floats in two 128-byte lines:
+//   line 0: {s1, e1 (int bits), col0[r], col0[s1], col0[s2], col1[s1], col1[s2], ok (int bits)},
+//           the tree of (s1, e1) (floats 8-22), tree bits (float 23: 1 = tree 1, 2 = tree 2);
+//   line 1: the tree of (s2, e2) (floats 32-46).
+__host__ __device__ __forceinline__ void lk_row_fold(const LkTable& T, long long r, float* rec) {
   int fl = 0;
   const LkTxhBins b = lk_txh_span(T, r, fl);
   const bool s2_used = b.s2 < T.n - 1;
   const bool ok = fl == 0 && b.s1 >= 0 && b.s1 < T.n && r < T.n && b.s1 < (1LL << 31) &&
                   b.e1 >= -(1LL << 31) && b.e1 < (1LL << 31) && b.s2 >= 0;
+  for (int k = 0; k < AIRICE_LOOKUP_ROW_FLOATS; ++k) rec[k] = 0.0f;
   rec[0] = lk_bits_f((int32_t)(ok ? b.s1 : 0));
   rec[1] = lk_bits_f((int32_t)(ok ? b.e1 : 0));
   rec[2] = ok ? T.col[0][r] : 0.0f;
@@ -172,24 +233,48 @@ __host__ __device__ __forceinline__ void lk_row_fold(const LkTable& T, long long
   rec[5] = ok ? T.col[1][b.s1] : 0.0f;
   rec[6] = ok && s2_used ? T.col[1][b.s2] : 0.0f;
   rec[7] = lk_bits_f(ok ? 1 : 0);
+  int trees = 0;
+  if (ok) {
+    LkTxhBins b2 = b;  // the span lk_row rebuilds from (s1, e1)
+    lk_span2(T, b2);
+    if (lk_tree_fold(T, b2.s1, b2.e1, rec + 8)) trees |= 1;
+    if (lk_tree_fold(T, b2.s2, b2.e2, rec + 32)) trees |= 2;
+  }
+  rec[23] = lk_bits_f(trees);
+}
+__host__ __device__ __forceinline__ const float4* lk_row_rec(const LkTable& T, long long index) {
+  return reinterpret_cast<const float4*>(T.e + T.n * AIRICE_LOOKUP_ENTRY_FLOATS +
+                                         index * AIRICE_LOOKUP_ROW_FLOATS);
+}
+__host__ __device__ __forceinline__ void lk_tree_unpack(const float4* p, LkTree& T_) {
+  float* t = T_.v;
+  // floats 0-14 of the 4 float4 at p
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const float4 a = p[q];
+    t[4 * q] = a.x;
+    t[4 * q + 1] = a.y;
+    t[4 * q + 2] = a.z;
+    if (4 * q + 3 < kLkTreeNodes) t[4 * q + 3] = a.w;
+  }
 }
 __host__ __device__ __forceinline__ bool lk_row(const LkTable& T, long long index, LkRow& R) {
   if (T.e == nullptr || index < 0 || index >= T.rows) return false;
-  const float4* p = reinterpret_cast<const float4*>(T.e + T.n * AIRICE_LOOKUP_ENTRY_FLOATS +
-                                                    index * AIRICE_LOOKUP_ROW_FLOATS);
+  const float4* p = lk_row_rec(T, index);
   const float4 a = p[0], c = p[1];
   if (lk_bits_i(c.w) == 0) return false;
   R.b.s1 = lk_bits_i(a.x);
   R.b.e1 = lk_bits_i(a.y);
-  R.b.s2 = R.b.s1 - T.asteps;
-  R.b.e2 = R.b.e1 - T.asteps;
-  if (R.b.s2 < 0) R.b.s2 = R.b.s1 + T.asteps;
-  if (R.b.e2 < 0) R.b.e2 = R.b.e1 + T.asteps;
+  lk_span2(T, R.b);
   R.c1v = a.z;
   R.h1 = a.w;
   R.h2 = c.x;
   R.mt1 = c.y;
   R.mt2 = c.z;
+  R.rec = reinterpret_cast<const float*>(p);
+  const int trees = lk_bits_i(R.rec[23]);
+  R.tree1 = (trees & 1) != 0;
+  R.tree2 = (trees & 2) != 0;
   return true;
 }
 
@@ -232,14 +317,139 @@ __host__ __device__ __forceinline__ LkThdBins lk_closest_thd(const LkTable& T, d
   return LkThdBins{index1, index2, minimum};
 }
 
+// v[j] of N values by a binary multiplexer on the bits of j (0 <= j < N): selects only, so the
+// values stay in registers (an equality chain is turned back into an indexed private array).
+template <int N>
+__host__ __device__ __forceinline__ float lk_mux(const float* v, int j) {
+  float m[N];
+#pragma unroll
+  for (int i = 0; i < N; ++i) m[i] = v[i];
+#pragma unroll
+  for (int w = 1; w < N; w *= 2) {
+    const bool hi = (j & w) != 0;
+#pragma unroll
+    for (int i = 0; i + w < N; i += 2 * w) m[i] = hi ? m[i + w] : m[i];
+  }
+  return m[0];
+}
+
+// One step of lk_closest_thd's bisection (.cc:1140-1147) on indices s <= e below 2^31 and the
+// THD value v at their midpoint: s = mid if v - P > 0, e = mid if v - P < 0, and otherwise (equal,
+// NaN) `fin`, since every later step would repeat this one unchanged.  Returns the branch taken.
+__host__ __device__ __forceinline__ bool lk_step32(double v, double P, int& s, int& e, bool& fin) {
+  const int mid = (int)(((unsigned)s + (unsigned)e) >> 1);  // (s + e) / 2, s, e >= 0
+  const bool up = v - P > 0, down = v - P < 0;
+  s = up ? mid : s;
+  e = down ? mid : e;
+  fin = fin || !(up || down);
+  return up;
+}
+
+// lk_closest_thd from a row record's tree (the first four steps) and kLkWindow consecutive THD
+// values (the rest of the steps and the scan): the same index1, index2, minimum and pair, read
+// from the packed copy.  False -- the caller then runs lk_closest_thd -- when the span left after
+// the tree is wider than the window, the search ends on a span of more than 3 entries (an equal
+// or NaN midpoint), the scan runs off its end without a break, or the pair has no packed record;
+// every value it reads lies inside the table, so no flag changes.  Indices are 32-bit here (the
+// row fold admits spans below 2^31 only).
+__host__ __device__ __forceinline__ bool lk_closest_thd_tree(const LkTable& T, double P, long long s_in,
+                                                             long long e_in, const float* t,
+                                                             LkThdBins& out, LkThdPair& pr) {
+  if (s_in < 0 || e_in < s_in || T.n < kLkWindow || T.n >= (1LL << 31)) return false;
+  int s = (int)s_in, e = (int)e_in;
+  bool fin = false;
+  int k = 0;  // tree node of the current step
+#pragma unroll
+  for (int lvl = 0; lvl < 4; ++lvl) {
+    fin = fin || e - s < 3;
+    if (!fin) {
+      // the node's value from the row record (one dependent 4-byte read of a line the lane
+      // has just read)
+      const bool up = lk_step32((double)t[k], P, s, e, fin);
+      k = 2 * k + (up ? 1 : 2);
+    }
+  }
+  if (e - s >= kLkWindow) return false;
+  const int n32 = (int)T.n;
+  const int base = s <= n32 - kLkWindow ? s : n32 - kLkWindow;  // the window covers [s, e]
+  // the window, indexed per lane: on the device in the block's LDS (one column of 4-byte slots
+  // per lane, kLkWindow rows 256 lanes apart: conflict-free, and each read one instruction where
+  // a register multiplexer takes 11 selects); the lane reads only what it wrote
+  const float* src = T.col[1] + base;
+#if defined(__HIP_DEVICE_COMPILE__)
+  __shared__ float s_win[kLkWindow][256];
+  float* w = &s_win[0][threadIdx.x & 255];
+  constexpr int ws = 256;
+  // three 16-byte loads at 4-byte alignment (gfx950 vector memory takes unaligned dwordx4)
+  typedef float f4u __attribute__((ext_vector_type(4), aligned(4)));
+#pragma unroll
+  for (int q = 0; q < kLkWindow / 4; ++q) {
+    const f4u a = reinterpret_cast<const f4u*>(src)[q];
+    w[(4 * q) * ws] = a.x;
+    w[(4 * q + 1) * ws] = a.y;
+    w[(4 * q + 2) * ws] = a.z;
+    w[(4 * q + 3) * ws] = a.w;
+  }
+#else
+  float w[kLkWindow];
+  constexpr int ws = 1;
+  std::memcpy(w, src, sizeof(w));
+#endif
+#pragma unroll
+  for (int i = 4; i < 8; ++i) {
+    fin = fin || e - s < 3;
+    if (!fin) {
+      const int mid = (int)(((unsigned)s + (unsigned)e) >> 1);
+      lk_step32((double)w[(mid - base) * ws], P, s, e, fin);
+    }
+  }
+  if (e - s > 2) return false;
+  // the linear scan (.cc:1150-1160) over the <= 3 entries of [s, e]
+  const int j0 = s - base;  // j0 + 2 <= 11 when the third entry exists (e <= base + 11)
+  const int j1 = j0 + 1 < kLkWindow ? j0 + 1 : kLkWindow - 1;
+  const int j2 = j0 + 2 < kLkWindow ? j0 + 2 : kLkWindow - 1;
+  const float sv[3] = {w[j0 * ws], w[j1 * ws], w[j2 * ws]};
+  double minimum = 100000000000.0;
+  int index2 = 0;
+  bool brk = false;
+#pragma unroll
+  for (int j = 0; j < 3; ++j) {
+    if (!brk && s + j <= e) {
+      const double v = (double)sv[j];
+      const double minval = fabs(v - P);
+      if (minval < minimum && v > P) {
+        minimum = minval;
+      } else {
+        index2 = s + j;
+        brk = true;
+      }
+    }
+  }
+  if (!brk) return false;
+  const long long index1 = (long long)index2 - 1;
+  if (!lk_pair(T, index1, pr.r1, pr.r2)) return false;
+  pr.have_pair = true;
+  const double v2 = (double)pr.r2.c[0], v1 = (double)pr.r1.c[0];
+  minimum = fabs(P - v2);
+  if (minimum > fabs(P - v1)) minimum = fabs(P - v1);
+  out = LkThdBins{index1, (long long)index2, minimum};
+  return true;
+}
+
 // The 10 parameters of one table row at horizontal distance D (.cc:1199-1240 / 1250-1289).
+// tree: the row record's bisection tree of (s, e) when use_tree.
 __host__ __device__ __forceinline__ void lk_row_params(const LkTable& T, double D, long long s, long long e,
                                               double par[10], double* closest, int& fl,
-                                              const double* max_thd_row = nullptr) {
+                                              const double* max_thd_row = nullptr,
+                                              const float* tree = nullptr) {
   const double max_thd = max_thd_row != nullptr ? *max_thd_row : lk_at(T, 1, s, fl);
   if (D <= max_thd) {
     LkThdPair pr;
-    const LkThdBins b = lk_closest_thd(T, D, s, e, fl, pr);
+    LkThdBins b;
+    if (tree == nullptr || !lk_closest_thd_tree(T, D, s, e, tree, b, pr)) {
+      pr.have_pair = false;
+      b = lk_closest_thd(T, D, s, e, fl, pr);
+    }
     *closest = b.c;
     if (b.c != 0) {
       // b.e == b.s + 1 (index1 = index2 - 1)
@@ -277,12 +487,14 @@ __host__ __device__ __forceinline__ void lk_par_values(const LkTable& T, double 
   }
   double c1 = 0;
   *h1 = fast ? R.h1 : lk_at(T, 0, b.s1, fl);
-  lk_row_params(T, D, b.s1, b.e1, par1, &c1, fl, fast ? &R.mt1 : nullptr);
+  lk_row_params(T, D, b.s1, b.e1, par1, &c1, fl, fast ? &R.mt1 : nullptr,
+                fast && R.tree1 ? R.rec + 8 : nullptr);
   *h2 = *h1;
   if (b.c1 != 0 && H > min_h && b.s2 < T.n - 1) {
     *h2 = fast ? R.h2 : lk_at(T, 0, b.s2, fl);
     double c2 = 0;
-    lk_row_params(T, D, b.s2, b.e2, par2, &c2, fl, fast ? &R.mt2 : nullptr);
+    lk_row_params(T, D, b.s2, b.e2, par2, &c2, fl, fast ? &R.mt2 : nullptr,
+                  fast && R.tree2 ? R.rec + 32 : nullptr);
   } else {
 #pragma unroll
     for (int ip = 0; ip < 10; ++ip) par2[ip] = par1[ip];

@@ -193,9 +193,10 @@ typedef struct airice_lookup_table {
  * THD values at the pair. */
 #define AIRICE_LOOKUP_ENTRY_FLOATS 32
 /* Floats per row record, after the n_entries entry records, one per full table row
- * (n_entries / total_angle_steps rows): the row's FindClosestAirTxHeight span and the table
- * values the lookup reads at its ends (32 B), folded once by the pack. */
-#define AIRICE_LOOKUP_ROW_FLOATS 8
+ * (n_entries / total_angle_steps rows): the row's FindClosestAirTxHeight span, the table values
+ * the lookup reads at its ends and the THD values of the first four FindClosestTHD bisection
+ * steps on both interpolation heights' spans (two 128-byte lines), folded once by the pack. */
+#define AIRICE_LOOKUP_ROW_FLOATS 64
 /* Floats of the whole packed copy. */
 #define AIRICE_LOOKUP_PACK_FLOATS(n_entries, angle_steps)                 \
   ((size_t)(n_entries) * AIRICE_LOOKUP_ENTRY_FLOATS +                    \

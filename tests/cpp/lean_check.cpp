@@ -70,7 +70,43 @@ int main(int argc, char** argv) {
                got.lo, got.hi, got.steps, got.done, got.maxiter);
     }
   }
-  printf("cases %ld closed %ld done %ld maxiter %ld mismatches %ld\n", n, closed, done, maxiter,
-         bad);
-  return bad == 0 ? 0 : 1;
+  // the probe's steps (probe_steps) against the loop: lo from 90.001 (or anywhere), stop bound
+  // T = hi - 0.1 with hi = thR over the whole angle range (binade 64-128 and 128-256 crossings),
+  // with and without the Snell bound thr; plus odd steps and bounds (ties, non-finite)
+  long pcases = 0, pbad = 0, psteps = 0;
+  for (long c = 0; c < n / 4; ++c) {
+    const double thR = (c % 7 == 0) ? 60.0 + 300.0 * U(rng) : 90.0 + 90.0 * U(rng);
+    double lo = (c % 5 == 0) ? 90.0 * U(rng) + 30.0 : 90.001;
+    const double T = thR - 0.1;
+    const bool use_thr = c % 2 == 0;
+    double thr = 90.0 + 90.0 * U(rng);
+    double step = 0.05;
+    if (c % 13 == 0) step = pow(2.0, -3 - (int)(U(rng) * 20)) * (1 + U(rng));
+    if (c % 17 == 0) step = 0.05 * (1 + 1e-3 * U(rng));
+    if (c % 101 == 0) thr = NAN;
+    if (c % 103 == 0) lo = INFINITY;
+    // the loop, step by step (capped: a non-finite bound may never stop it)
+    double ref = lo;
+    bool ref_stepped = false;
+    long k = 0;
+    while (((!use_thr || ref < thr) && !(ref > T)) && k < 100000) {
+      ref = ref + step;
+      ref_stepped = true;
+      ++k;
+    }
+    if (k >= 100000) continue;
+    bool st = false;
+    const double got = probe_steps(lo, step, T, thr, use_thr, st);
+    ++pcases;
+    psteps += k;
+    if (dbits(got) != dbits(ref) || st != ref_stepped) {
+      if (++pbad <= 10)
+        printf("PROBE MISMATCH lo=%.17g step=%.17g T=%.17g thr=%.17g use_thr=%d: ref %.17g (%d) "
+               "got %.17g (%d)\n", lo, step, T, thr, (int)use_thr, ref, (int)ref_stepped, got,
+               (int)st);
+    }
+  }
+  printf("cases %ld closed %ld done %ld maxiter %ld mismatches %ld probe_cases %ld probe_steps %ld "
+         "probe_mismatches %ld\n", n, closed, done, maxiter, bad, pcases, psteps, pbad);
+  return bad == 0 && pbad == 0 ? 0 : 1;
 }

@@ -73,7 +73,8 @@ def _run_case(solver, oracle_medium, depth_cm, hstep, a0, a1, astep, nq, seed):
     assert np.array_equal(packed[:-1, 10:20].T, host[1:11, 1:], equal_nan=True)
     assert np.isnan(packed[-1, 10:20]).all() and not packed[:, 20:].any()
     # row records: the row's usable-THD span inside the row and the values at its ends
-    rows = flat[ne * 32:].reshape(ne // asteps, 8)
+    from airiceraytracing_amd import _lib
+    rows = flat[ne * 32:].reshape(ne // asteps, _lib.LOOKUP_ROW_FLOATS)
     ri = rows.view(np.int32)
     r = np.arange(rows.shape[0])
     okr = ri[:, 7] == 1
@@ -82,6 +83,12 @@ def _run_case(solver, oracle_medium, depth_cm, hstep, a0, a1, astep, nq, seed):
     assert (s1 >= r[okr] * asteps).all() and (e1 <= r[okr] * asteps + asteps - 1).all()
     assert np.array_equal(rows[okr, 2], host[0][r[okr]])
     assert np.array_equal(rows[okr, 3], host[0][s1]) and np.array_equal(rows[okr, 5], host[1][s1])
+    # bisection trees: node 0 of the first height's tree is the THD at FindClosestTHD's first
+    # midpoint of (s1, e1), where the span is wide enough to take a step
+    tr = ri[okr, 23]
+    assert ((tr & 1) != 0).mean() > 0.9
+    wide = ((tr & 1) != 0) & (e1 - s1 >= 3)
+    assert np.array_equal(rows[okr, 8][wide], host[1][(s1[wide] + e1[wide]) // 2])
     rout, rok, rfl = oracle.table_lookup_batch(oracle_medium, oracle.lookup_table(host, og),
                                                src, dist, dep, ICE_CM, nthreads=NTHREADS)
     assert np.array_equal(fl, rfl), np.flatnonzero(fl != rfl)[:10]

@@ -19,5 +19,7 @@ def test_closed_form_lean_run_matches_the_steps(tmp_path):
     assert r.returncode == 0, r.stdout
     f = dict(zip(r.stdout.split()[0::2], map(int, r.stdout.split()[1::2])))
     assert f["mismatches"] == 0
+    # the probe's steps in closed form: bit-identical to the loop on every case
+    assert f["probe_mismatches"] == 0 and f["probe_cases"] > 0.2 * f["cases"]
     # most brackets take the closed form, and a good share of the runs end the solve
     assert f["closed"] > 0.6 * f["cases"] and f["done"] > 0.1 * f["closed"]
