@@ -35,7 +35,7 @@ namespace airice {
 
 namespace {
 
-constexpr int kLkBlock = 256;
+static_assert(kLkBlock == 256, "lookup_kernel's LDS window (airice_lookup.hpp) and grids");
 
 // Occupancy: the compiler's choice (87 VGPRs = 5 waves/SIMD).  Measured (1e6 cfg3 queries,
 // tools/gpu_ab_lookup.sh, identical outputs): 6 waves (80 VGPRs, 36 B/lane spilled) 138 against

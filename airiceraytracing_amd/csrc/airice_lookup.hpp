@@ -148,6 +148,8 @@ __host__ __device__ __forceinline__ LkTxhBins lk_closest_txh(const LkTable& T, d
 // interpolation height searches (s2, e2): a query then takes its first four steps from two 128-byte
 // lines it reads anyway instead of four dependent gathers into the THD column, and the rest of
 // the search and the linear scan from one short window of that column (lk_closest_thd_tree).
+constexpr int kLkBlock = 256;      // threads per block of the batch lookup_kernel (the LDS window
+                                   // below has one column per thread of such a block)
 constexpr int kLkTreeNodes = 15;  // bisection steps 0-3
 constexpr int kLkWindow = 12;     // THD entries the steps 4-7 and the scan may read
 struct LkTree {
@@ -378,13 +380,13 @@ __host__ __device__ __forceinline__ bool lk_closest_thd_tree(const LkTable& T, d
   const int n32 = (int)T.n;
   const int base = s <= n32 - kLkWindow ? s : n32 - kLkWindow;  // the window covers [s, e]
   // the window, indexed per lane: on the device in the block's LDS (one column of 4-byte slots
-  // per lane, kLkWindow rows 256 lanes apart: conflict-free, and each read one instruction where
+  // per lane, kLkWindow rows kLkBlock lanes apart: conflict-free, and each read one instruction where
   // a register multiplexer takes 11 selects); the lane reads only what it wrote
   const float* src = T.col[1] + base;
 #if defined(__HIP_DEVICE_COMPILE__)
-  __shared__ float s_win[kLkWindow][256];
-  float* w = &s_win[0][threadIdx.x & 255];
-  constexpr int ws = 256;
+  __shared__ float s_win[kLkWindow][kLkBlock];
+  float* w = &s_win[0][threadIdx.x % kLkBlock];  // launched with kLkBlock threads per block
+  constexpr int ws = kLkBlock;
   // three 16-byte loads at 4-byte alignment (gfx950 vector memory takes unaligned dwordx4)
   typedef float f4u __attribute__((ext_vector_type(4), aligned(4)));
 #pragma unroll
