@@ -1332,13 +1332,26 @@ __device__ __forceinline__ SolveResult solve_root(const DevMedium& M, const IceC
       if (!isfinite(f)) {
         phase = PH_BISECT;
       } else if (fabs(f) < tau) {
-        // at the root: guards a few tau either side, scaled by the local secant slope; a side
-        // whose guard already lies at the root needs none
-        dlt = 4.0 * tau * fabs((x2 - x1) * __builtin_amdgcn_rcp(f2 - f1));
-        const double Wq = 0.0;
-        const bool needL = !(x2 - gL <= Wq), needR = !(gR - x2 <= Wq);
-        phase = (dlt > 0.0 && dlt < (gR - gL)) ? (needL ? PH_G1 : (needR ? PH_G2 : PH_BISECT))
-                                               : PH_BISECT;
+        // at the root: guards a few tau either side, scaled by the local secant slope
+        const double sl = (x2 - x1) * __builtin_amdgcn_rcp(f2 - f1);  // dtheta / df
+        dlt = 4.0 * tau * fabs(sl);
+        const bool room = dlt > 0.0 && dlt < (gR - gL);
+        if (room && est >= 2) {
+          // x1 is a search point near the root, so the secant slope is the local one: f at
+          // x2 -+ dlt is f2 -+ 4 tau sign(sl) to first order, |.| >= 3 tau with the root
+          // between, and the guards take those signs without evaluating f there (DESIGN.md §4:
+          // a slope off by more than 4x would move the root by less than |f2| / f', far inside
+          // the bisection's last interval)
+          const double fm = sl > 0.0 ? -tau : tau;  // f(x2 - dlt)
+          guard(x2 - dlt, fm);
+          guard(x2 + dlt, -fm);
+          phase = PH_BISECT;
+        } else {
+          // the first search point (x1 is the bracket end): evaluate both guards; a side whose
+          // guard already lies at the root needs none
+          const bool needL = x2 > gL, needR = gR > x2;
+          phase = room ? (needL ? PH_G1 : (needR ? PH_G2 : PH_BISECT)) : PH_BISECT;
+        }
       } else {
         guard(x, f);
         if (est >= 12) phase = PH_BISECT;

@@ -1,7 +1,10 @@
 """The root finder's guarded bisection (evaluating f only at midpoints between the sign guards)
 must reproduce GSL bisection with f evaluated at every midpoint, bit for bit: same roots, same
 status bits, same outputs.  AIRICE_BISECT_EXACT=1 selects the every-midpoint form on the same
-device f, so the comparison isolates the sign prediction from the evaluation's rounding."""
+device f, so the comparison isolates the sign prediction from the evaluation's rounding.  Since
+round 4 the two guards around a converged secant search are placed from the secant slope instead
+of being evaluated; these batches check that the placed guards decide every
+midpoint as its evaluation does."""
 import os
 
 import numpy as np

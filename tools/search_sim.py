@@ -65,9 +65,9 @@ def solve(f, lo, hi, tau, strategy):
 
     fL, fR = ev(lo), ev(hi)
     if not (math.isfinite(fL) and math.isfinite(fR)):
-        return n, None
+        return n, None, float("nan")
     if (fL < 0) == (fR < 0) or abs(fL) < tau or abs(fR) < tau:
-        return n, None
+        return n, None, float("nan")
     gL, gR = lo, hi
     ul, uh = f32(math.tan(f32((180 - lo) * D2R))), f32(math.tan(f32((180 - hi) * D2R)))
     un = f32(uh - f32(fR) * f32(f32(uh - ul) / f32(fR - fL)))
@@ -108,6 +108,17 @@ def solve(f, lo, hi, tau, strategy):
             break
         if abs(f2) < tau:
             dlt = 4.0 * tau * abs((x2 - x1) / (f2 - f1))
+            if strategy == "model" and 0 < dlt < gR - gL and est >= 2:
+                # solve_root since round 4: guards placed by the secant slope, not evaluated
+                # (f(x2 -+ dlt) ~ f2 -+ 4 tau sign(slope))
+                left_neg = ((f2 - f1) / (x2 - x1)) > 0
+                for xg, neg in ((x2 - dlt, left_neg), (x2 + dlt, not left_neg)):
+                    if gL < xg < gR:
+                        if neg == (fL < 0):
+                            gL = xg
+                        else:
+                            gR = xg
+                break
             if 0 < dlt < gR - gL:
                 for xg in (x2 - dlt, x2 + dlt):
                     v = ev(xg)
@@ -125,8 +136,8 @@ def solve(f, lo, hi, tau, strategy):
         if est >= 12:
             break
     cnt = [0, tau]
-    gsl_midpoint_evals(lo, hi, gL, gR, f, fL, cnt)
-    return n + cnt[0], est
+    blo, bhi = gsl_midpoint_evals(lo, hi, gL, gR, f, fL, cnt)
+    return n + cnt[0], est, 0.5 * (blo + bhi)
 
 
 def main():
@@ -134,7 +145,9 @@ def main():
     m = oracle.load_atmosphere(os.path.join(ROOT, "airiceraytracing_amd", "data",
                                             "Atmosphere.dat.gz"))
     txh, dst, dep = cfg3_queries(4 * n, seed=2024)
-    res = {"base": [], "merge": []}
+    res = {"base": [], "merge": [], "model": []}
+    roots = {k: [] for k in res}
+    exact = []
     ests = []
     used = 0
     for i in range(len(txh)):
@@ -149,15 +162,25 @@ def main():
 
         tau = 1e-6 + 1e-10 * abs(D)
         for s in res:
-            k, e = solve(f, lo, hi, tau, s)
+            k, e, r = solve(f, lo, hi, tau, s)
             res[s].append(k)
+            roots[s].append(r)
             if s == "base" and e is not None:
                 ests.append(e)
+        # GSL's bisection evaluating every midpoint (the reference's root)
+        c = [0, float("inf")]
+        elo, ehi = gsl_midpoint_evals(lo, hi, -1e300, 1e300, f, f(lo), c)
+        exact.append(0.5 * (elo + ehi))
         used += 1
         if used >= n:
             break
+    ex = np.array(exact)
     for s, v in res.items():
-        print(f"{s}: {np.mean(v):.3f} evaluations per solve over {len(v)} queries")
+        rr = np.array(roots[s], dtype=float)
+        ok = np.isfinite(rr)
+        same = int(np.sum(rr[ok] == ex[ok]))
+        print(f"{s}: {np.mean(v):.3f} evaluations per solve over {len(v)} queries; root equal to "
+              f"the every-midpoint bisection on {same}/{int(ok.sum())}")
     print(f"search steps (base) {np.mean(ests):.3f}")
 
 
