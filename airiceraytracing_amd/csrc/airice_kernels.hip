@@ -1300,6 +1300,17 @@ __device__ __forceinline__ SolveResult solve_root(const DevMedium& M, const IceC
           status |= AIRICE_SOLVE_BAD_BRACKET;
           root_zero = true;
           phase = PH_DONE;
+        } else if constexpr (!WAVE) {
+          // this trip evaluated f at x = lo, the point gsl_root_fsolver_set evaluates next
+          // (f(lo)): the same point and arithmetic, so its value is PH_FLO's result and the lane
+          // goes on to f(hi) one trip earlier
+          if (!isfinite(f)) {
+            status |= AIRICE_SOLVE_NONFINITE_END;
+            phase = PH_BISECT;
+          } else {
+            fL = f;
+            phase = PH_FHI;
+          }
         }
       } else {
         lo = lo + 0.05;
@@ -1349,7 +1360,7 @@ __device__ __forceinline__ SolveResult solve_root(const DevMedium& M, const IceC
         } else {
           // the first search point (x1 is the bracket end): evaluate both guards; a side whose
           // guard already lies at the root needs none
-          const bool needL = x2 > gL, needR = gR > x2;
+          const bool needL = !(x2 - gL <= 0.0), needR = !(gR - x2 <= 0.0);
           phase = room ? (needL ? PH_G1 : (needR ? PH_G2 : PH_BISECT)) : PH_BISECT;
         }
       } else {
@@ -1644,7 +1655,13 @@ static inline int bisect_exact() {
 constexpr int kSortBuckets = 16;
 // 1024 queries per block: larger groups sort better, and a 16-wave block runs at 4 waves/SIMD
 // (128 VGPRs, some spilled) -- measured faster than 256 (3 waves, no spills), 512 and 768.
-constexpr int kRootsBlock = 1024;
+#ifndef AIRICE_RK_BLOCK
+#define AIRICE_RK_BLOCK 1024
+#endif
+#ifndef AIRICE_RK_VARIANT
+#define AIRICE_RK_VARIANT 0
+#endif
+constexpr int kRootsBlock = AIRICE_RK_BLOCK;
 constexpr int kRootsWaves = 4;  // 127 VGPRs: 4 waves/SIMD (5 and 6 spill and run slower)
 // batch-wide grouping: batches of at least kGroupMin queries (AIRICE_GROUP_MIN in the environment
 // overrides it; 0: never) are sorted across the whole batch and solved in kSortedBlock-thread
@@ -1659,9 +1676,38 @@ __device__ __forceinline__ void fallback_out_direct(const DevMedium& M, const Ic
                                                     long long k, const double* tab,
                                                     const Geometry& g, double root, int status);
 
+constexpr int kGroupAngles = 8;
+constexpr int kGroupHeights = 4;
+// The sort key is roots_kernel's straight-line-angle bucket, b = floor((thR - 90) * B / 90) with
+// thR = 180 - atan(x) deg, x = D / (H - ice - depth), evaluated without the atan: b >= j exactly
+// when x <= tan(90 deg * (1 - j / B)), so b counts the host-computed thresholds x lies below.
+// (The key only orders the work; results do not depend on it.)
+struct GroupKey {
+  double t[kGroupAngles];  // t[j - 1] = tan(90 deg * (1 - j / B)), j = 1 .. B-1
+};
+
+template <int IN>
+__device__ __forceinline__ int query_bucket(const DevMedium& M, const QueryArgs& Q, long long k,
+                                            const GroupKey& K) {
+  if (IN == IN_CM100 && !(Q.mask[k] & AIRICE_LOOKUP_FALLBACK)) return -1;  // not a fallback lane
+  double thR_unused;
+  const Geometry g = load_query<IN>(M, Q, k, thR_unused);
+  const double den = g.H - g.ice - g.depth;
+  int b = 0;
+  if (!(den > 0)) {
+    b = den < 0 ? kGroupAngles - 1 : 0;  // thR > 180 (clamped) / 90 or NaN
+  } else {
+#pragma unroll
+    for (int j = 0; j < kGroupAngles - 1; ++j) b += (g.D <= K.t[j] * den) ? 1 : 0;
+  }
+  const int span = top_layer(M, g.H) - bottom_layer(M, g.ice);
+  return b * kGroupHeights + (span < 0 ? 0 : (span > 3 ? 3 : span));
+}
+
 template <int IN>
 __global__ __launch_bounds__(kRootsBlock, kRootsWaves) void roots_kernel(DevMedium M, IceConsts I,
-                                                                         QueryArgs Q, Park park) {
+                                                                         QueryArgs Q, Park park,
+                                                                         GroupKey K) {
   __shared__ int s_count[kSortBuckets + 1];
   __shared__ int s_slot[kRootsBlock];
   const long long k0 = (long long)blockIdx.x * kRootsBlock;
@@ -1678,10 +1724,16 @@ __global__ __launch_bounds__(kRootsBlock, kRootsWaves) void roots_kernel(DevMedi
   // bucket of this lane's own query (unused lanes last)
   int bucket = kSortBuckets;
   if (kt < Q.n) {
-    double thR0;
-    (void)load_query<IN>(M, Q, kt, thR0);
-    const double b = (thR0 - 90.0) * (kSortBuckets / 90.0);
-    bucket = (b >= 0.0 && b < kSortBuckets) ? (int)b : ((b >= kSortBuckets) ? kSortBuckets - 1 : 0);
+    if (AIRICE_RK_VARIANT == 1) {
+      bucket = query_bucket<IN>(M, Q, kt, K) >> 1;  // 32 classes -> 16 (angle x span pairs)
+    } else if (AIRICE_RK_VARIANT == 2) {
+      bucket = 0;
+    } else {
+      double thR0;
+      (void)load_query<IN>(M, Q, kt, thR0);
+      const double b = (thR0 - 90.0) * (kSortBuckets / 90.0);
+      bucket = (b >= 0.0 && b < kSortBuckets) ? (int)b : ((b >= kSortBuckets) ? kSortBuckets - 1 : 0);
+    }
   }
   const int rank = atomicAdd(&s_count[bucket], 1);
   __syncthreads();
@@ -1718,42 +1770,16 @@ __global__ __launch_bounds__(kRootsBlock, kRootsWaves) void roots_kernel(DevMedi
 // queries in that order in small blocks that the CU replaces independently.  Each query is still
 // solved on its own and written by its index: results are identical either way.
 // ---------------------------------------------------------------------------
-constexpr int kGroupAngles = 8;   // straight-line-angle classes (16 measured +0.4 %)
+// kGroupAngles = 8 straight-line-angle classes (16 measured +0.4 %)
 // the classes within each angle class are the number of air layers the path spans (0-3+): a wave
 // then runs only the middle-layer segments its own queries have
-constexpr int kGroupHeights = 4;  // classes within each
+// kGroupHeights = 4 classes within each
 constexpr int kGroupBuckets = kGroupAngles * kGroupHeights;
 constexpr int kGroupItems = 2;  // queries per thread in the sort passes
 constexpr int kGroupThreads = 1024;  // threads per block of the sort passes
 constexpr int kGroupChunk = kGroupThreads * kGroupItems;  // queries per block and round
 constexpr int kGroupBlocks = 512;                     // blocks of the sort passes (at most)
 constexpr int kSortedBlock = 256;
-
-// The sort key is roots_kernel's straight-line-angle bucket, b = floor((thR - 90) * B / 90) with
-// thR = 180 - atan(x) deg, x = D / (H - ice - depth), evaluated without the atan: b >= j exactly
-// when x <= tan(90 deg * (1 - j / B)), so b counts the host-computed thresholds x lies below.
-// (The key only orders the work; results do not depend on it.)
-struct GroupKey {
-  double t[kGroupAngles];  // t[j - 1] = tan(90 deg * (1 - j / B)), j = 1 .. B-1
-};
-
-template <int IN>
-__device__ __forceinline__ int query_bucket(const DevMedium& M, const QueryArgs& Q, long long k,
-                                            const GroupKey& K) {
-  if (IN == IN_CM100 && !(Q.mask[k] & AIRICE_LOOKUP_FALLBACK)) return -1;  // not a fallback lane
-  double thR_unused;
-  const Geometry g = load_query<IN>(M, Q, k, thR_unused);
-  const double den = g.H - g.ice - g.depth;
-  int b = 0;
-  if (!(den > 0)) {
-    b = den < 0 ? kGroupAngles - 1 : 0;  // thR > 180 (clamped) / 90 or NaN
-  } else {
-#pragma unroll
-    for (int j = 0; j < kGroupAngles - 1; ++j) b += (g.D <= K.t[j] * den) ? 1 : 0;
-  }
-  const int span = top_layer(M, g.H) - bottom_layer(M, g.ice);
-  return b * kGroupHeights + (span < 0 ? 0 : (span > 3 ? 3 : span));
-}
 
 // Pass 1: the key of every query and each block's bucket counts, bucket-major:
 // cnt[b * nblocks + block] (no global atomics: thousands of blocks adding into a few counters
@@ -2203,6 +2229,16 @@ hipError_t scratch_alloc(void** p, size_t bytes, hipStream_t st) {
   return hipMallocFromPoolAsync(p, bytes, pool, st);
 }
 
+static const GroupKey& group_thresholds() {
+  static const GroupKey K = [] {
+    GroupKey k{};
+    for (int j = 1; j < kGroupAngles; ++j)
+      k.t[j - 1] = tan(M_PI / 2 * (1.0 - (double)j / kGroupAngles));
+    return k;
+  }();
+  return K;
+}
+
 size_t group_min_batch() {
   static const long long v = getenv("AIRICE_GROUP_MIN") ? atoll(getenv("AIRICE_GROUP_MIN"))
                                                          : kGroupMin;
@@ -2224,16 +2260,12 @@ static int launch_roots(const DevMedium& M, const IceConsts& I, const QueryArgs&
   if (IN == IN_CM100 || group_min == 0 || n < group_min ||
       (park.stats != nullptr && !AIRICE_SORTED_STATS) || n >= (1ull << 31)) {
     ktimer_begin(KT_ROOTS, st);
-    hipLaunchKernelGGL((roots_kernel<IN>), roots_grid(n), dim3(kRootsBlock), 0, st, M, I, Q, park);
+    hipLaunchKernelGGL((roots_kernel<IN>), roots_grid(n), dim3(kRootsBlock), 0, st, M, I, Q, park,
+                       group_thresholds());
     ktimer_end(KT_ROOTS, st);
     return launch_ok();
   }
-  static const GroupKey thresholds = [] {
-    GroupKey K{};
-    for (int j = 1; j < kGroupAngles; ++j)
-      K.t[j - 1] = tan(M_PI / 2 * (1.0 - (double)j / kGroupAngles));
-    return K;
-  }();
+  const GroupKey& thresholds = group_thresholds();
   // at most kGroupBlocks blocks in the two passes (each scatter block reads every block's
   // counts); larger batches give each block several chunks
   const size_t chunks = (n + kGroupChunk - 1) / kGroupChunk;
