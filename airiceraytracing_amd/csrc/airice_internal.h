@@ -36,8 +36,9 @@ int launch_hdtip(const DevMedium& M, const IceConsts& I, const double* src, cons
                  uint8_t* ok, hipStream_t st);
 // Stream-ordered scratch from a library-owned pool that keeps freed blocks (hipFreeAsync).
 hipError_t scratch_alloc(void** p, size_t bytes, hipStream_t st);
-// Batch size from which the minimizer and the table lookup group their queries (AIRICE_GROUP_MIN).
-size_t group_min_batch();
+// Batch size from which the minimizer groups the queries of source `in` batch-wide
+// (AIRICE_GROUP_MIN overrides it; 0 when a source never groups by default).
+size_t group_min_batch(int in);
 // Table lookup: lookup_kernel, then the masked minimizer fallback for AIRICE_LOOKUP_FALLBACK
 // lanes (airice_lookup.hip / airice_kernels.hip).
 int launch_lookup(const DevMedium& M, const IceConsts& I, const airice_lookup_table* t,

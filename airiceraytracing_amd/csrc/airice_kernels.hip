@@ -1655,17 +1655,11 @@ static inline int bisect_exact() {
 constexpr int kSortBuckets = 16;
 // 1024 queries per block: larger groups sort better, and a 16-wave block runs at 4 waves/SIMD
 // (128 VGPRs, some spilled) -- measured faster than 256 (3 waves, no spills), 512 and 768.
-#ifndef AIRICE_RK_BLOCK
-#define AIRICE_RK_BLOCK 1024
-#endif
-#ifndef AIRICE_RK_VARIANT
-#define AIRICE_RK_VARIANT 0
-#endif
-constexpr int kRootsBlock = AIRICE_RK_BLOCK;
+constexpr int kRootsBlock = 1024;
 constexpr int kRootsWaves = 4;  // 127 VGPRs: 4 waves/SIMD (5 and 6 spill and run slower)
-// batch-wide grouping: batches of at least kGroupMin queries (AIRICE_GROUP_MIN in the environment
-// overrides it; 0: never) are sorted across the whole batch and solved in kSortedBlock-thread
-// blocks (roots_sorted_kernel)
+// batch-wide grouping: trace (IN_TRACE) batches of at least kGroupMin queries are sorted across
+// the whole batch and solved in kSortedBlock-thread blocks (roots_sorted_kernel; group_min_batch:
+// the other sources stay block-local, AIRICE_GROUP_MIN in the environment overrides it)
 constexpr long long kGroupMin = 65536;
 
 // Stage 2 of the lookup fallback with the root handed over in registers (lookup_fallback_kernel):
@@ -1676,7 +1670,9 @@ __device__ __forceinline__ void fallback_out_direct(const DevMedium& M, const Ic
                                                     long long k, const double* tab,
                                                     const Geometry& g, double root, int status);
 
-constexpr int kGroupAngles = 8;
+constexpr int kGroupAngles = 8;   // straight-line-angle classes (16 measured +0.4 %)
+// the classes within each angle class are the number of air layers the path spans (0-3+): a wave
+// then runs only the middle-layer segments its own queries have
 constexpr int kGroupHeights = 4;
 // The sort key is roots_kernel's straight-line-angle bucket, b = floor((thR - 90) * B / 90) with
 // thR = 180 - atan(x) deg, x = D / (H - ice - depth), evaluated without the atan: b >= j exactly
@@ -1706,8 +1702,7 @@ __device__ __forceinline__ int query_bucket(const DevMedium& M, const QueryArgs&
 
 template <int IN>
 __global__ __launch_bounds__(kRootsBlock, kRootsWaves) void roots_kernel(DevMedium M, IceConsts I,
-                                                                         QueryArgs Q, Park park,
-                                                                         GroupKey K) {
+                                                                         QueryArgs Q, Park park) {
   __shared__ int s_count[kSortBuckets + 1];
   __shared__ int s_slot[kRootsBlock];
   const long long k0 = (long long)blockIdx.x * kRootsBlock;
@@ -1724,16 +1719,10 @@ __global__ __launch_bounds__(kRootsBlock, kRootsWaves) void roots_kernel(DevMedi
   // bucket of this lane's own query (unused lanes last)
   int bucket = kSortBuckets;
   if (kt < Q.n) {
-    if (AIRICE_RK_VARIANT == 1) {
-      bucket = query_bucket<IN>(M, Q, kt, K) >> 1;  // 32 classes -> 16 (angle x span pairs)
-    } else if (AIRICE_RK_VARIANT == 2) {
-      bucket = 0;
-    } else {
-      double thR0;
-      (void)load_query<IN>(M, Q, kt, thR0);
-      const double b = (thR0 - 90.0) * (kSortBuckets / 90.0);
-      bucket = (b >= 0.0 && b < kSortBuckets) ? (int)b : ((b >= kSortBuckets) ? kSortBuckets - 1 : 0);
-    }
+    double thR0;
+    (void)load_query<IN>(M, Q, kt, thR0);
+    const double b = (thR0 - 90.0) * (kSortBuckets / 90.0);
+    bucket = (b >= 0.0 && b < kSortBuckets) ? (int)b : ((b >= kSortBuckets) ? kSortBuckets - 1 : 0);
   }
   const int rank = atomicAdd(&s_count[bucket], 1);
   __syncthreads();
@@ -1770,10 +1759,6 @@ __global__ __launch_bounds__(kRootsBlock, kRootsWaves) void roots_kernel(DevMedi
 // queries in that order in small blocks that the CU replaces independently.  Each query is still
 // solved on its own and written by its index: results are identical either way.
 // ---------------------------------------------------------------------------
-// kGroupAngles = 8 straight-line-angle classes (16 measured +0.4 %)
-// the classes within each angle class are the number of air layers the path spans (0-3+): a wave
-// then runs only the middle-layer segments its own queries have
-// kGroupHeights = 4 classes within each
 constexpr int kGroupBuckets = kGroupAngles * kGroupHeights;
 constexpr int kGroupItems = 2;  // queries per thread in the sort passes
 constexpr int kGroupThreads = 1024;  // threads per block of the sort passes
@@ -2239,10 +2224,17 @@ static const GroupKey& group_thresholds() {
   return K;
 }
 
-size_t group_min_batch() {
-  static const long long v = getenv("AIRICE_GROUP_MIN") ? atoll(getenv("AIRICE_GROUP_MIN"))
-                                                         : kGroupMin;
-  return v > 0 ? (size_t)v : 0;
+// Measured with the slope-placed guards (round 4): cfg3 (IN_M, 1e6) 0.241 ms per call
+// block-local against 0.276 ms grouped -- four to five evaluations per query leave the 1,024-query
+// blocks' angle sort as good as the batch-wide one, and the grouping passes and the stage-2 gather
+// cost more -- while cfg5 (IN_TRACE, 1e7, Tx up to 20 km, per-query ice) takes 2.23 ms grouped
+// against 2.53 block-local.  So the batch-wide grouping is the default of the trace source only;
+// AIRICE_GROUP_MIN overrides it for every source (0: never group).
+size_t group_min_batch(int in) {
+  static const char* env = getenv("AIRICE_GROUP_MIN");
+  static const long long v = env ? atoll(env) : -1;
+  if (v >= 0) return (size_t)v;
+  return in == IN_TRACE ? (size_t)kGroupMin : 0;
 }
 
 // Stage 1 of every minimizer launch: roots_kernel (block-local grouping) for small batches and
@@ -2254,14 +2246,13 @@ static int launch_roots(const DevMedium& M, const IceConsts& I, const QueryArgs&
                         const Park& park, size_t n, hipStream_t st, SortedPark& sp, void*& ws) {
   sp = SortedPark{nullptr, nullptr};
   ws = nullptr;
-  const size_t group_min = group_min_batch();
+  const size_t group_min = group_min_batch(IN);
   // (the table lookup's fallback pass stays block-local: its batch is the whole lookup batch,
   // of which typically well under 1 % of lanes are fallback lanes)
   if (IN == IN_CM100 || group_min == 0 || n < group_min ||
       (park.stats != nullptr && !AIRICE_SORTED_STATS) || n >= (1ull << 31)) {
     ktimer_begin(KT_ROOTS, st);
-    hipLaunchKernelGGL((roots_kernel<IN>), roots_grid(n), dim3(kRootsBlock), 0, st, M, I, Q, park,
-                       group_thresholds());
+    hipLaunchKernelGGL((roots_kernel<IN>), roots_grid(n), dim3(kRootsBlock), 0, st, M, I, Q, park);
     ktimer_end(KT_ROOTS, st);
     return launch_ok();
   }

@@ -460,10 +460,11 @@ def main(argv=None, make_backend=None, json_path=None):
             "ms_per_call": call_ms, "kernel_ms": call_ms, **stage,
             "solved_fraction": float(solved.mean()),
             "unpinned_fraction": float(((st_h & 35) != 0).mean()),
-            # dominant kernel: the root finder; algorithmic bytes per query = 24 B of inputs +
-            # 4 B perm read, 8 B root + 1 B status parked
-            "roofline": counter_roofline("roots_sorted_kernel", args.solve_n,
-                                         stage.get("roots_kernel_ms"), pmc, 37.0),
+            # dominant kernel: the root finder (block-local grouping, roots_kernel: the default of
+            # this source since round 4); algorithmic bytes per query = 24 B of inputs, 8 B root +
+            # 8 B status parked in the output slots
+            "roofline": counter_roofline("roots_kernel", args.solve_n,
+                                         stage.get("roots_kernel_ms"), pmc, 40.0),
         }
         out_h = out.cpu().numpy()
 
