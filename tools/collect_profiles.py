@@ -23,7 +23,7 @@ DST = os.path.join(ROOT, "profiles")
 # item -> (kernel name prefix in the stats file, path of the bench-reported ms in the line)
 CHECKS = {
     "table": [("airice::table_kernel<false", ("roofline", "kernel_ms"))],
-    "solve": [("void airice::roots_kernel<0>", ("minimizer", "roots_kernel_ms")),
+    "solve": [("airice::roots_kernel<0>", ("minimizer", "roots_kernel_ms")),
               ("airice::solve_out_kernel<0>", ("minimizer", "out_kernel_ms"))],
     "lookup": [("airice::(anonymous namespace)::lookup_kernel", ("table_lookup", "lookup_kernel_ms"))],
     "cfg4": [("airice::table_kernel<false", ("table_cfg4", "kernel_ms"))],
