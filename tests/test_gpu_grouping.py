@@ -1,7 +1,8 @@
 """The minimizer's batch-wide grouping (roots_sorted_kernel) against its block-local
-form (roots_kernel): large batches are sorted across the whole batch by straight-line angle and
-solved in that order, but every query is still solved on its own and written by its index, so
-the two schedules must give bit-identical outputs.  Both are run in fresh processes
+form (roots_kernel): a grouped batch is sorted across the whole batch by straight-line angle and
+layer span and solved in that order (the default of the trace source), a block-local one inside
+each 1,024-query block (the default of the other sources), but every query is still solved on its
+own and written by its index, so the two schedules must give bit-identical outputs.  Both are run in fresh processes
 (AIRICE_GROUP_MIN=0: never group; =1: always group) through the minimizer entries --
 airice_solve_launch, airice_hdtip_launch and airice_trace_ice_to_air_launch, plus the table
 lookup, whose fallback pass stays block-local in both -- and the grouped solve is also checked

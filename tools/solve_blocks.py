@@ -4,7 +4,9 @@ and each phase's update -- the instruction streams the VALU issue counts (pmc_su
 made of.
 
     tools/build_variant.sh airiceraytracing_amd/csrc /tmp/stats.so -DAIRICE_SORTED_STATS=1
-    AB_LIB=/tmp/stats.so python tools/solve_blocks.py [n]
+    AIRICE_GROUP_MIN=1 AB_LIB=/tmp/stats.so python tools/solve_blocks.py [n]
+
+(AIRICE_GROUP_MIN=1: the batch-wide grouping, since round 4 the default of the trace source only.)
 """
 import ctypes
 import json

@@ -1,6 +1,7 @@
 """Evaluation counts of the grouped root finder in the order its waves run them (debug, GPU box).
 
-Needs a library built with -DAIRICE_SORTED_STATS=1 (AB_LIB=<that .so>): the per-query counts are
+Needs a library built with -DAIRICE_SORTED_STATS=1 (AB_LIB=<that .so>) and AIRICE_GROUP_MIN=1 (the
+batch-wide grouping, since round 4 the default of the trace source only): the per-query counts are
 then recorded by sorted position, so 64 consecutive entries are one wave of roots_sorted_kernel.
 Prints the mean evaluations per query, the mean of the per-wave maxima (a wave runs until its last
 lane is done) and what a trip cap with a continuation pass would leave for each cap.
