@@ -162,7 +162,8 @@ struct LkRow {
   double mt1, mt2; // column 1 (THD) at s1, at s2
   bool tree1, tree2;  // the node values below are usable (every node's midpoint inside the table)
   const float* rec;   // the row record: tree 1 at floats 8-22, tree 2 at floats 32-46
-  float4 top1, top2;  // nodes 0-3 of each tree (levels 0 and 1 without a dependent read)
+  float4 top1, top2;    // nodes 0-3 of each tree (levels 0 and 1 without a dependent read)
+  float4 top1b, top2b;  // nodes 4-7 (level 2 with node 3)
 };
 __host__ __device__ __forceinline__ float lk_bits_f(int32_t i) {
   float f;
@@ -277,6 +278,8 @@ __host__ __device__ __forceinline__ bool lk_row(const LkTable& T, long long inde
   R.rec = reinterpret_cast<const float*>(p);
   R.top1 = p[2];
   R.top2 = p[8];
+  R.top1b = p[3];
+  R.top2b = p[9];
   const int trees = lk_bits_i(R.rec[23]);
   R.tree1 = (trees & 1) != 0;
   R.tree2 = (trees & 2) != 0;
@@ -359,8 +362,8 @@ __host__ __device__ __forceinline__ bool lk_step32(double v, double P, int& s, i
 // row fold admits spans below 2^31 only).
 __host__ __device__ __forceinline__ bool lk_closest_thd_tree(const LkTable& T, double P, long long s_in,
                                                              long long e_in, const float* t,
-                                                             float4 top, LkThdBins& out,
-                                                             LkThdPair& pr) {
+                                                             float4 top, float4 topb,
+                                                             LkThdBins& out, LkThdPair& pr) {
   if (s_in < 0 || e_in < s_in || T.n < kLkWindow || T.n >= (1LL << 31)) return false;
   int s = (int)s_in, e = (int)e_in;
   bool fin = false;
@@ -369,9 +372,12 @@ __host__ __device__ __forceinline__ bool lk_closest_thd_tree(const LkTable& T, d
   for (int lvl = 0; lvl < 4; ++lvl) {
     fin = fin || e - s < 3;
     if (!fin) {
-      // the node's value: levels 0 and 1 from the record's first 16 bytes, read with the row,
-      // levels 2 and 3 from the record (one dependent 4-byte read of a line the lane has read)
-      const float v = lvl == 0 ? top.x : lvl == 1 ? (k == 1 ? top.y : top.z) : t[k];
+      // the node's value: levels 0-2 from the record's first 32 bytes, read with the row, level 3
+      // from the record (one dependent 4-byte read of a line the lane has read)
+      const float v = lvl == 0   ? top.x
+                      : lvl == 1 ? (k == 1 ? top.y : top.z)
+                      : lvl == 2 ? (k == 3 ? top.w : k == 4 ? topb.x : k == 5 ? topb.y : topb.z)
+                                 : t[k];
       const bool up = lk_step32((double)v, P, s, e, fin);
       k = 2 * k + (up ? 1 : 2);
     }
@@ -449,12 +455,13 @@ __host__ __device__ __forceinline__ void lk_row_params(const LkTable& T, double 
                                               double par[10], double* closest, int& fl,
                                               const double* max_thd_row = nullptr,
                                               const float* tree = nullptr,
-                                              float4 tree_top = float4{}) {
+                                              float4 tree_top = float4{},
+                                              float4 tree_topb = float4{}) {
   const double max_thd = max_thd_row != nullptr ? *max_thd_row : lk_at(T, 1, s, fl);
   if (D <= max_thd) {
     LkThdPair pr;
     LkThdBins b;
-    if (tree == nullptr || !lk_closest_thd_tree(T, D, s, e, tree, tree_top, b, pr)) {
+    if (tree == nullptr || !lk_closest_thd_tree(T, D, s, e, tree, tree_top, tree_topb, b, pr)) {
       pr.have_pair = false;
       b = lk_closest_thd(T, D, s, e, fl, pr);
     }
@@ -496,13 +503,13 @@ __host__ __device__ __forceinline__ void lk_par_values(const LkTable& T, double 
   double c1 = 0;
   *h1 = fast ? R.h1 : lk_at(T, 0, b.s1, fl);
   lk_row_params(T, D, b.s1, b.e1, par1, &c1, fl, fast ? &R.mt1 : nullptr,
-                fast && R.tree1 ? R.rec + 8 : nullptr, R.top1);
+                fast && R.tree1 ? R.rec + 8 : nullptr, R.top1, R.top1b);
   *h2 = *h1;
   if (b.c1 != 0 && H > min_h && b.s2 < T.n - 1) {
     *h2 = fast ? R.h2 : lk_at(T, 0, b.s2, fl);
     double c2 = 0;
     lk_row_params(T, D, b.s2, b.e2, par2, &c2, fl, fast ? &R.mt2 : nullptr,
-                  fast && R.tree2 ? R.rec + 32 : nullptr, R.top2);
+                  fast && R.tree2 ? R.rec + 32 : nullptr, R.top2, R.top2b);
   } else {
 #pragma unroll
     for (int ip = 0; ip < 10; ++ip) par2[ip] = par1[ip];
