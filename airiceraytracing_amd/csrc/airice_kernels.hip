@@ -2831,10 +2831,26 @@ __global__ __launch_bounds__(kFbBlock, kRootsWaves) void lookup_fallback_kernel(
   if (threadIdx.x == 0) s_n = 0;
   __syncthreads();
   const long long c0 = (long long)blockIdx.x * kFbChunk;
+  static_assert(kFbChunk == 16 * kFbBlock, "16 flags per thread");
+  const int j0 = 16 * (int)threadIdx.x;  // this thread's 16 consecutive flags
+  if (c0 + kFbChunk <= Q.n && (reinterpret_cast<uintptr_t>(Q.mask + c0) & 15) == 0) {
+    // one 16-byte load per thread (a full, aligned chunk): the scan is one round trip
+    const uint4 v = *reinterpret_cast<const uint4*>(Q.mask + c0 + j0);
+    const unsigned w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      if (w[q] & (AIRICE_LOOKUP_FALLBACK * 0x01010101u)) {
+#pragma unroll
+        for (int b = 0; b < 4; ++b)
+          if ((w[q] >> (8 * b)) & AIRICE_LOOKUP_FALLBACK) s_list[atomicAdd(&s_n, 1)] = j0 + 4 * q + b;
+      }
+    }
+  } else {
 #pragma unroll 4
-  for (int j = threadIdx.x; j < kFbChunk; j += kFbBlock) {
-    const long long k = c0 + j;
-    if (k < Q.n && (Q.mask[k] & AIRICE_LOOKUP_FALLBACK)) s_list[atomicAdd(&s_n, 1)] = j;
+    for (int j = j0; j < j0 + 16; ++j) {
+      const long long k = c0 + j;
+      if (k < Q.n && (Q.mask[k] & AIRICE_LOOKUP_FALLBACK)) s_list[atomicAdd(&s_n, 1)] = j;
+    }
   }
   __syncthreads();
   const int cnt = s_n;
