@@ -15,4 +15,4 @@ __all__ = [
     "LookupTable", "Medium", "VARIANT_MULTIRAY",
     "VARIANT_PYWRAPPER", "build", "default_atmosphere_path", "lib", "load_medium", "make_grid",
 ]
-__version__ = "0.1.0"
+__version__ = "0.2.0"

@@ -103,8 +103,18 @@ class LookupTable(ctypes.Structure):
     ]
 
 
-LOOKUP_ENTRY_FLOATS = 32  # AIRICE_LOOKUP_ENTRY_FLOATS
+LOOKUP_ENTRY_FLOATS = 16  # AIRICE_LOOKUP_ENTRY_FLOATS (pack format 2)
 LOOKUP_ROW_FLOATS = 64  # AIRICE_LOOKUP_ROW_FLOATS
+
+
+def lookup_rows_offset(n):
+    """AIRICE_LOOKUP_ROWS_OFFSET: first float of the row records in the packed copy."""
+    return (n * LOOKUP_ENTRY_FLOATS + 31) // 32 * 32
+
+
+def lookup_pack_floats(n, asteps):
+    """AIRICE_LOOKUP_PACK_FLOATS: floats of the whole packed copy."""
+    return lookup_rows_offset(n) + n // asteps * LOOKUP_ROW_FLOATS + (asteps + 3) // 4 * 4 + 4
 
 
 class SingleRayInfo(ctypes.Structure):
@@ -140,7 +150,7 @@ EXPORTED_SYMBOLS = (
     "airice_nz_air", "airice_nz_ice", "airice_grid_init", "airice_table_launch",
     "airice_table_launch_multi",
     "airice_table_host", "airice_rays_launch", "airice_solve_launch", "airice_solve_host",
-    "airice_hdtip_launch", "airice_table_lookup_launch", "airice_lookup_pack", "airice_single_ray_plan",
+    "airice_hdtip_launch", "airice_table_lookup_launch", "airice_lookup_pack", "airice_lookup_pack_floats", "airice_single_ray_plan",
     "airice_single_ray_launch", "airice_single_ray_host", "airice_trace_ice_to_air_launch",
     "airice_trace_ice_to_air_host", "airice_rtf_outputs", "airice_rtf_eval",
     "airice_rtf_eval_variant", "Py_TraceIceToAir", "airice_device_count", "airice_set_device", "airice_malloc",
@@ -202,7 +212,8 @@ def lib() -> ctypes.CDLL:
         "airice_hdtip_launch": ([M, P, P, P, D, S, P, S, P, P], I),
         "airice_table_lookup_launch": ([M, ctypes.POINTER(LookupTable), P, P, P, D, S, P, S, P,
                                         P, P], I),
-        "airice_lookup_pack": ([ctypes.POINTER(LookupTable), P, P], I),
+        "airice_lookup_pack": ([ctypes.POINTER(LookupTable), P, S, P], I),
+        "airice_lookup_pack_floats": ([S, ctypes.c_int32], S),
         "airice_single_ray_plan": ([M, D, D, D, D, ctypes.POINTER(SingleRayInfo)], I),
         "airice_single_ray_launch": ([M, D, D, D, D, P, P, P, S, P], I),
         "airice_single_ray_host": ([M, D, D, D, D, P, P, P, S], I),

@@ -263,7 +263,7 @@ using namespace airice;
 extern "C" {
 
 const char* airice_last_error(void) { return g_err; }
-const char* airice_version(void) { return "airice-mi355x 0.1.0 (gfx950, fp64)"; }
+const char* airice_version(void) { return "airice-mi355x 0.2.0 (gfx950, fp64; lookup pack format 2)"; }
 
 int airice_atmosphere_parse(const char* text, size_t len, int variant, airice_medium* out) {
   if (text == nullptr || out == nullptr) {

@@ -46,6 +46,9 @@ constexpr int kTableWaves = 8;
 #ifndef AIRICE_RAY_STAMP
 #define AIRICE_RAY_STAMP 0
 #endif
+#ifndef AIRICE_NO_CHECK
+#define AIRICE_NO_CHECK 0
+#endif
 #ifndef AIRICE_SORTED_STATS
 #define AIRICE_SORTED_STATS 0
 #endif
@@ -928,12 +931,7 @@ __device__ __forceinline__ Geometry shift(double H, double D, double ice, double
   return g;
 }
 
-// Root finding of Air2IceRayTracing (.cc:1487-1521): the probe loop, gsl_root_fsolver_set
-// and the FindFunctionRoot driver (.cc:340-374) with gsl_root_fsolver_bisection +
-// gsl_root_test_interval(lo, hi, 0, 1e-9) semantics, as one per-lane state machine with a
-// single evaluation site: lanes that are probing, setting up the bracket or bisecting share
-// each evaluation instead of waiting for each other (the probe runs in ~7% of queries).
-// An uninitialised solver state (non-finite bracket end) is modelled as zeros.
+// What the root finder returns for one query.
 struct SolveResult {
   double root;
   int status;
@@ -962,115 +960,131 @@ __device__ unsigned long long g_dbg_exec[16];
   } while (0)
 #endif
 
-template <bool WAVE = false>
-__device__ __forceinline__ SolveResult solve_root(const DevMedium& M, const IceConsts& I,
-                                                  const Geometry& g, double thR, bool exact,
-                                                  const double* tab) {
-#if AIRICE_SCALAR_STAMP
-  const unsigned long long ts0 = __builtin_amdgcn_s_memtime();
-  int t_lean = 0;
-#endif
-  int status = 0;
+// The root finder of one query as a state machine with a single evaluation site (RootSearch):
+// begin() sets up the bracket and the probe, next_point() runs the evaluation-free bisection
+// steps and returns the point to evaluate next, update() takes f there.  solve_root() below drives
+// one query to its root.
+struct RootSearch {
   Query q;
-  q.depth_pos = g.depth_pos;
-  q.dist = g.D;
-  q.top = top_layer(M, g.H);
-  q.bot = bottom_layer(M, g.ice);
-  q.tx = air_slim(M, g.H, q.n_tx);
-  double n_ice;
-  q.iceair = air_slim(M, g.ice, n_ice);
-  // Rx end of the top layer: the ice, or the layer's lower boundary (stop endpoint)
-  const bool to_ice = q.top == q.bot;
-  q.rtop = pick(to_ice, q.iceair, stop_slim(M, q.top));
-  q.n_rtop = to_ice ? n_ice : stop_n(M, q.top);
-  const double x_rtop = to_ice ? g.ice : sel5(M.atm, q.top);
-  if (x_rtop == g.H) {  // zero-length top segment (see segment())
-    q.rtop = q.tx;
-    q.n_rtop = q.n_tx;
-  }
-  q.ratio = q.n_tx / q.n_rtop;
-  {
-    const double e = exp(M.negC_ice * g.depth_pos);
-    const double y = M.A_ice + M.B_ice * e;
-    // 1/C of the ice from the host-folded surface endpoint (the same IEEE quotient): a kernel
-    // argument, so it occupies no VGPRs across the loop
-    q.rx = Slim{y * y, M.A_ice * y, M.negC_ice * g.depth_pos, I.ice0.invC};
-  }
-
-  double lo = thR - 16;
-  double hi = thR;
-  int phase = PH_FLO;
-  bool probe_bad = false;  // the probe ended with lo > hi: the reference then reports root 0
-  if (M.const_air) lo = 90;  // pythonwrapper constant air index: [90, thR], no probe (.cc:978-980)
-  if (!M.const_air && lo < 90.001) {
-    lo = 90.001;
-    phase = PH_PROBE;
-    // While n(Tx) sin(180-lo) exceeds 1 by a margin (1e-6) the ray parameter L > A_air = 1,
-    // so sqrt(A^2-L^2) and THD are NaN whatever the rounding: those probe steps need no
-    // evaluation (.cc:1496-1509 would reject each of them).
-    if (q.top >= q.bot) {
-      const double thr = 180 - asin((1 + 1e-6) / q.n_tx) * M.r2d;  // NaN if n(Tx) < 1+1e-6
-      // while (lo < thr && !(lo > hi - 0.1)) lo = lo + 0.05, in closed form (airice_lean.hpp)
-      bool stepped;
-      lo = probe_steps(lo, 0.05, hi - 0.1, thr, true, stepped);
-      if (stepped) status |= AIRICE_SOLVE_PROBED;
-    } else {
-      // no air layer (Tx above the atmosphere, e.g. the table lookup's x100 fallback): THD in
-      // air is 0 at every angle, so the probe only stops at lo > hi - 0.1 -- up to ~900 steps
-      // whose outcome needs no evaluation, taken in closed form (airice_lean.hpp)
-      bool stepped;
-      lo = probe_steps(lo, 0.05, hi - 0.1, 0.0, false, stepped);
-      if (stepped) status |= AIRICE_SOLVE_PROBED;
-      if (hi < 90.001 && hi > 90.00) hi = 90.05;
-      phase = PH_FLO;
-      if (lo > hi) {
-        status |= AIRICE_SOLVE_BAD_BRACKET;
-        probe_bad = true;
-        phase = PH_DONE;
-      }
-    }
-  } else {
-    if (hi < 90.001 && hi > 90.00) hi = 90.05;
-    if (lo > hi) {  // gsl_root_fsolver_set: EINVAL, nothing initialised
-      status |= AIRICE_SOLVE_BAD_BRACKET;
-      phase = PH_DONE;
-    }
-  }
-  // GSL's reported root is 0.5 (lo + hi) of the final bracket on every path (each iterate sets it
-  // so, and the exact-zero exits make lo == hi), except the failed probe, which reports 0: the
-  // root is formed once at the end instead of being carried through the loop
-  bool root_zero = probe_bad;
-  double f_lower = 0.0, f_upper = 0.0;
-  const double tol = 0.000000001;
-  int iter = 0;
+  double lo, hi;
+  double f_lower, f_upper;
+  double tau;
   // Sign guards.  f(theta) = D - THD(theta) is monotone in theta wherever it is finite, so
   // between two exactly evaluated points with the same sign and |f| >= tau (far above the
   // evaluation's rounding noise) every point has that sign.  gL / gR: the innermost evaluated
   // points with the sign of f(lo) / f(hi); okL / okR: |f(lo)| / |f(hi)| >= tau, so the guard
-  // regions [lo, gL] / [gR, hi] are safe.  A secant search finds the root, two guard
-  // evaluations straddle it, and the bisection then evaluates f only at midpoints between the
-  // guards: the same midpoints, signs and root as evaluating every one
-  // (tests/test_gpu_bisect_replay.py checks this bit for bit against AIRICE_BISECT_EXACT=1).
-  const double tau = 1e-6 + 1e-10 * fabs(g.D);
-  bool okL = false, okR = false;
-  double gL = 0.0, fL = 0.0, gR = 0.0, fR = 0.0;  // fL holds f(lo) between PH_FLO and PH_FHI
+  // regions [lo, gL] / [gR, hi] are safe.  A secant search finds the root, two guards straddle
+  // it, and the bisection then evaluates f only at midpoints between the guards: the same
+  // midpoints, signs and root as evaluating every one (tests/test_gpu_bisect_replay.py checks
+  // this bit for bit against AIRICE_BISECT_EXACT=1).
+  double gL, fL, gR, fR;  // fL holds f(lo) between PH_FLO and PH_FHI
   // secant search for the root: the first step in u = tan(180 - theta), where THD is close to
   // linear (a straight ray's is exactly H u; single precision is plenty for a first guess), then
-  // secant steps in theta on the last two points (x1, f1), (x2, f2)
-  double x1 = 0.0, f1 = 0.0, x2 = 0.0, f2 = 0.0;
-  // the point before (x1, f1): from the second search point on the search steps by inverse
-  // quadratic interpolation on the last three points (the secant step plus a curvature term)
-  double x0 = 0.0, f0 = 0.0;
-  // PH_G1/G2: guards at x2 -/+ dlt, where x2 is the secant search's last point (it stays put after
-  // the search) and dlt lives in x1 (dead once the search ends)
-  double& dlt = x1;
-  int est = 0, n_eval = 0, n_inside = 0;
-  // WAVE: f(lo) and f(hi), and the two guards, are independent pairs of points; the wave evaluates
-  // each pair at once and keeps the second value for the next trip (the same points, the same
-  // bits, two sequential evaluations fewer)
-  bool have_next = false;
-  double next_air = 0.0, next_ice = 0.0;
-  auto guard = [&](double x, double f) {
+  // steps on the last points (x1, f1), (x2, f2) and, from the second search point on, inverse
+  // quadratic interpolation through (x0, f0) as well (the secant step plus a curvature term).
+  // PH_G1/G2: guards at x2 -/+ dlt, where x2 is the search's last point (it stays put after the
+  // search) and dlt lives in x1 (dead once the search ends).
+  double x0, f0, x1, f1, x2, f2;
+  int phase, status, iter, est, n_eval, n_inside;
+  bool root_zero;  // the failed probe reports root 0 (.cc:1500-1509)
+  bool okL, okR, exact;
+#if AIRICE_SCALAR_STAMP
+  int t_lean;
+#endif
+
+  __device__ __forceinline__ double& dlt() { return x1; }
+
+  // Air2IceRayTracing's set-up (.cc:1487-1509): the query's endpoints, the bracket [thR - 16, thR]
+  // and the 0.05-degree probe.  An uninitialised solver state (non-finite bracket end) is modelled
+  // as zeros.
+  __device__ __forceinline__ void begin(const DevMedium& M, const IceConsts& I, const Geometry& g,
+                                        double thR, bool exact_) {
+    status = 0;
+    exact = exact_;
+#if AIRICE_SCALAR_STAMP
+    t_lean = 0;
+#endif
+    q.depth_pos = g.depth_pos;
+    q.dist = g.D;
+    q.top = top_layer(M, g.H);
+    q.bot = bottom_layer(M, g.ice);
+    q.tx = air_slim(M, g.H, q.n_tx);
+    double n_ice;
+    q.iceair = air_slim(M, g.ice, n_ice);
+    // Rx end of the top layer: the ice, or the layer's lower boundary (stop endpoint)
+    const bool to_ice = q.top == q.bot;
+    q.rtop = pick(to_ice, q.iceair, stop_slim(M, q.top));
+    q.n_rtop = to_ice ? n_ice : stop_n(M, q.top);
+    const double x_rtop = to_ice ? g.ice : sel5(M.atm, q.top);
+    if (x_rtop == g.H) {  // zero-length top segment (see segment())
+      q.rtop = q.tx;
+      q.n_rtop = q.n_tx;
+    }
+    q.ratio = q.n_tx / q.n_rtop;
+    {
+      const double e = exp(M.negC_ice * g.depth_pos);
+      const double y = M.A_ice + M.B_ice * e;
+      // 1/C of the ice from the host-folded surface endpoint (the same IEEE quotient): a kernel
+      // argument, so it occupies no VGPRs across the loop
+      q.rx = Slim{y * y, M.A_ice * y, M.negC_ice * g.depth_pos, I.ice0.invC};
+    }
+    lo = thR - 16;
+    hi = thR;
+    phase = PH_FLO;
+    bool probe_bad = false;  // the probe ended with lo > hi: the reference then reports root 0
+    if (M.const_air) lo = 90;  // pythonwrapper constant air index: [90, thR], no probe (.cc:978-980)
+    if (!M.const_air && lo < 90.001) {
+      lo = 90.001;
+      phase = PH_PROBE;
+      // While n(Tx) sin(180-lo) exceeds 1 by a margin (1e-6) the ray parameter L > A_air = 1,
+      // so sqrt(A^2-L^2) and THD are NaN whatever the rounding: those probe steps need no
+      // evaluation (.cc:1496-1509 would reject each of them).
+      if (q.top >= q.bot) {
+        const double thr = 180 - asin((1 + 1e-6) / q.n_tx) * M.r2d;  // NaN if n(Tx) < 1+1e-6
+        // while (lo < thr && !(lo > hi - 0.1)) lo = lo + 0.05, in closed form (airice_lean.hpp)
+        bool stepped;
+        lo = probe_steps(lo, 0.05, hi - 0.1, thr, true, stepped);
+        if (stepped) status |= AIRICE_SOLVE_PROBED;
+      } else {
+        // no air layer (Tx above the atmosphere, e.g. the table lookup's x100 fallback): THD in
+        // air is 0 at every angle, so the probe only stops at lo > hi - 0.1 -- up to ~900 steps
+        // whose outcome needs no evaluation, taken in closed form (airice_lean.hpp)
+        bool stepped;
+        lo = probe_steps(lo, 0.05, hi - 0.1, 0.0, false, stepped);
+        if (stepped) status |= AIRICE_SOLVE_PROBED;
+        if (hi < 90.001 && hi > 90.00) hi = 90.05;
+        phase = PH_FLO;
+        if (lo > hi) {
+          status |= AIRICE_SOLVE_BAD_BRACKET;
+          probe_bad = true;
+          phase = PH_DONE;
+        }
+      }
+    } else {
+      if (hi < 90.001 && hi > 90.00) hi = 90.05;
+      if (lo > hi) {  // gsl_root_fsolver_set: EINVAL, nothing initialised
+        status |= AIRICE_SOLVE_BAD_BRACKET;
+        phase = PH_DONE;
+      }
+    }
+    // GSL's reported root is 0.5 (lo + hi) of the final bracket on every path (each iterate sets
+    // it so, and the exact-zero exits make lo == hi), except the failed probe, which reports 0:
+    // the root is formed once at the end instead of being carried through the loop
+    root_zero = probe_bad;
+    f_lower = 0.0;
+    f_upper = 0.0;
+    iter = 0;
+    tau = 1e-6 + 1e-10 * fabs(g.D);
+    okL = false;
+    okR = false;
+    gL = fL = gR = fR = 0.0;
+    x0 = f0 = x1 = f1 = x2 = f2 = 0.0;
+    est = 0;
+    n_eval = 0;
+    n_inside = 0;
+  }
+
+  __device__ __forceinline__ void guard(double x, double f) {
     if (!(fabs(f) >= tau) || !(x > gL && x < gR)) return;
     if ((f < 0.0) == (fL < 0.0)) {
       gL = x;
@@ -1079,9 +1093,11 @@ __device__ __forceinline__ SolveResult solve_root(const DevMedium& M, const IceC
       gR = x;
       fR = f;
     }
-  };
+  }
+
   // gsl_root_test_interval(lo, hi, 0, 1e-9) and the driver's max_iter (.cc:355-371)
-  auto finish = [&](bool frozen) {
+  __device__ __forceinline__ void finish(bool frozen) {
+    const double tol = 0.000000001;
     bool cont;
     if (lo > hi) {
       cont = false;
@@ -1094,10 +1110,11 @@ __device__ __forceinline__ SolveResult solve_root(const DevMedium& M, const IceC
     }
     if (cont && iter == 40) status |= AIRICE_SOLVE_MAXITER;
     if (frozen || !cont || iter == 40) phase = PH_DONE;
-  };
+  }
+
   // gsl_root_fsolver_set's second end, f(hi) (fL holds f(lo)): the bracket state, the guards and
   // the secant search's first guess
-  auto on_fhi = [&](double f) {
+  __device__ __forceinline__ void on_fhi(const DevMedium& M, double f) {
     phase = PH_BISECT;
     if (!isfinite(f)) {
       status |= AIRICE_SOLVE_NONFINITE_END;
@@ -1127,42 +1144,32 @@ __device__ __forceinline__ SolveResult solve_root(const DevMedium& M, const IceC
         }
       }
     }
-  };
-  if constexpr (!WAVE) {
-    // f(lo) and f(hi) in one pass (eval_thd2: two independent chains per lane, ~1.3x the time of
-    // one evaluation instead of 2x) before the loop, so that the loop carries no extra state; the
-    // probing lanes reach PH_FLO inside the loop and evaluate the ends there
-    if (phase == PH_FLO) {
-      double air_a, ice_a, air_b, ice_b;
-      eval_thd2(M, I, q, lo, hi, tab, air_a, ice_a, air_b, ice_b);
-      const double fa = (q.dist - (ice_a + air_a));
+  }
+
+  // f(lo) and f(hi) in one pass (eval_thd2: two independent chains per lane, ~1.3x the time of one
+  // evaluation instead of 2x); a lane that is probing reaches PH_FLO in the loop and evaluates the
+  // ends there
+  __device__ __forceinline__ void ends_paired(const DevMedium& M, const IceConsts& I,
+                                              const double* tab) {
+    if (phase != PH_FLO) return;
+    double air_a, ice_a, air_b, ice_b;
+    eval_thd2(M, I, q, lo, hi, tab, air_a, ice_a, air_b, ice_b);
+    const double fa = (q.dist - (ice_a + air_a));
+    ++n_eval;
+    if (!isfinite(fa)) {
+      status |= AIRICE_SOLVE_NONFINITE_END;
+      phase = PH_BISECT;
+    } else {
+      fL = fa;
       ++n_eval;
-      if (!isfinite(fa)) {
-        status |= AIRICE_SOLVE_NONFINITE_END;
-        phase = PH_BISECT;
-      } else {
-        fL = fa;
-        ++n_eval;
-        on_fhi(q.dist - (ice_b + air_b));
-      }
+      on_fhi(M, q.dist - (ice_b + air_b));
     }
   }
-#if AIRICE_SCALAR_STAMP
-  const int t_setup = (int)(__builtin_amdgcn_s_memtime() - ts0) + (int)(0.0 * (lo + hi));
-#endif
-#if AIRICE_SCALAR_STAMP
-  int t_pre = 0, t_post = 0;
-  unsigned long long tq = __builtin_amdgcn_s_memtime();
-#endif
-  while (phase != PH_DONE) {
-    DBG_EXEC(0);
-    if constexpr (WAVE) {
-      // one query per wave: the phase and the counters are the same on every lane; scalar copies
-      // let the phase dispatch branch on SCC instead of exec masks
-      phase = __builtin_amdgcn_readfirstlane(phase);
-      est = __builtin_amdgcn_readfirstlane(est);
-      iter = __builtin_amdgcn_readfirstlane(iter);
-    }
+
+  // The evaluation-free bisection steps and the next point to evaluate.  False: the query is done
+  // (phase PH_DONE) without another evaluation.
+  __device__ __forceinline__ bool next_point(const DevMedium& M, double& x) {
+    const double tol = 0.000000001;
     if (phase == PH_BISECT) {
       DBG_EXEC(1);
       // steps that need no evaluation: an exact zero at a bracket end (GSL returns that end),
@@ -1174,7 +1181,8 @@ __device__ __forceinline__ SolveResult solve_root(const DevMedium& M, const IceC
         lo = r0;
         hi = r0;
         finish(false);
-        break;  // lo == hi: gsl_root_test_interval converges
+        phase = PH_DONE;  // lo == hi: gsl_root_test_interval converges
+        return false;
       }
       if ((okL || okR) && lo > 0.0) {
 #if AIRICE_SCALAR_STAMP
@@ -1223,10 +1231,12 @@ __device__ __forceinline__ SolveResult solve_root(const DevMedium& M, const IceC
 #if AIRICE_SCALAR_STAMP
         t_lean += (int)(__builtin_amdgcn_s_memtime() - tl0) + (int)(0.0 * (lo + hi));
 #endif
-        if (done) break;
+        if (done) {
+          phase = PH_DONE;
+          return false;
+        }
       }
     }
-    double x;
     if (phase == PH_FHI) {
       x = hi;
     } else if (phase == PH_BISECT) {
@@ -1246,50 +1256,22 @@ __device__ __forceinline__ SolveResult solve_root(const DevMedium& M, const IceC
       }
       if (!(x > gL && x < gR)) x = 0.5 * (gL + gR);  // safeguard: the guards' midpoint
     } else if (phase == PH_G1) {
-      x = x2 - dlt;
+      x = x2 - dlt();
     } else if (phase == PH_G2) {
-      x = x2 + dlt;
+      x = x2 + dlt();
     } else {
       x = lo;
     }
-    // the single evaluation site: MinimizeforLaunchAngle (.cc:873-917)
-    DBG_EXEC(4);
+    return true;
+  }
+
+  // f = D - THD at x, the point next_point() returned.  REUSE_PROBE: a probing lane's last probe
+  // evaluation (at x = lo, the point gsl_root_fsolver_set evaluates next) is taken as f(lo).
+  template <bool REUSE_PROBE>
+  __device__ __forceinline__ void update(const DevMedium& M, double x, double thd_air,
+                                         double thd_ice) {
     ++n_eval;
     n_inside += (phase == PH_BISECT);
-    double thd_air, thd_ice;
-    if constexpr (WAVE) {
-      if (have_next) {
-        thd_air = next_air;
-        thd_ice = next_ice;
-        have_next = false;
-      } else {
-        // the point the next trip evaluates when this one is f(lo) (then f(hi)) or the first guard
-        // (then always the second: PH_G1 -> PH_G2)
-        const bool pair = phase == PH_FLO || phase == PH_G1;
-        const double xb = phase == PH_FLO ? hi : x2 + dlt;
-#if AIRICE_SCALAR_STAMP
-        const unsigned long long e0 = __builtin_amdgcn_s_memtime();
-        t_pre += (int)(e0 - tq) + (int)(0.0 * x);
-#endif
-        eval_thd_wave(M, I, q, x, pair ? xb : x, tab, thd_air, thd_ice, next_air, next_ice);
-#if AIRICE_SCALAR_STAMP
-        // debug: evaluation ticks in n_inside (the wave form does not count midpoints)
-        tq = __builtin_amdgcn_s_memtime();
-        n_inside += (int)(tq - e0) + (int)(0.0 * (thd_air + thd_ice));
-#endif
-        have_next = pair;
-      }
-    } else {
-      {
-        double L;
-        thd_air = air_thd(M, q, x, L, tab);
-        thd_ice = 0;
-        if (q.depth_pos != 0) {
-          const RayL RL = ray_L(M.A_ice * M.A_ice, L);
-          thd_ice += delta_D(slim(I.ice0), q.rx, RL, tab);
-        }
-      }
-    }
     const double f = (q.dist - (thd_ice + thd_air));
     if (phase == PH_PROBE) {
       DBG_EXEC(5);
@@ -1300,7 +1282,7 @@ __device__ __forceinline__ SolveResult solve_root(const DevMedium& M, const IceC
           status |= AIRICE_SOLVE_BAD_BRACKET;
           root_zero = true;
           phase = PH_DONE;
-        } else if constexpr (!WAVE) {
+        } else if (REUSE_PROBE) {
           // this trip evaluated f at x = lo, the point gsl_root_fsolver_set evaluates next
           // (f(lo)): the same point and arithmetic, so its value is PH_FLO's result and the lane
           // goes on to f(hi) one trip earlier
@@ -1321,14 +1303,13 @@ __device__ __forceinline__ SolveResult solve_root(const DevMedium& M, const IceC
       if (!isfinite(f)) {
         status |= AIRICE_SOLVE_NONFINITE_END;
         phase = PH_BISECT;
-        have_next = false;  // f(hi) is not wanted after all
       } else {
         fL = f;
         phase = PH_FHI;
       }
     } else if (phase == PH_FHI) {
       DBG_EXEC(7);
-      on_fhi(f);
+      on_fhi(M, f);
     } else if (phase == PH_EST) {
       DBG_EXEC(8);
       if (est > 0) {
@@ -1345,21 +1326,24 @@ __device__ __forceinline__ SolveResult solve_root(const DevMedium& M, const IceC
       } else if (fabs(f) < tau) {
         // at the root: guards a few tau either side, scaled by the local secant slope
         const double sl = (x2 - x1) * __builtin_amdgcn_rcp(f2 - f1);  // dtheta / df
-        dlt = 4.0 * tau * fabs(sl);
-        const bool room = dlt > 0.0 && dlt < (gR - gL);
-        if (room && est >= 2) {
-          // x1 is a search point near the root, so the secant slope is the local one: f at
-          // x2 -+ dlt is f2 -+ 4 tau sign(sl) to first order, |.| >= 3 tau with the root
-          // between, and the guards take those signs without evaluating f there (DESIGN.md §4:
-          // a slope off by more than 4x would move the root by less than |f2| / f', far inside
-          // the bisection's last interval)
+        const double a = (x2 - x1) * (f1 - f0), b = (x1 - x0) * (f2 - f1);  // (before dlt takes x1)
+        dlt() = 4.0 * tau * fabs(sl);
+        const bool room = dlt() > 0.0 && dlt() < (gR - gL);
+        // x1 is a search point near the root (est >= 2), so the secant slope through it is the
+        // local one, and f at x2 -+ dlt is f2 -+ 4 tau sign(sl) to first order: |.| >= 3 tau with
+        // the root between.  The guards then take those signs without evaluating f there -- when
+        // the slope is consistent: the previous secant slope (x0, x1) has the same sign and is
+        // within 2x of it (sl (f2 - f1) = x2 - x1 and its twin, compared as products: no
+        // quotient, and any NaN fails), so f's curvature cannot have moved the root out of
+        // [x2 - dlt, x2 + dlt].  Otherwise, and for the first search point (x1 is the bracket
+        // end), both guards are evaluated (a side whose guard already lies at the root needs none).
+        const bool consistent = a * b > 0.0 && fabs(a) <= 2.0 * fabs(b) && fabs(b) <= 2.0 * fabs(a);
+        if (room && est >= 2 && (AIRICE_NO_CHECK || consistent)) {
           const double fm = sl > 0.0 ? -tau : tau;  // f(x2 - dlt)
-          guard(x2 - dlt, fm);
-          guard(x2 + dlt, -fm);
+          guard(x2 - dlt(), fm);
+          guard(x2 + dlt(), -fm);
           phase = PH_BISECT;
         } else {
-          // the first search point (x1 is the bracket end): evaluate both guards; a side whose
-          // guard already lies at the root needs none
           const bool needL = !(x2 - gL <= 0.0), needR = !(gR - x2 <= 0.0);
           phase = room ? (needL ? PH_G1 : (needR ? PH_G2 : PH_BISECT)) : PH_BISECT;
         }
@@ -1393,23 +1377,110 @@ __device__ __forceinline__ SolveResult solve_root(const DevMedium& M, const IceC
       }
       finish(frozen);
     }
+  }
+
+  __device__ __forceinline__ double root() const { return root_zero ? 0.0 : 0.5 * (lo + hi); }
+};
+
+// MinimizeforLaunchAngle's f terms at theta (.cc:873-917): THD in air and in the ice.
+__device__ __forceinline__ void eval_thd(const DevMedium& M, const IceConsts& I, const Query& q,
+                                         double theta, const double* tab, double& thd_air,
+                                         double& thd_ice) {
+  double L;
+  thd_air = air_thd(M, q, theta, L, tab);
+  thd_ice = 0;
+  if (q.depth_pos != 0) {
+    const RayL RL = ray_L(M.A_ice * M.A_ice, L);
+    thd_ice += delta_D(slim(I.ice0), q.rx, RL, tab);
+  }
+}
+
+// Root finding of Air2IceRayTracing (.cc:1487-1521): the probe loop, gsl_root_fsolver_set and the
+// FindFunctionRoot driver (.cc:340-374) with gsl_root_fsolver_bisection +
+// gsl_root_test_interval(lo, hi, 0, 1e-9) semantics, as one per-lane state machine with a single
+// evaluation site: lanes that are probing, setting up the bracket or bisecting share each
+// evaluation instead of waiting for each other (the probe runs in ~7% of queries).
+// WAVE: one query per wave (scalar_solve_kernel), each evaluation spread over the lanes.
+template <bool WAVE = false>
+__device__ __forceinline__ SolveResult solve_root(const DevMedium& M, const IceConsts& I,
+                                                  const Geometry& g, double thR, bool exact,
+                                                  const double* tab) {
+#if AIRICE_SCALAR_STAMP
+  const unsigned long long ts0 = __builtin_amdgcn_s_memtime();
+#endif
+  RootSearch s;
+  s.begin(M, I, g, thR, exact);
+  if constexpr (!WAVE) s.ends_paired(M, I, tab);
+#if AIRICE_SCALAR_STAMP
+  const int t_setup = (int)(__builtin_amdgcn_s_memtime() - ts0) + (int)(0.0 * (s.lo + s.hi));
+  int t_pre = 0, t_post = 0;
+  unsigned long long tq = __builtin_amdgcn_s_memtime();
+#endif
+  // WAVE: f(lo) and f(hi), and the two guards, are independent pairs of points; the wave evaluates
+  // each pair at once and keeps the second value for the next trip (the same points, the same
+  // bits, two sequential evaluations fewer)
+  bool have_next = false;
+  double next_air = 0.0, next_ice = 0.0;
+  while (s.phase != PH_DONE) {
+    DBG_EXEC(0);
+    if constexpr (WAVE) {
+      // one query per wave: the phase and the counters are the same on every lane; scalar copies
+      // let the phase dispatch branch on SCC instead of exec masks
+      s.phase = __builtin_amdgcn_readfirstlane(s.phase);
+      s.est = __builtin_amdgcn_readfirstlane(s.est);
+      s.iter = __builtin_amdgcn_readfirstlane(s.iter);
+    }
+    double x;
+    if (!s.next_point(M, x)) break;
+    // the single evaluation site: MinimizeforLaunchAngle (.cc:873-917)
+    DBG_EXEC(4);
+    double thd_air, thd_ice;
+    const int ph = s.phase;
+    if constexpr (WAVE) {
+      if (have_next) {
+        thd_air = next_air;
+        thd_ice = next_ice;
+        have_next = false;
+      } else {
+        // the point the next trip evaluates when this one is f(lo) (then f(hi)) or the first guard
+        // (then always the second: PH_G1 -> PH_G2)
+        const bool pair = ph == PH_FLO || ph == PH_G1;
+        const double xb = ph == PH_FLO ? s.hi : s.x2 + s.dlt();
+#if AIRICE_SCALAR_STAMP
+        const unsigned long long e0 = __builtin_amdgcn_s_memtime();
+        t_pre += (int)(e0 - tq) + (int)(0.0 * x);
+#endif
+        eval_thd_wave(M, I, s.q, x, pair ? xb : x, tab, thd_air, thd_ice, next_air, next_ice);
+#if AIRICE_SCALAR_STAMP
+        // debug: evaluation ticks in n_inside (the wave form does not count midpoints)
+        tq = __builtin_amdgcn_s_memtime();
+        s.n_inside += (int)(tq - e0) + (int)(0.0 * (thd_air + thd_ice));
+#endif
+        have_next = pair;
+      }
+    } else {
+      eval_thd(M, I, s.q, x, tab, thd_air, thd_ice);
+    }
+    s.template update<!WAVE>(M, x, thd_air, thd_ice);
+    // f(hi) is not wanted after all when f(lo) was not finite
+    if (WAVE && ph == PH_FLO && s.phase != PH_FHI) have_next = false;
 #if AIRICE_SCALAR_STAMP
     if constexpr (WAVE) {
       const unsigned long long te = __builtin_amdgcn_s_memtime();
-      t_post += (int)(te - tq) + (int)(0.0 * (lo + hi + x2));
+      t_post += (int)(te - tq) + (int)(0.0 * (s.lo + s.hi + s.x2));
       tq = te;
     }
 #endif
   }
 #if AIRICE_SCALAR_STAMP
-  SolveResult sr{root_zero ? 0.0 : 0.5 * (lo + hi), status, n_eval, est, n_inside};
+  SolveResult sr{s.root(), s.status, s.n_eval, s.est, s.n_inside};
   sr.t_setup = t_setup;
-  sr.t_lean = t_lean;
+  sr.t_lean = s.t_lean;
   sr.t_pre = t_pre;
   sr.t_post = t_post;
   return sr;
 #else
-  return SolveResult{root_zero ? 0.0 : 0.5 * (lo + hi), status, n_eval, est, n_inside};
+  return SolveResult{s.root(), s.status, s.n_eval, s.est, s.n_inside};
 #endif
 }
 
@@ -1700,9 +1771,13 @@ __device__ __forceinline__ int query_bucket(const DevMedium& M, const QueryArgs&
   return b * kGroupHeights + (span < 0 ? 0 : (span > 3 ? 3 : span));
 }
 
+// (the table lookup's fallback solves only its flagged lanes: lookup_fallback_kernel, not this)
+constexpr bool solves_every_lane(int in) { return in != IN_CM100; }
+
 template <int IN>
 __global__ __launch_bounds__(kRootsBlock, kRootsWaves) void roots_kernel(DevMedium M, IceConsts I,
                                                                          QueryArgs Q, Park park) {
+  static_assert(solves_every_lane(IN), "IN_CM100 lanes are masked: use lookup_fallback_kernel");
   __shared__ int s_count[kSortBuckets + 1];
   __shared__ int s_slot[kRootsBlock];
   const long long k0 = (long long)blockIdx.x * kRootsBlock;
@@ -1875,6 +1950,7 @@ __global__ __launch_bounds__(kSortedBlock, kRootsWaves) void roots_sorted_kernel
   }
   __syncthreads();
   const long long ks = (long long)blockIdx.x * kSortedBlock + threadIdx.x;
+  static_assert(solves_every_lane(IN), "IN_CM100 lanes are masked: use lookup_fallback_kernel");
   if (ks >= *grouped) return;  // past the queries with a bucket
   DBG_EXEC(12);
   double thR;
@@ -2244,12 +2320,11 @@ size_t group_min_batch(int in) {
 template <int IN>
 static int launch_roots(const DevMedium& M, const IceConsts& I, const QueryArgs& Q,
                         const Park& park, size_t n, hipStream_t st, SortedPark& sp, void*& ws) {
+  static_assert(solves_every_lane(IN), "IN_CM100 lanes are masked: use launch_lookup_fallback");
   sp = SortedPark{nullptr, nullptr};
   ws = nullptr;
   const size_t group_min = group_min_batch(IN);
-  // (the table lookup's fallback pass stays block-local: its batch is the whole lookup batch,
-  // of which typically well under 1 % of lanes are fallback lanes)
-  if (IN == IN_CM100 || group_min == 0 || n < group_min ||
+  if (group_min == 0 || n < group_min ||
       (park.stats != nullptr && !AIRICE_SORTED_STATS) || n >= (1ull << 31)) {
     ktimer_begin(KT_ROOTS, st);
     hipLaunchKernelGGL((roots_kernel<IN>), roots_grid(n), dim3(kRootsBlock), 0, st, M, I, Q, park);

@@ -50,6 +50,10 @@ __global__ __launch_bounds__(kLkBlock) void lookup_kernel(LkTable T, const doubl
   const long long k = (long long)blockIdx.x * kLkBlock + threadIdx.x;
   if (k >= n) return;
   (void)ice_cm;  // the table path never reads the ice height (.cc:1309 converts it, unused)
+  // a table whose rows have different launch angles (the pack cleared the word) reads column 4
+  if (T.ang != nullptr && *reinterpret_cast<const int*>(T.ang + (lk_angles_ok_offset(T.n, T.asteps) -
+                                                                  lk_angles_offset(T.n, T.asteps))) == 0)
+    T.ang = nullptr;
   int fl = 0;
   double o[9];
   bool good = false;
@@ -61,26 +65,30 @@ __global__ __launch_bounds__(kLkBlock) void lookup_kernel(LkTable T, const doubl
   flags[k] = (uint8_t)fl;
 }
 
-// airice_lookup_pack: one lane per record (entries i and i + 1, columns 1-10 each); the column
-// reads are coalesced across the wave and each wave writes one contiguous 8 KB run of records.
-__global__ __launch_bounds__(kLkBlock) void lookup_pack_kernel(const float* __restrict__ t,
-                                                               long long ld, long long n,
-                                                               float* __restrict__ e) {
+// airice_lookup_pack, first the angle vector: column 4 of the table's first row, and its
+// verification word set to 1 (lookup_pack_kernel clears it when another row differs).
+__global__ __launch_bounds__(kLkBlock) void lookup_angles_kernel(LkTable T, float* __restrict__ e) {
+  const long long j = (long long)blockIdx.x * kLkBlock + threadIdx.x;
+  float* ang = e + lk_angles_offset(T.n, T.asteps);
+  if (j < T.asteps) ang[j] = j < T.n ? T.col[4][j] : __builtin_nanf("");
+  if (j == 0) *reinterpret_cast<int*>(e + lk_angles_ok_offset(T.n, T.asteps)) = 1;
+}
+
+// Then one lane per pair record (lk_pair_fold: entries i and i + 1); the column reads are coalesced
+// across the wave and each wave writes one contiguous 4 KB run of records.  Each lane also checks
+// its entry's launch angle against the first row's (bit for bit): the table's column 4 is the
+// angle grid in every row (.cc:2084-2105), and a table where it is not keeps the column path.
+__global__ __launch_bounds__(kLkBlock) void lookup_pack_kernel(LkTable T, float* __restrict__ e) {
   const long long i = (long long)blockIdx.x * kLkBlock + threadIdx.x;
-  if (i >= n) return;
-  const bool last = i + 1 >= n;
+  if (i >= T.n) return;
   float c[AIRICE_LOOKUP_ENTRY_FLOATS];
-#pragma unroll
-  for (int k = 0; k < 10; ++k) {
-    c[k] = t[(long long)(1 + k) * ld + i];
-    c[10 + k] = last ? __builtin_nanf("") : t[(long long)(1 + k) * ld + i + 1];
-  }
-#pragma unroll
-  for (int k = 20; k < AIRICE_LOOKUP_ENTRY_FLOATS; ++k) c[k] = 0.0f;
+  lk_pair_fold(T.col, T.n, i, c);
   float4* p = reinterpret_cast<float4*>(e + (long long)AIRICE_LOOKUP_ENTRY_FLOATS * i);
 #pragma unroll
   for (int q = 0; q < AIRICE_LOOKUP_ENTRY_FLOATS / 4; ++q)
     p[q] = make_float4(c[4 * q], c[4 * q + 1], c[4 * q + 2], c[4 * q + 3]);
+  if (lk_bits_i(T.col[4][i]) != lk_bits_i(T.col[4][i % T.asteps]))
+    atomicAnd(reinterpret_cast<int*>(e + lk_angles_ok_offset(T.n, T.asteps)), 0);
 }
 
 // Row records after the entry records: one lane per full table row (lk_row_fold).
@@ -89,8 +97,7 @@ __global__ __launch_bounds__(kLkBlock) void lookup_rows_kernel(LkTable T, float*
   if (r >= T.rows) return;
   float rec[AIRICE_LOOKUP_ROW_FLOATS];
   lk_row_fold(T, r, rec);
-  float4* p = reinterpret_cast<float4*>(e + T.n * AIRICE_LOOKUP_ENTRY_FLOATS +
-                                        r * AIRICE_LOOKUP_ROW_FLOATS);
+  float4* p = reinterpret_cast<float4*>(e + lk_rows_offset(T.n) + r * AIRICE_LOOKUP_ROW_FLOATS);
 #pragma unroll
   for (int q = 0; q < AIRICE_LOOKUP_ROW_FLOATS / 4; ++q)
     p[q] = make_float4(rec[4 * q], rec[4 * q + 1], rec[4 * q + 2], rec[4 * q + 3]);
@@ -106,6 +113,8 @@ LkTable lk_table(const airice_lookup_table* t) {
   T.hsteps = t->total_height_steps;
   T.asteps = t->total_angle_steps;
   T.rows = T.e != nullptr ? T.n / T.asteps : 0;
+  // the angle vector; lookup_kernel drops it when the pack found a row with other angles
+  T.ang = T.e != nullptr ? T.e + lk_angles_offset(T.n, T.asteps) : nullptr;
   return T;
 }
 
@@ -114,11 +123,13 @@ LkTable lk_table(const airice_lookup_table* t) {
 int launch_lookup_pack(const airice_lookup_table* t, float* e, hipStream_t st) {
   const long long n = (long long)t->n_entries;
   if (n == 0) return AIRICE_OK;
-  hipLaunchKernelGGL(lookup_pack_kernel, dim3((unsigned)((n + kLkBlock - 1) / kLkBlock)),
-                     dim3(kLkBlock), 0, st, t->table, (long long)t->ld, n, e);
   LkTable T = lk_table(t);
   T.e = e;
   T.rows = n / T.asteps;
+  hipLaunchKernelGGL(lookup_angles_kernel, dim3((unsigned)((T.asteps + kLkBlock - 1) / kLkBlock)),
+                     dim3(kLkBlock), 0, st, T, e);
+  hipLaunchKernelGGL(lookup_pack_kernel, dim3((unsigned)((n + kLkBlock - 1) / kLkBlock)),
+                     dim3(kLkBlock), 0, st, T, e);
   if (T.rows > 0)
     hipLaunchKernelGGL(lookup_rows_kernel, dim3((unsigned)((T.rows + kLkBlock - 1) / kLkBlock)),
                        dim3(kLkBlock), 0, st, T, e);

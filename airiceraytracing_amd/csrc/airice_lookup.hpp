@@ -17,12 +17,27 @@ namespace airice {
 
 struct LkTable {
   const float* col[AIRICE_TABLE_COLUMNS];  // column c of entry i at col[c][i]
-  const float* e;                          // packed entries (airice_lookup_pack) or nullptr
+  const float* e;                          // packed copy (airice_lookup_pack) or nullptr
   long long n;
   double stop_h, step_h;  // LoopStopHeight, HeightStepSize of the last table made
   int hsteps, asteps;     // TotalHeightSteps, TotalAngleSteps
-  long long rows;         // row records after the entry records in e (n / asteps), 0: none
+  long long rows;         // row records in e (n / asteps), 0: none
+  // the packed copy's launch angle of each grid column (column 4 of every table row, which the
+  // pack verified), or nullptr: the lookup reads column 4
+  const float* ang = nullptr;
 };
+
+// Offsets into the packed copy (floats): the pair records, then the row records (128-byte
+// aligned), then the angle vector and its verification word (airice.h, AIRICE_LOOKUP_PACK_FLOATS).
+__host__ __device__ __forceinline__ long long lk_rows_offset(long long n) {
+  return (n * AIRICE_LOOKUP_ENTRY_FLOATS + 31) / 32 * 32;
+}
+__host__ __device__ __forceinline__ long long lk_angles_offset(long long n, long long asteps) {
+  return lk_rows_offset(n) + n / asteps * AIRICE_LOOKUP_ROW_FLOATS;
+}
+__host__ __device__ __forceinline__ long long lk_angles_ok_offset(long long n, long long asteps) {
+  return lk_angles_offset(n, asteps) + (asteps + 3) / 4 * 4;
+}
 struct LkTxhBins {
   long long s1, e1, s2, e2;
   double c1, c2;
@@ -50,21 +65,48 @@ __host__ __device__ __forceinline__ LkRec lk_rec(const LkTable& T, long long i, 
   return r;
 }
 
-// Entries i and i + 1 (an interpolation pair) from one 128-byte packed record -- five 16-byte
-// loads of one L2 line -- when there is a packed copy and both entries exist; false otherwise.
-__host__ __device__ __forceinline__ bool lk_pair(const LkTable& T, long long i, LkRec& r0,
+// Entries i and i + 1 (an interpolation pair) when there is a packed copy and both entries exist
+// (false otherwise): columns 2, 3, 5-10 of both from one 64-byte pair record (four 16-byte loads,
+// one fabric request), THD (column 1) as the search read it (thd0, thd1: the caller's values of
+// entries i, i + 1), the launch angle (column 4) from the angle vector when the pair lies inside
+// the row starting at entry abase (else from column 4).
+__host__ __device__ __forceinline__ bool lk_pair(const LkTable& T, long long i, float thd0,
+                                                 float thd1, long long abase, LkRec& r0,
                                                  LkRec& r1) {
   if (T.e == nullptr || i < 0 || i + 1 >= T.n) return false;
   const float4* p = reinterpret_cast<const float4*>(T.e + (long long)AIRICE_LOOKUP_ENTRY_FLOATS * i);
-  const float4 a = p[0], b = p[1], c = p[2], d = p[3], e = p[4];
-  const float v[20] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w, c.x, c.y,
-                       c.z, c.w, d.x, d.y, d.z, d.w, e.x, e.y, e.z, e.w};
+  const float4 a = p[0], b = p[1], c = p[2], d = p[3];
+  const float v[16] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w,
+                       c.x, c.y, c.z, c.w, d.x, d.y, d.z, d.w};
+  // record slot k holds parameter par[k] (column 1 + par[k]); lk_pair_fold writes them
+  constexpr int par[8] = {1, 2, 4, 5, 6, 7, 8, 9};
 #pragma unroll
-  for (int k = 0; k < 10; ++k) {
-    r0.c[k] = v[k];
-    r1.c[k] = v[10 + k];
+  for (int k = 0; k < 8; ++k) {
+    r0.c[par[k]] = v[k];
+    r1.c[par[k]] = v[8 + k];
+  }
+  r0.c[0] = thd0;
+  r1.c[0] = thd1;
+  const long long j = i - abase;
+  if (T.ang != nullptr && abase >= 0 && j >= 0 && j + 1 < T.asteps) {
+    r0.c[3] = T.ang[j];
+    r1.c[3] = T.ang[j + 1];
+  } else {
+    r0.c[3] = T.col[4][i];
+    r1.c[3] = T.col[4][i + 1];
   }
   return true;
+}
+
+// Pair record i (pack time): columns 2, 3, 5-10 of entries i and i + 1 (NaN past the last entry).
+__host__ __device__ __forceinline__ void lk_pair_fold(const float* const* col, long long n,
+                                                      long long i, float* rec) {
+  constexpr int cols[8] = {2, 3, 5, 6, 7, 8, 9, 10};
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    rec[k] = col[cols[k]][i];
+    rec[8 + k] = i + 1 < n ? col[cols[k]][i + 1] : __builtin_nanf("");
+  }
 }
 
 __host__ __device__ __forceinline__ double lk_at(const LkTable& T, int c, long long i, int& fl) {
@@ -247,7 +289,7 @@ __host__ __device__ __forceinline__ void lk_row_fold(const LkTable& T, long long
   rec[23] = lk_bits_f(trees);
 }
 __host__ __device__ __forceinline__ const float4* lk_row_rec(const LkTable& T, long long index) {
-  return reinterpret_cast<const float4*>(T.e + T.n * AIRICE_LOOKUP_ENTRY_FLOATS +
+  return reinterpret_cast<const float4*>(T.e + lk_rows_offset(T.n) +
                                          index * AIRICE_LOOKUP_ROW_FLOATS);
 }
 __host__ __device__ __forceinline__ void lk_tree_unpack(const float4* p, LkTree& T_) {
@@ -286,14 +328,15 @@ __host__ __device__ __forceinline__ bool lk_row(const LkTable& T, long long inde
   return true;
 }
 
-// FindClosestTHD (.cc:1128-1169).  With a packed table the THD values at the final pair come
-// from the pair's record, which also carries the parameters lk_row_params interpolates (have_pair).
+// FindClosestTHD (.cc:1128-1169).  With a packed table the final pair's record carries the
+// parameters lk_row_params interpolates (have_pair).  abase: first entry of the searched row (the
+// angle vector's origin), or -1.
 struct LkThdPair {
   LkRec r1, r2;  // entries index1, index2
   bool have_pair = false;
 };
 __host__ __device__ __forceinline__ LkThdBins lk_closest_thd(const LkTable& T, double P, long long s, long long e,
-                                            int& fl, LkThdPair& pr) {
+                                            int& fl, LkThdPair& pr, long long abase = -1) {
 #pragma unroll 1
   for (int i = 0; i < 8; ++i) {
     if (e - s >= 3) {
@@ -317,9 +360,9 @@ __host__ __device__ __forceinline__ LkThdBins lk_closest_thd(const LkTable& T, d
     }
   }
   const long long index1 = index2 - 1;
-  pr.have_pair = lk_pair(T, index1, pr.r1, pr.r2);
-  const double v2 = pr.have_pair ? (double)pr.r2.c[0] : lk_at(T, 1, index2, fl);
-  const double v1 = pr.have_pair ? (double)pr.r1.c[0] : lk_at(T, 1, index1, fl);
+  const double v2 = lk_at(T, 1, index2, fl);
+  const double v1 = lk_at(T, 1, index1, fl);
+  pr.have_pair = lk_pair(T, index1, (float)v1, (float)v2, abase, pr.r1, pr.r2);
   minimum = fabs(P - v2);
   if (minimum > fabs(P - v1)) minimum = fabs(P - v1);
   return LkThdBins{index1, index2, minimum};
@@ -363,7 +406,8 @@ __host__ __device__ __forceinline__ bool lk_step32(double v, double P, int& s, i
 __host__ __device__ __forceinline__ bool lk_closest_thd_tree(const LkTable& T, double P, long long s_in,
                                                              long long e_in, const float* t,
                                                              float4 top, float4 topb,
-                                                             LkThdBins& out, LkThdPair& pr) {
+                                                             LkThdBins& out, LkThdPair& pr,
+                                                             long long abase) {
   if (s_in < 0 || e_in < s_in || T.n < kLkWindow || T.n >= (1LL << 31)) return false;
   int s = (int)s_in, e = (int)e_in;
   bool fin = false;
@@ -440,9 +484,12 @@ __host__ __device__ __forceinline__ bool lk_closest_thd_tree(const LkTable& T, d
   }
   if (!brk) return false;
   const long long index1 = (long long)index2 - 1;
-  if (!lk_pair(T, index1, pr.r1, pr.r2)) return false;
+  // THD at the pair from the window (index2 is in [s, e]; index1 too unless index2 == base)
+  const float t2 = w[(index2 - base) * ws];
+  const float t1 = index2 > base ? w[(index2 - 1 - base) * ws] : (index1 >= 0 ? T.col[1][index1] : 0.0f);
+  if (!lk_pair(T, index1, t1, t2, abase, pr.r1, pr.r2)) return false;
   pr.have_pair = true;
-  const double v2 = (double)pr.r2.c[0], v1 = (double)pr.r1.c[0];
+  const double v2 = (double)t2, v1 = (double)t1;
   minimum = fabs(P - v2);
   if (minimum > fabs(P - v1)) minimum = fabs(P - v1);
   out = LkThdBins{index1, (long long)index2, minimum};
@@ -451,19 +498,22 @@ __host__ __device__ __forceinline__ bool lk_closest_thd_tree(const LkTable& T, d
 
 // The 10 parameters of one table row at horizontal distance D (.cc:1199-1240 / 1250-1289).
 // tree: the row record's bisection tree of (s, e) when use_tree.
+// abase: first entry of the row the span lies in (the angle vector's origin), or -1.
 __host__ __device__ __forceinline__ void lk_row_params(const LkTable& T, double D, long long s, long long e,
                                               double par[10], double* closest, int& fl,
                                               const double* max_thd_row = nullptr,
                                               const float* tree = nullptr,
                                               float4 tree_top = float4{},
-                                              float4 tree_topb = float4{}) {
+                                              float4 tree_topb = float4{},
+                                              long long abase = -1) {
   const double max_thd = max_thd_row != nullptr ? *max_thd_row : lk_at(T, 1, s, fl);
   if (D <= max_thd) {
     LkThdPair pr;
     LkThdBins b;
-    if (tree == nullptr || !lk_closest_thd_tree(T, D, s, e, tree, tree_top, tree_topb, b, pr)) {
+    if (tree == nullptr ||
+        !lk_closest_thd_tree(T, D, s, e, tree, tree_top, tree_topb, b, pr, abase)) {
       pr.have_pair = false;
-      b = lk_closest_thd(T, D, s, e, fl, pr);
+      b = lk_closest_thd(T, D, s, e, fl, pr, abase);
     }
     *closest = b.c;
     if (b.c != 0) {
@@ -491,7 +541,8 @@ __host__ __device__ __forceinline__ void lk_par_values(const LkTable& T, double 
                                        double par1[10], double* h2, double par2[10], int& fl) {
   const double min_h = lk_at(T, 0, T.n - 1, fl);
   LkRow R;  // packed row record: the span and its end values without the scans
-  const bool fast = lk_row(T, lk_txh_index(T, H), R);
+  const long long index = lk_txh_index(T, H);
+  const bool fast = lk_row(T, index, R);
   LkTxhBins b;
   if (fast) {
     b = R.b;
@@ -502,14 +553,17 @@ __host__ __device__ __forceinline__ void lk_par_values(const LkTable& T, double 
   }
   double c1 = 0;
   *h1 = fast ? R.h1 : lk_at(T, 0, b.s1, fl);
+  // the rows of the two spans: the height's own, and the one s2 moved to (.cc:1118-1121)
+  const long long abase1 = index * T.asteps;
+  const long long abase2 = b.s2 < b.s1 ? abase1 - T.asteps : abase1 + T.asteps;
   lk_row_params(T, D, b.s1, b.e1, par1, &c1, fl, fast ? &R.mt1 : nullptr,
-                fast && R.tree1 ? R.rec + 8 : nullptr, R.top1, R.top1b);
+                fast && R.tree1 ? R.rec + 8 : nullptr, R.top1, R.top1b, abase1);
   *h2 = *h1;
   if (b.c1 != 0 && H > min_h && b.s2 < T.n - 1) {
     *h2 = fast ? R.h2 : lk_at(T, 0, b.s2, fl);
     double c2 = 0;
     lk_row_params(T, D, b.s2, b.e2, par2, &c2, fl, fast ? &R.mt2 : nullptr,
-                  fast && R.tree2 ? R.rec + 32 : nullptr, R.top2, R.top2b);
+                  fast && R.tree2 ? R.rec + 32 : nullptr, R.top2, R.top2b, abase2);
   } else {
 #pragma unroll
     for (int ip = 0; ip < 10; ++ip) par2[ip] = par1[ip];

@@ -603,7 +603,13 @@ int airice_table_lookup_launch(const airice_medium* m, const airice_lookup_table
   return rc;
 }
 
-int airice_lookup_pack(const airice_lookup_table* t, float* d_entries, void* stream) {
+size_t airice_lookup_pack_floats(size_t n_entries, int32_t total_angle_steps) {
+  if (n_entries < 1 || total_angle_steps < 1) return 0;
+  return AIRICE_LOOKUP_PACK_FLOATS(n_entries, total_angle_steps);
+}
+
+int airice_lookup_pack(const airice_lookup_table* t, float* d_entries, size_t capacity_floats,
+                       void* stream) {
   if (t == nullptr || t->table == nullptr || d_entries == nullptr) {
     set_error("null argument");
     return AIRICE_EINVAL;
@@ -615,6 +621,12 @@ int airice_lookup_pack(const airice_lookup_table* t, float* d_entries, void* str
   if (t->n_entries < 1 || t->total_angle_steps < 1) {  // the row records divide by the row length
     set_error("lookup pack: n_entries (%zu) and total_angle_steps (%d) must be >= 1",
               t->n_entries, t->total_angle_steps);
+    return AIRICE_EINVAL;
+  }
+  const size_t need = AIRICE_LOOKUP_PACK_FLOATS(t->n_entries, t->total_angle_steps);
+  if (capacity_floats < need) {
+    set_error("lookup pack: %zu floats given, pack format 2 needs %zu "
+              "(AIRICE_LOOKUP_PACK_FLOATS / airice_lookup_pack_floats)", capacity_floats, need);
     return AIRICE_EINVAL;
   }
   const int rc = launch_lookup_pack(t, d_entries, (hipStream_t)stream);

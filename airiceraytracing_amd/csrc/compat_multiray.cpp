@@ -677,7 +677,8 @@ void TableLookupBatch(const double* SrcHeightASL, const double* HorizontalDistan
   if (dt.packed == nullptr) {
     if (t.total_angle_steps < 1 ||
         hipMalloc(&dt.packed, sizeof(float) * AIRICE_LOOKUP_PACK_FLOATS(entries, t.total_angle_steps)) != hipSuccess ||
-        airice_lookup_pack(&t, dt.packed, nullptr) != AIRICE_OK)
+        airice_lookup_pack(&t, dt.packed, AIRICE_LOOKUP_PACK_FLOATS(entries, t.total_angle_steps),
+                           nullptr) != AIRICE_OK)
       die("airice_lookup_pack");
     dt.packed_asteps = t.total_angle_steps;
   }

@@ -180,19 +180,20 @@ class AirIceSolver:
 
     @staticmethod
     def lookup_pack(lt: LookupTable, stream=None):
-        """airice_lookup_pack: a packed copy of the table (one 128-byte record per entry, holding
-        it and the next entry, then one 32-byte record per table row; torch tensor on the table's
-        device) that ``lt`` then reads; the tensor is kept on ``lt``."""
+        """airice_lookup_pack: a packed copy of the table (pack format 2: one 64-byte pair record
+        per entry, holding it and the next entry, one 256-byte record per table row and the angle
+        vector; torch tensor on the table's device) that ``lt`` then reads; the tensor is kept on
+        ``lt``."""
         import torch
         n, asteps = int(lt.n_entries), int(lt.total_angle_steps)
         if n < 1 or asteps < 1:  # as airice_lookup_pack: the row records divide by the row length
             raise ValueError(f"lookup_pack: n_entries ({n}) and total_angle_steps ({asteps}) "
                              "must be >= 1")
-        floats = n * _lib.LOOKUP_ENTRY_FLOATS + (n // asteps) * _lib.LOOKUP_ROW_FLOATS
+        floats = int(lib().airice_lookup_pack_floats(n, asteps))
         packed = torch.empty(floats, dtype=torch.float32,
                              device=torch.device("cuda", torch.cuda.current_device()))
-        check(lib().airice_lookup_pack(ctypes.byref(lt), ptr(packed), _stream_handle(stream)),
-              "airice_lookup_pack")
+        check(lib().airice_lookup_pack(ctypes.byref(lt), ptr(packed), floats,
+                                       _stream_handle(stream)), "airice_lookup_pack")
         lt.entries = ptr(packed).value
         lt._packed = packed
         return packed

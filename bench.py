@@ -527,7 +527,8 @@ def main(argv=None, make_backend=None, json_path=None):
         for _ in range(10):  # each pack bracketed on its own (median: a one-time setup cost)
             e0.record(stream)
             _lib.check(_lib.lib().airice_lookup_pack(ctypes.byref(lt), _lib.ptr(lt._packed),
-                                                     _stream_handle(stream)), "airice_lookup_pack")
+                                                     lt._packed.numel(), _stream_handle(stream)),
+                       "airice_lookup_pack")
             e1.record(stream)
             torch.cuda.synchronize()
             pack_times.append(e0.elapsed_time(e1))

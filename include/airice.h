@@ -186,29 +186,40 @@ typedef struct airice_lookup_table {
                                  reads the columns only); same values, fewer cache lines */
 } airice_lookup_table;
 
-/* Floats per packed record: record i holds columns 1-10 of entry i (floats 0-9) and of entry
- * i + 1 (floats 10-19; NaN for the last entry), then 12 zeros: 128 B, one L2 line when the array
- * is 128-byte aligned.  The lookup interpolates between entries i and i + 1 (FindClosestTHD's
- * index1, index2), so each table row it visits costs it one record line, which also supplies the
- * THD values at the pair. */
-#define AIRICE_LOOKUP_ENTRY_FLOATS 32
-/* Floats per row record, after the n_entries entry records, one per full table row
- * (n_entries / total_angle_steps rows): the row's FindClosestAirTxHeight span, the table values
- * the lookup reads at its ends and the THD values of the first four FindClosestTHD bisection
- * steps on both interpolation heights' spans (two 128-byte lines), folded once by the pack. */
+/* The packed copy (pack format 2, library 0.2; format 1 of 0.1.x had 32-float pair records and
+ * no angle vector -- a buffer sized for it is too small and airice_lookup_pack refuses it):
+ *  - pair records: record i holds columns 2, 3, 5, 6, 7, 8, 9, 10 of entry i (floats 0-7) and of
+ *    entry i + 1 (floats 8-15; NaN for the last entry): 64 B, one fabric request when the array
+ *    is 64-byte aligned.  The lookup interpolates between entries i and i + 1 (FindClosestTHD's
+ *    index1, index2), so each table row it visits costs it one record; the THD values at the pair
+ *    (column 1) come from its own search, the launch angles (column 4) from the angle vector;
+ *  - row records, from float AIRICE_LOOKUP_ROWS_OFFSET(n_entries) on (128-byte aligned), one per
+ *    full table row (n_entries / total_angle_steps rows): the row's FindClosestAirTxHeight span,
+ *    the table values the lookup reads at its ends and the THD values of the first four
+ *    FindClosestTHD bisection steps on both interpolation heights' spans (two 128-byte lines);
+ *  - the angle vector: column 4 of the first row (total_angle_steps floats, padded to 4), then one
+ *    int32 word: 1 when every row's column 4 equals it bit for bit (a MakeRayTracingTable table:
+ *    the launch angle is the grid's, .cc:2084-2105), else 0 and the lookup reads column 4. */
+#define AIRICE_LOOKUP_ENTRY_FLOATS 16
 #define AIRICE_LOOKUP_ROW_FLOATS 64
+#define AIRICE_LOOKUP_ROWS_OFFSET(n_entries) \
+  (((size_t)(n_entries) * AIRICE_LOOKUP_ENTRY_FLOATS + 31) / 32 * 32)
 /* Floats of the whole packed copy. */
-#define AIRICE_LOOKUP_PACK_FLOATS(n_entries, angle_steps)                 \
-  ((size_t)(n_entries) * AIRICE_LOOKUP_ENTRY_FLOATS +                    \
-   ((size_t)(n_entries) / (size_t)(angle_steps)) * AIRICE_LOOKUP_ROW_FLOATS)
+#define AIRICE_LOOKUP_PACK_FLOATS(n_entries, angle_steps)                          \
+  (AIRICE_LOOKUP_ROWS_OFFSET(n_entries) +                                         \
+   ((size_t)(n_entries) / (size_t)(angle_steps)) * AIRICE_LOOKUP_ROW_FLOATS +     \
+   ((size_t)(angle_steps) + 3) / 4 * 4 + 4)
+/* The same, as a call (0 when n_entries or total_angle_steps is < 1). */
+size_t airice_lookup_pack_floats(size_t n_entries, int32_t total_angle_steps);
 
-/* Pack one antenna's table for the lookup: AIRICE_LOOKUP_PACK_FLOATS(n_entries, total_angle_steps)
- * floats -- the entry records, then the row records (above) -- 16-byte aligned (128-byte for one
- * line per record).  The lookup reads the 10
- * interpolated parameters of both entries of a pair from one record instead of 10 columns ld
- * floats apart; results are identical.  Stream-ordered; run once per table, then set
+/* Pack one antenna's table for the lookup into d_entries: capacity_floats (at least
+ * AIRICE_LOOKUP_PACK_FLOATS(n_entries, total_angle_steps), else AIRICE_EINVAL and nothing is
+ * written) device floats, 16-byte aligned (64-byte for one request per pair record).  The lookup
+ * then reads the interpolated parameters of both entries of a pair from one record instead of 10
+ * columns ld floats apart; results are identical.  Stream-ordered; run once per table, then set
  * t->entries = d_entries. */
-int airice_lookup_pack(const airice_lookup_table *t, float *d_entries, void *stream);
+int airice_lookup_pack(const airice_lookup_table *t, float *d_entries, size_t capacity_floats,
+                       void *stream);
 
 #define AIRICE_LOOKUP_FALLBACK 1 /* the minimizer fallback ran (.cc:1418-1420) */
 #define AIRICE_LOOKUP_UNPINNED 2 /* the reference reads uninitialised/out-of-range memory here:

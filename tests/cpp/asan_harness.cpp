@@ -154,20 +154,21 @@ int main(int argc, char** argv) {
   std::vector<float> packed(AIRICE_LOOKUP_PACK_FLOATS(n, asteps) + 4);
   float* e = packed.data();
   while ((reinterpret_cast<uintptr_t>(e) & 15) != 0) ++e;  // 16-byte aligned records
-  for (int64_t i = 0; i < n; ++i) {
-    float* r = e + (size_t)AIRICE_LOOKUP_ENTRY_FLOATS * i;
-    for (int k = 0; k < 10; ++k) {
-      r[k] = T.col[1 + k][i];
-      r[10 + k] = i + 1 < n ? T.col[1 + k][i + 1] : NAN;
-    }
-    for (int k = 20; k < AIRICE_LOOKUP_ENTRY_FLOATS; ++k) r[k] = 0.0f;
-  }
+  for (int64_t i = 0; i < n; ++i)
+    airice::lk_pair_fold(T.col, n, i, e + (size_t)AIRICE_LOOKUP_ENTRY_FLOATS * i);
   airice::LkTable P = T;
   P.e = e;
   P.rows = n / asteps;
   for (int64_t r = 0; r < P.rows; ++r)
-    airice::lk_row_fold(P, r, e + (size_t)n * AIRICE_LOOKUP_ENTRY_FLOATS +
-                                  (size_t)r * AIRICE_LOOKUP_ROW_FLOATS);
+    airice::lk_row_fold(P, r, e + AIRICE_LOOKUP_ROWS_OFFSET(n) + (size_t)r * AIRICE_LOOKUP_ROW_FLOATS);
+  // the angle vector (column 4 of the first row; the harness's tables are MakeRayTracingTable's,
+  // so every row has it -- checked here as the pack checks it)
+  float* ang = e + airice::lk_angles_offset(n, asteps);
+  bool ang_ok = true;
+  for (int64_t j = 0; j < asteps; ++j) ang[j] = j < n ? T.col[4][j] : NAN;
+  for (int64_t i = 0; i < n; ++i)
+    ang_ok = ang_ok && airice::lk_bits_i(T.col[4][i]) == airice::lk_bits_i(T.col[4][i % asteps]);
+  P.ang = ang_ok ? ang : nullptr;
   or_lookup_table ot;
   for (int c = 0; c < 11; ++c) ot.col[c] = T.col[c];
   ot.n = (long)n;

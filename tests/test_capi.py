@@ -275,8 +275,31 @@ def test_lookup_pack_rejects_empty_angle_grid():
         t.n_entries = n
         t.loop_stop_height, t.height_step = 3000.0, 10.0
         t.total_height_steps, t.total_angle_steps = 10, asteps
-        rc = L.airice_lookup_pack(ctypes.byref(t), ctypes.c_void_p(0x20000), None)
+        rc = L.airice_lookup_pack(ctypes.byref(t), ctypes.c_void_p(0x20000), 1 << 20, None)
         assert rc == -1, rc  # AIRICE_EINVAL
         assert b"total_angle_steps" in L.airice_last_error()
+        assert L.airice_lookup_pack_floats(n, asteps) == 0
         with pytest.raises(ValueError):
             AirIceSolver.lookup_pack(t)
+
+
+def test_lookup_pack_checks_capacity():
+    """Pack format 2 (library 0.2) changed the packed copy's size: the pack takes the
+    buffer's capacity and refuses one sized for another format (format 1's 32-float records are
+    larger, but a caller with a smaller buffer -- or a stale AIRICE_LOOKUP_PACK_FLOATS -- must get
+    AIRICE_EINVAL, never a write past the end).  No device memory is touched."""
+    import ctypes
+    from airiceraytracing_amd import _lib
+    L = _lib.lib()
+    assert b"0.2.0" in L.airice_version() and b"pack format 2" in L.airice_version()
+    n, asteps = 858627, 177
+    need = L.airice_lookup_pack_floats(n, asteps)
+    assert need == _lib.lookup_pack_floats(n, asteps)
+    assert need == _lib.lookup_rows_offset(n) + (n // asteps) * 64 + 180 + 4
+    t = _lib.LookupTable()
+    t.table, t.ld, t.n_entries = 0x10000, n, n
+    t.loop_stop_height, t.height_step = 3000.0, 20.0
+    t.total_height_steps, t.total_angle_steps = n // asteps, asteps
+    rc = L.airice_lookup_pack(ctypes.byref(t), ctypes.c_void_p(0x20000), need - 1, None)
+    assert rc == -1, rc
+    assert b"pack format 2" in L.airice_last_error()

@@ -107,3 +107,25 @@ def test_replay_edge_grid(solvers):
     g = g[keep]
     fast, exact = _both(lambda: sp.trace_ice_to_air_host(g[:, 2], g[:, 3], g[:, 0], g[:, 1]))
     _same(fast, exact)
+
+
+def test_replay_grazing_and_layer_bounds(solvers):
+    """Where f is most curved: launch angles near 90 degrees (distances of 5-400x the height over
+    the ice: the probe runs and f steepens towards the NaN edge) and transmitters within a metre
+    of the atmosphere's layer bounds.  The slope-placed guards (placed only where the last two
+    secant slopes agree within 2x, else evaluated) must decide every midpoint as its evaluation
+    does."""
+    s, _ = solvers
+    rng = np.random.default_rng(21)
+    n = 60000
+    bounds = np.array([3217.48275, 8363.53902, 23141.7538, 50000.0])
+    h1 = rng.uniform(3050, 20000, n // 2)
+    d1 = (h1 - 3000) * rng.uniform(5, 400, n // 2)
+    h2 = rng.choice(bounds, n // 2) + rng.uniform(-1, 1, n // 2)
+    d2 = (h2 - 3000) * rng.uniform(0.01, 50, n // 2)
+    txh = np.concatenate([h1, h2])
+    dist = np.concatenate([d1, d2])
+    depth = -rng.uniform(0, 200, n)
+    (out_f, st_f), (out_e, st_e) = _both(lambda: s.solve_host(txh, dist, depth, 3000.0))
+    _same(st_f, st_e)
+    _same(out_f, out_e)

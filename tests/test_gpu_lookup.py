@@ -68,13 +68,23 @@ def _run_case(solver, oracle_medium, depth_cm, hstep, a0, a1, astep, nq, seed):
     assert np.array_equal(ok_p.cpu().numpy(), ok) and np.array_equal(fl_p.cpu().numpy(), fl)
     flat = lp._packed.cpu().numpy()
     ne, asteps = host.shape[1], g.angle_steps
-    packed = flat[:ne * 32].reshape(-1, 32)  # record i: columns 1-10 of entries i, i+1
-    assert np.array_equal(packed[:, :10].T, host[1:11], equal_nan=True)
-    assert np.array_equal(packed[:-1, 10:20].T, host[1:11, 1:], equal_nan=True)
-    assert np.isnan(packed[-1, 10:20]).all() and not packed[:, 20:].any()
-    # row records: the row's usable-THD span inside the row and the values at its ends
     from airiceraytracing_amd import _lib
-    rows = flat[ne * 32:].reshape(ne // asteps, _lib.LOOKUP_ROW_FLOATS)
+    assert flat.size == _lib.lookup_pack_floats(ne, asteps)
+    # pair record i (64 B): columns 2, 3, 5-10 of entries i, i+1 (THD and the launch angle come
+    # from the search and the angle vector)
+    cols = [2, 3, 5, 6, 7, 8, 9, 10]
+    packed = flat[:ne * 16].reshape(-1, 16)
+    assert np.array_equal(packed[:, :8].T, host[cols], equal_nan=True)
+    assert np.array_equal(packed[:-1, 8:].T, host[cols][:, 1:], equal_nan=True)
+    assert np.isnan(packed[-1, 8:]).all()
+    # the angle vector: column 4 of the first row, verified against every row (word = 1)
+    a0 = _lib.lookup_rows_offset(ne) + (ne // asteps) * _lib.LOOKUP_ROW_FLOATS
+    assert np.array_equal(flat[a0:a0 + asteps], host[4][:asteps])
+    assert flat[a0 + (asteps + 3) // 4 * 4:].view(np.int32)[0] == 1
+    assert np.array_equal(host[4].reshape(-1, asteps), np.tile(host[4][:asteps], (ne // asteps, 1)))
+    # row records: the row's usable-THD span inside the row and the values at its ends
+    r0 = _lib.lookup_rows_offset(ne)
+    rows = flat[r0:a0].reshape(ne // asteps, _lib.LOOKUP_ROW_FLOATS)
     ri = rows.view(np.int32)
     r = np.arange(rows.shape[0])
     okr = ri[:, 7] == 1
