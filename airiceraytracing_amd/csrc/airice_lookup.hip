@@ -54,10 +54,12 @@ __global__ __launch_bounds__(kLkBlock) void lookup_kernel(LkTable T, const doubl
   if (T.ang != nullptr && *reinterpret_cast<const int*>(T.ang + (lk_angles_ok_offset(T.n, T.asteps) -
                                                                   lk_angles_offset(T.n, T.asteps))) == 0)
     T.ang = nullptr;
+  // the THD windows of lk_closest_thd_tree: one 4-byte column per thread
+  __shared__ float s_win[kLkWindow][kLkBlock];
   int fl = 0;
   double o[9];
   bool good = false;
-  if (!lk_query(T, src[k] / 100, dist[k] / 100, d2r, o, &good, fl)) {
+  if (!lk_query(T, src[k] / 100, dist[k] / 100, d2r, o, &good, fl, &s_win[0][threadIdx.x])) {
 #pragma unroll
     for (int c = 0; c < 9; ++c) out[c * ld + k] = o[c];
   }

@@ -190,8 +190,8 @@ __host__ __device__ __forceinline__ LkTxhBins lk_closest_txh(const LkTable& T, d
 // interpolation height searches (s2, e2): a query then takes its first four steps from two 128-byte
 // lines it reads anyway instead of four dependent gathers into the THD column, and the rest of
 // the search and the linear scan from one short window of that column (lk_closest_thd_tree).
-constexpr int kLkBlock = 256;      // threads per block of the batch lookup_kernel (the LDS window
-                                   // below has one column per thread of such a block)
+constexpr int kLkBlock = 256;      // threads per block of the batch lookup_kernel (its LDS window
+                                   // has one column per thread: lk_closest_thd_tree)
 constexpr int kLkTreeNodes = 15;  // bisection steps 0-3
 constexpr int kLkWindow = 12;     // THD entries the steps 4-7 and the scan may read
 struct LkTree {
@@ -403,11 +403,14 @@ __host__ __device__ __forceinline__ bool lk_step32(double v, double P, int& s, i
 // or NaN midpoint), the scan runs off its end without a break, or the pair has no packed record;
 // every value it reads lies inside the table, so no flag changes.  Indices are 32-bit here (the
 // row fold admits spans below 2^31 only).
+// win: on the device, this lane's column of the caller's LDS window (lookup_kernel: kLkWindow rows
+// of kLkBlock lanes, row stride kLkBlock; without one the lane takes the column path); on the
+// host the window is a private array.
 __host__ __device__ __forceinline__ bool lk_closest_thd_tree(const LkTable& T, double P, long long s_in,
                                                              long long e_in, const float* t,
                                                              float4 top, float4 topb,
                                                              LkThdBins& out, LkThdPair& pr,
-                                                             long long abase) {
+                                                             long long abase, float* win) {
   if (s_in < 0 || e_in < s_in || T.n < kLkWindow || T.n >= (1LL << 31)) return false;
   int s = (int)s_in, e = (int)e_in;
   bool fin = false;
@@ -429,14 +432,22 @@ __host__ __device__ __forceinline__ bool lk_closest_thd_tree(const LkTable& T, d
   if (e - s >= kLkWindow) return false;
   const int n32 = (int)T.n;
   const int base = s <= n32 - kLkWindow ? s : n32 - kLkWindow;  // the window covers [s, e]
-  // the window, indexed per lane: on the device in the block's LDS (one column of 4-byte slots
-  // per lane, kLkWindow rows kLkBlock lanes apart: conflict-free, and each read one instruction where
-  // a register multiplexer takes 11 selects); the lane reads only what it wrote
+  // the window, indexed per lane: in lookup_kernel in the block's LDS (one column of 4-byte slots
+  // per lane, kLkWindow rows kLkBlock lanes apart: conflict-free, and each read one instruction
+  // where a register multiplexer takes 11 selects; the lane reads only what it wrote), otherwise
+  // a private array
   const float* src = T.col[1] + base;
 #if defined(__HIP_DEVICE_COMPILE__)
-  __shared__ float s_win[kLkWindow][kLkBlock];
-  float* w = &s_win[0][threadIdx.x % kLkBlock];  // launched with kLkBlock threads per block
+  // device callers pass their window (a private array indexed per lane would live in scratch)
+  if (win == nullptr) return false;
+  float* w = win;
   constexpr int ws = kLkBlock;
+#else
+  float priv[kLkWindow];
+  float* w = priv;
+  constexpr int ws = 1;
+  (void)win;
+#endif
   // three 16-byte loads at 4-byte alignment (gfx950 vector memory takes unaligned dwordx4)
   typedef float f4u __attribute__((ext_vector_type(4), aligned(4)));
 #pragma unroll
@@ -447,11 +458,6 @@ __host__ __device__ __forceinline__ bool lk_closest_thd_tree(const LkTable& T, d
     w[(4 * q + 2) * ws] = a.z;
     w[(4 * q + 3) * ws] = a.w;
   }
-#else
-  float w[kLkWindow];
-  constexpr int ws = 1;
-  std::memcpy(w, src, sizeof(w));
-#endif
 #pragma unroll
   for (int i = 4; i < 8; ++i) {
     fin = fin || e - s < 3;
@@ -505,13 +511,13 @@ __host__ __device__ __forceinline__ void lk_row_params(const LkTable& T, double 
                                               const float* tree = nullptr,
                                               float4 tree_top = float4{},
                                               float4 tree_topb = float4{},
-                                              long long abase = -1) {
+                                              long long abase = -1, float* win = nullptr) {
   const double max_thd = max_thd_row != nullptr ? *max_thd_row : lk_at(T, 1, s, fl);
   if (D <= max_thd) {
     LkThdPair pr;
     LkThdBins b;
     if (tree == nullptr ||
-        !lk_closest_thd_tree(T, D, s, e, tree, tree_top, tree_topb, b, pr, abase)) {
+        !lk_closest_thd_tree(T, D, s, e, tree, tree_top, tree_topb, b, pr, abase, win)) {
       pr.have_pair = false;
       b = lk_closest_thd(T, D, s, e, fl, pr, abase);
     }
@@ -536,9 +542,10 @@ __host__ __device__ __forceinline__ void lk_row_params(const LkTable& T, double 
   }
 }
 
-// GetParValues (.cc:1172-1302) for a Tx height inside the table's range
+// GetParValues (.cc:1172-1302) for a Tx height inside the table's range (win: lk_closest_thd_tree)
 __host__ __device__ __forceinline__ void lk_par_values(const LkTable& T, double H, double D, double* h1,
-                                       double par1[10], double* h2, double par2[10], int& fl) {
+                                       double par1[10], double* h2, double par2[10], int& fl,
+                                       float* win = nullptr) {
   const double min_h = lk_at(T, 0, T.n - 1, fl);
   LkRow R;  // packed row record: the span and its end values without the scans
   const long long index = lk_txh_index(T, H);
@@ -557,13 +564,13 @@ __host__ __device__ __forceinline__ void lk_par_values(const LkTable& T, double 
   const long long abase1 = index * T.asteps;
   const long long abase2 = b.s2 < b.s1 ? abase1 - T.asteps : abase1 + T.asteps;
   lk_row_params(T, D, b.s1, b.e1, par1, &c1, fl, fast ? &R.mt1 : nullptr,
-                fast && R.tree1 ? R.rec + 8 : nullptr, R.top1, R.top1b, abase1);
+                fast && R.tree1 ? R.rec + 8 : nullptr, R.top1, R.top1b, abase1, win);
   *h2 = *h1;
   if (b.c1 != 0 && H > min_h && b.s2 < T.n - 1) {
     *h2 = fast ? R.h2 : lk_at(T, 0, b.s2, fl);
     double c2 = 0;
     lk_row_params(T, D, b.s2, b.e2, par2, &c2, fl, fast ? &R.mt2 : nullptr,
-                  fast && R.tree2 ? R.rec + 32 : nullptr, R.top2, R.top2b, abase2);
+                  fast && R.tree2 ? R.rec + 32 : nullptr, R.top2, R.top2b, abase2, win);
   } else {
 #pragma unroll
     for (int ip = 0; ip < 10; ++ip) par2[ip] = par1[ip];
@@ -574,7 +581,7 @@ __host__ __device__ __forceinline__ void lk_par_values(const LkTable& T, double 
 // in the reference's argument order, *good = CheckSolution.  Returns true when the query hits the
 // one-sided extrapolation case, whose outputs the minimizer fallback (.cc:1418-1420) rewrites.
 __host__ __device__ __forceinline__ bool lk_query(const LkTable& T, double H, double D, double d2r, double out[9],
-                                  bool* good_out, int& fl) {
+                                  bool* good_out, int& fl, float* win = nullptr) {
   const double max_h = lk_at(T, 0, 0, fl);
   const double min_h = lk_at(T, 0, T.n - 1, fl);
   double x1 = 0, x2 = 0, y1 = 0, y2 = 0;
@@ -584,7 +591,7 @@ __host__ __device__ __forceinline__ bool lk_query(const LkTable& T, double H, do
   for (int i = 0; i < 10; ++i) piv[i] = 0;
   if (H <= max_h && H >= min_h && H > 0) {
     double par1[10], par2[10];
-    lk_par_values(T, H, D, &x1, par1, &x2, par2, fl);
+    lk_par_values(T, H, D, &x1, par1, &x2, par2, fl, win);
     // interpolation in height (.cc:1376-1401); a parameter missing at both heights ends the
     // loop writing its value into slot 9 (the reference sets ipar = 9 before the store)
     bool done = false;

@@ -136,10 +136,12 @@ def assemble_to_host(slab: torch.Tensor, count_items: int, first_item: int, host
 
 
 def _try(make):
-    """(make(), None), or (None, the error's text) when it raises OSError / ValueError."""
+    """(make(), None), or (None, the error's text) when it raises: any exception (a RuntimeError
+    from torch.from_file as well as an OSError), so that every failure reaches the agreement
+    all-reduce (_all_ok) instead of leaving the other ranks waiting in it."""
     try:
         return make(), None
-    except (OSError, ValueError) as e:
+    except Exception as e:  # noqa: BLE001 -- reported to every rank, never swallowed
         return None, f"{type(e).__name__}: {e}"
 
 
@@ -206,9 +208,9 @@ def run_sharded_table(grid, compute: Callable[[int, int, torch.Tensor], None], s
       backend "nccl"; gather_slabs), the root holding the table once;
     * ``assemble="host"``: in host memory, where the reference keeps the table (its row loop
       appends to AllTableAllAntData, .cc:2079-2136): every rank copies its slab into its rows of a
-      SharedHostTable at ``host_path`` (``host_copy``: the GPU path's 2-D DMA, airice_table_to_host,
-      into page-locked pages, ``host_register``), all ranks' copies in parallel over their own
-      PCIe links; no collective moves table data.
+      SharedHostTable at ``host_path`` (``host_copy``: the GPU path's strided D2H copy per
+      column, airice_table_to_host, into page-locked pages, ``host_register``), all ranks' copies
+      in parallel over their own PCIe links; no collective moves table data.
 
     ``compute(row_begin, row_count, slab)`` fills the slab (stride = rows_per_rank x
     angle_steps); ``sync`` waits for the device (torch.cuda.synchronize on a GPU).  Returns the

@@ -401,6 +401,9 @@ def main(argv=None, make_backend=None, json_path=None):
     if not cfg4_headline:
         # (a rank whose slab is empty recorded no events; only rank 0 reports, and it has rows)
         kern_ms = ev0.elapsed_time(ev1) / args.steps if n_local > 0 else None
+    # every rank's own kernel time (HIP events on its launch stream), gathered for the line
+    kern_ms_ranks = gather_floats(kern_ms if not cfg4_headline else rep4.get("kernel_ms_this_rank"),
+                                  distributed, world, coll_dev)
     value = total_rays / elapsed
     extra = {}
 
@@ -748,7 +751,15 @@ def main(argv=None, make_backend=None, json_path=None):
             "scaling": "strong" if cfg4_headline else "weak",
             "vs_baseline": None,
             "dtype": "f64",
-            "data": "synthetic (BASELINE cfg2 grid) over the reference GDAS Atmosphere.dat",
+            "data": ("synthetic (BASELINE cfg4 grid, sharded over %d GPUs)" % world
+                     if cfg4_headline else
+                     "synthetic (BASELINE cfg2 grid refined %dx in TxH, sharded over %d GPUs)"
+                     % (world, world) if sharded else
+                     "synthetic (BASELINE cfg2 grid%s)" % (", one per GPU" if world > 1 else ""))
+                    + " over the reference GDAS Atmosphere.dat",
+            "rccl_world_size": dist.get_world_size() if distributed else 1,
+            "dist_backend": backend if distributed else None,
+            "kernel_ms_per_rank": kern_ms_ranks,
             "config": {"workload": workload, "rays_per_gpu_step": n_local, "table_columns": 11,
                        "store": "f32", "parallelism": par},
             "roofline": roof,
@@ -762,6 +773,19 @@ def main(argv=None, make_backend=None, json_path=None):
         os.write(json_fd, (json.dumps(line) + "\n").encode())
     if distributed:
         dist.destroy_process_group()
+
+
+def gather_floats(x, distributed, world, coll_dev) -> list:
+    """One float (None: NaN) from every rank, in rank order (all_gather; [x] on one process)."""
+    if not distributed:
+        return [x]
+    import torch
+    import torch.distributed as dist
+    t = torch.tensor([float("nan") if x is None else float(x)], dtype=torch.float64,
+                     device=coll_dev)
+    parts = [torch.zeros_like(t) for _ in range(world)]
+    dist.all_gather(parts, t)
+    return [None if v != v else v for v in (float(q.item()) for q in parts)]
 
 
 def table_cold(solver, grid, table, stream, rank, warm_kernel_ms, builds: int = 16) -> dict:
@@ -834,9 +858,10 @@ def cfg4_check_rows(height_steps: int, step: float = 1.0) -> list[int]:
 def table_cfg4(args, be, world, rank, distributed, coll_dev, pmc) -> dict:
     """BASELINE cfg4, the fine table (872,135,991 rays, 38.4 GB): built in HBM (N=1: the whole
     grid on one GPU; N>1: contiguous TxH-row slabs, one per GPU), timed over cfg4_reps builds, then
-    assembled in host memory where the reference keeps AllTableAllAntData (.cc:2079-2136): one
-    2-D DMA per GPU (airice_table_to_host) into page-locked host pages -- a private buffer at N=1,
-    a node-shared mapping (distributed.SharedHostTable) that every rank fills in parallel at N>1.
+    assembled in host memory where the reference keeps AllTableAllAntData (.cc:2079-2136): per
+    GPU one strided D2H copy per column (airice_table_to_host) into page-locked host pages -- a
+    private buffer at N=1, a node-shared mapping (distributed.SharedHostTable) that every rank
+    fills in parallel at N>1.
     Rank 0 checks cfg4_check_rows() of the host table against the oracle."""
     import torch
     import torch.distributed as dist
@@ -895,9 +920,10 @@ def table_cfg4(args, be, world, rank, distributed, coll_dev, pmc) -> dict:
         if r.get("host_assembly_error"):
             rep["host_assembly_error"] = r["host_assembly_error"]
         build_s = r["elapsed_s"] / args.cfg4_reps
+        kms_rank = ev0.elapsed_time(ev1) / args.cfg4_reps if r["rays_this_rank"] > 0 else None
         rep.update({"value": n / build_s, "ms_per_build": build_s * 1e3,
-                    "kernel_ms_rank0": ev0.elapsed_time(ev1) / args.cfg4_reps
-                    if r["rays_this_rank"] > 0 else None,
+                    "kernel_ms_rank0": kms_rank, "kernel_ms_this_rank": kms_rank,
+                    "kernel_ms_per_rank": gather_floats(kms_rank, distributed, world, coll_dev),
                     "rows_per_rank": r["rows_per_rank"], "assemble": mode,
                     "assemble_ms": r["gather_s"] * 1e3,
                     "assemble_GBps": r["bytes_assembled"] / r["gather_s"] / 1e9

@@ -138,13 +138,23 @@ def test_gloo_bench_sharded_mode_assembles_table_bitwise(world):
     assert nbytes == (g.height_steps - shard_rows(g.height_steps, world, 0)[1]) * g.angle_steps * 44
 
 
-def _cfg4_mode_worker(rank, world, port, q, assemble, host_path):
+def _cfg4_mode_worker(rank, world, port, q, assemble, host_path, map_raises=False):
     """bench.py's cfg4 item / --workload cfg4 logic (run_sharded_table with the cfg4 angle grid,
     coarsened in TxH for the CPU) with the oracle as the slab compute: the table assembled in host
-    memory (SharedHostTable, every rank writing its rows) or by per-column gathers."""
+    memory (SharedHostTable, every rank writing its rows) or by per-column gathers.  map_raises:
+    every non-root rank's mapping of the shared table raises a RuntimeError (not an OSError)."""
     import oracle
+    from airiceraytracing_amd import distributed as D
     from airiceraytracing_amd.distributed import run_sharded_table
     from tests.conftest import ATMOSPHERE_GZ
+    if map_raises and rank != 0:
+        real = D.SharedHostTable
+
+        def failing(path, cols, n, create):
+            if not create:
+                raise RuntimeError("injected: mapping the shared host table failed")
+            return real(path, cols, n, create=create)
+        D.SharedHostTable = failing
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     m = oracle.load_atmosphere(ATMOSPHERE_GZ)
@@ -166,19 +176,23 @@ def _cfg4_mode_worker(rank, world, port, q, assemble, host_path):
 
 
 @pytest.mark.parametrize("assemble,world", [("host", 2), ("host", 3), ("rccl", 3),
-                                            ("host-fail", 2)])
+                                            ("host-fail", 2), ("host-map-raises", 3)])
 def test_gloo_cfg4_mode_assembles_table_bitwise(tmp_path, assemble, world):
     """host-fail: the root cannot create the shared host table (its directory does not exist):
-    every rank learns it and takes the gather path, instead of the others waiting in a barrier."""
+    every rank learns it and takes the gather path, instead of the others waiting in a barrier.
+    host-map-raises: the non-root ranks' mappings raise a RuntimeError (only OSError /
+    ValueError used to reach the agreement); the same fallback, no deadlock."""
     import oracle
     from tests.conftest import ATMOSPHERE_GZ
     ctx = mp.get_context("spawn")
     q = ctx.SimpleQueue()
     port = _free_port()
-    fail = assemble == "host-fail"
+    raises = assemble == "host-map-raises"
+    fail = assemble == "host-fail" or raises
     assemble = "host" if fail else assemble
-    host_path = str(tmp_path / ("no_such_dir" if fail else "") / "airice_host_table")
-    procs = [ctx.Process(target=_cfg4_mode_worker, args=(r, world, port, q, assemble, host_path))
+    host_path = str(tmp_path / ("no_such_dir" if fail and not raises else "") / "airice_host_table")
+    procs = [ctx.Process(target=_cfg4_mode_worker,
+                         args=(r, world, port, q, assemble, host_path, raises))
              for r in range(world)]
     for p in procs:
         p.start()
@@ -190,7 +204,9 @@ def test_gloo_cfg4_mode_assembles_table_bitwise(tmp_path, assemble, world):
     g = oracle.grid_init(-20000.0, 300000.0, 997.0, 90.1, 180.0, 0.37)
     ref = oracle.table_rows(m, g, 0, g.height_steps)
     if fail:
-        assert mode == "rccl" and err is not None and "FileNotFoundError" in err
+        assert mode == "rccl" and err is not None
+        assert ("RuntimeError" if raises else "FileNotFoundError") in err or \
+            (raises and "could not map" in err), err
         assemble = "rccl"
     else:
         assert err is None
