@@ -103,6 +103,8 @@ class LookupTable(ctypes.Structure):
     ]
 
 
+SCALAR_HOST, SCALAR_DEVICE = 0, 1  # AIRICE_SCALAR_HOST / AIRICE_SCALAR_DEVICE
+
 LOOKUP_ENTRY_FLOATS = 16  # AIRICE_LOOKUP_ENTRY_FLOATS (pack format 2)
 LOOKUP_ROW_FLOATS = 64  # AIRICE_LOOKUP_ROW_FLOATS
 
@@ -144,12 +146,15 @@ LOOKUP_UNPINNED = 2  # AIRICE_LOOKUP_UNPINNED
 # RayTracingFunctions:: scalar ops (include/airice.h AIRICE_RTF_*)
 RTF_HIT_POINT, RTF_OPTICAL_PATH, RTF_PROPAGATION_TIME, RTF_AIR_PROPAGATION = 0, 1, 2, 3
 RTF_ICE_PROPAGATION, RTF_FDNFR, RTF_FTIMED, RTF_MIN_LAUNCH = 4, 5, 6, 7
+# MultiRayAirIceRefraction:: forms of the ray layer (AIRICE_MR_*)
+MR_FPATHD, MR_GEOMETRIC_PATH, MR_HIT_POINT, MR_AIR_PROPAGATION = 9, 10, 11, 12
+MR_ICE_PROPAGATION, MR_MIN_LAUNCH = 13, 14
 
 EXPORTED_SYMBOLS = (
     "airice_last_error", "airice_version", "airice_atmosphere_load", "airice_atmosphere_parse",
     "airice_nz_air", "airice_nz_ice", "airice_grid_init", "airice_table_launch",
     "airice_table_launch_multi",
-    "airice_table_host", "airice_rays_launch", "airice_solve_launch", "airice_solve_host",
+    "airice_table_host", "airice_rays_launch", "airice_rays_host", "airice_scalar_mode", "airice_solve_launch", "airice_solve_host",
     "airice_hdtip_launch", "airice_table_lookup_launch", "airice_lookup_pack", "airice_lookup_pack_floats", "airice_single_ray_plan",
     "airice_single_ray_launch", "airice_single_ray_host", "airice_trace_ice_to_air_launch",
     "airice_trace_ice_to_air_host", "airice_rtf_outputs", "airice_rtf_eval",
@@ -207,6 +212,8 @@ def lib() -> ctypes.CDLL:
         "airice_table_host": ([M, G, ctypes.c_int32, ctypes.c_int32, P, P, S], I),
         "airice_table_launch_multi": ([M, G, ctypes.c_int32, P, P, P], I),
         "airice_rays_launch": ([M, P, P, D, D, ctypes.c_int32, S, P, S, P], I),
+        "airice_rays_host": ([M, P, P, D, D, ctypes.c_int32, S, P, S], I),
+        "airice_scalar_mode": ([I], I),
         "airice_solve_launch": ([M, I, D, P, P, P, P, S, P, S, P, P], I),
         "airice_solve_host": ([M, I, D, P, P, P, P, S, P, S, P], I),
         "airice_hdtip_launch": ([M, P, P, P, D, S, P, S, P, P], I),

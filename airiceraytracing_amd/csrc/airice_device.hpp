@@ -28,6 +28,8 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <cmath>
+
 #include "airice_tlog.hpp"
 
 namespace airice {
@@ -126,7 +128,7 @@ __host__ __device__ inline TopEnd make_topend(const Endpoint& R) {
   return TopEnd{R.x, R.n, R.y2, R.Ay, R.invC, R.invC * (1.0 / speedc), R.Cx, R.ACx};
 }
 
-__device__ __forceinline__ double sel5(const double (&a)[5], int l) {
+__host__ __device__ __forceinline__ double sel5(const double (&a)[5], int l) {
   double r = a[0];
   r = (l == 1) ? a[1] : r;
   r = (l == 2) ? a[2] : r;
@@ -136,7 +138,7 @@ __device__ __forceinline__ double sel5(const double (&a)[5], int l) {
 }
 
 // Air layer of |z| (GetB_air/GetC_air scan, .cc:221-230).
-__device__ __forceinline__ int air_layer(const DevMedium& M, double zabs) {
+__host__ __device__ __forceinline__ int air_layer(const DevMedium& M, double zabs) {
   int which = 0;
   bool found = false;
 #pragma unroll
@@ -150,7 +152,7 @@ __device__ __forceinline__ int air_layer(const DevMedium& M, double zabs) {
   return which;
 }
 
-__device__ __forceinline__ Endpoint air_endpoint(const DevMedium& M, double x) {
+__host__ __device__ __forceinline__ Endpoint air_endpoint(const DevMedium& M, double x) {
   const double zabs = fabs(x);
   const int l = air_layer(M, zabs);
   const double B = sel5(M.B, l), C = sel5(M.negC, l);
@@ -159,14 +161,14 @@ __device__ __forceinline__ Endpoint air_endpoint(const DevMedium& M, double x) {
   return make_endpoint(M.A_air, B, C, x, e_abs, e_x);
 }
 
-__device__ __forceinline__ Endpoint ice_endpoint(const DevMedium& M, double x) {
+__host__ __device__ __forceinline__ Endpoint ice_endpoint(const DevMedium& M, double x) {
   const double zabs = fabs(x);
   const double e_abs = exp(M.negC_ice * zabs);
   const double e_x = (x >= 0.0) ? e_abs : exp(M.negC_ice * x);
   return make_endpoint(M.A_ice, M.B_ice, M.negC_ice, x, e_abs, e_x);
 }
 
-__device__ __forceinline__ Endpoint pick(bool c, const Endpoint& a, const Endpoint& b) {
+__host__ __device__ __forceinline__ Endpoint pick(bool c, const Endpoint& a, const Endpoint& b) {
   Endpoint r;
   r.x = c ? a.x : b.x;
   r.C = c ? a.C : b.C;
@@ -183,7 +185,7 @@ __device__ __forceinline__ Endpoint pick(bool c, const Endpoint& a, const Endpoi
 }
 
 // sin(asin(u)): u on the domain of asin, NaN outside it (identity (2)).
-__device__ __forceinline__ double sin_asin(double u) { return (fabs(u) <= 1.0) ? u : __builtin_nan(""); }
+__host__ __device__ __forceinline__ double sin_asin(double u) { return (fabs(u) <= 1.0) ? u : __builtin_nan(""); }
 
 // Per-segment constants of the ray parameter L.
 struct RayL {
@@ -191,7 +193,7 @@ struct RayL {
 };
 
 // High 32 bits (sign, exponent, top of the mantissa) of a double.
-__device__ __forceinline__ uint32_t hi_word(double x) {
+__host__ __device__ __forceinline__ uint32_t hi_word(double x) {
   return (uint32_t)(__builtin_bit_cast(uint64_t, x) >> 32);
 }
 
@@ -199,7 +201,14 @@ __device__ __forceinline__ uint32_t hi_word(double x) {
 // iteration ocml's sqrt uses, without its denormal rescaling: q here is a difference of squares of
 // O(1) refractive indices); both within ~1 ulp.  q = 0 gives (0, +inf) and q < 0 / NaN gives NaNs,
 // as sqrt() and 1/sqrt() do.
-__device__ __forceinline__ void sqrt_rsqrt(double q, double& s, double& rs) {
+__host__ __device__ __forceinline__ void sqrt_rsqrt(double q, double& s, double& rs) {
+#if !defined(__HIP_DEVICE_COMPILE__)
+  // host (the one-query calls, AIRICE_SCALAR): the correctly rounded forms (<= 1 ulp from the
+  // device iteration)
+  s = std::sqrt(q);
+  rs = 1.0 / s;
+  return;
+#else
   const double y = __builtin_amdgcn_rsq(q);
   double g = q * y, h = 0.5 * y;
   double e = __builtin_fma(-h, g, 0.5);
@@ -211,12 +220,16 @@ __device__ __forceinline__ void sqrt_rsqrt(double q, double& s, double& rs) {
   h = __builtin_fma(h, e, h);
   s = (q == 0.0) ? q : g;
   rs = (q == 0.0) ? __builtin_inf() : 2.0 * h;
+#endif
 }
 
 // sqrt(q) (same iteration, no reciprocal): within ~1 ulp; q = 0 -> 0, q < 0 / NaN -> NaN.
 // The q = 0 case needs no select: v_rsq_f64(q + 2^-1074) is finite at q = 0, and the added
 // 2^-1074 leaves every q >= 2^-1020 (and every q <= 0, NaN) unchanged.
-__device__ __forceinline__ double fast_sqrt(double q) {
+__host__ __device__ __forceinline__ double fast_sqrt(double q) {
+#if !defined(__HIP_DEVICE_COMPILE__)
+  return std::sqrt(q);  // host: correctly rounded (the device iteration is within ~1 ulp of it)
+#else
   const double y = __builtin_amdgcn_rsq(q + 0x1p-1074);
   double g = q * y, h = 0.5 * y;
   const double e = __builtin_fma(-h, g, 0.5);
@@ -225,6 +238,7 @@ __device__ __forceinline__ double fast_sqrt(double q) {
   const double d = __builtin_fma(-g, g, q);
   g = __builtin_fma(d, h, g);
   return g;  // q = 0: y finite, so g = 0 * y = 0 through every step
+#endif
 }
 
 // a / b for b positive and normal (2^-1000 <= b < 2^1000): v_rcp_f64 (24 bits, measured by
@@ -232,7 +246,10 @@ __device__ __forceinline__ double fast_sqrt(double q) {
 // (Markstein) -- the IEEE quotient but for rare last-bit cases.  Other b, and a non-finite
 // result (an infinite or NaN a, an overflowing quotient: the residual is then NaN), take the IEEE
 // division (tests/test_device_prims.py forces each case).
-__device__ __forceinline__ double div_pos(double a, double b) {
+__host__ __device__ __forceinline__ double div_pos(double a, double b) {
+#if !defined(__HIP_DEVICE_COMPILE__)
+  return a / b;  // host: the IEEE quotient (the device form's value but for rare last bits)
+#else
   if (!(hi_word(b) - 0x01700000u < 0x7D000000u)) return a / b;
   double y = __builtin_amdgcn_rcp(b);
   y = __builtin_fma(y, __builtin_fma(-b, y, 1.0), y);
@@ -240,12 +257,13 @@ __device__ __forceinline__ double div_pos(double a, double b) {
   const double q = __builtin_fma(__builtin_fma(-b, q0, a), y, q0);
   if (__builtin_expect(!__builtin_isfinite(q), 0)) return a / b;
   return q;
+#endif
 }
 
 // asin(x) (radians): t + t^3 P(t^2) on |x| < 1/2 (P: degree-12 fit, tools/gen_asin_poly.py, error
 // 1.2e-16 relative), pi/2 - 2 asin(sqrt((1 - |x|)/2)) above (1 - |x| exact there); NaN for
 // |x| > 1 or NaN, as asin().  ~25 FP64 ops against ~64 for ocml's asin (tools/opweights.json).
-__device__ __forceinline__ double asin_fast(double x) {
+__host__ __device__ __forceinline__ double asin_fast(double x) {
   const double ax = fabs(x);
   const bool big = ax >= 0.5;
   const double s = big ? 0.5 * (1.0 - ax) : ax * ax;
@@ -268,9 +286,9 @@ __device__ __forceinline__ double asin_fast(double x) {
 }
 
 // asin for the kernels' angle outputs
-__device__ __forceinline__ double k_asin(double x) { return asin_fast(x); }
+__host__ __device__ __forceinline__ double k_asin(double x) { return asin_fast(x); }
 
-__device__ __forceinline__ RayL ray_L(double A2, double L) {
+__host__ __device__ __forceinline__ RayL ray_L(double A2, double L) {
   RayL r;
   r.L = L;
   r.LL = L * L;
@@ -288,14 +306,20 @@ struct Segment {
 // and on the device can differ by an ulp, so one endpoint is reused.
 // Natural log: the table-driven tlog() of airice_tlog.hpp (< 1 ulp, no division, IEEE special
 // values; its g++-compiled twin is the bit reference in tests/test_tlog.py).
-__device__ __forceinline__ double fast_log(double x) { return tlog(x); }
+__host__ __device__ __forceinline__ double fast_log(double x) { return tlog(x); }
 
 // log(a) - log(b) as one logarithm (identity (5)).  Fast path -- a, b and a/b positive and
 // within 2^+-1000, i.e. every ray except special values -- takes the quotient from v_rcp_f64
 // refined by two Newton steps and one residual correction (Markstein; the IEEE quotient in all
 // but rare last-bit cases) and the table log without its special-value handling.  Otherwise:
 // the IEEE division and the IEEE value of log(a) - log(b) (-inf - finite, finite - (-inf), NaN).
-__device__ __forceinline__ double log_ratio_fast(double a, double b, const double* tab, bool& ok) {
+__host__ __device__ __forceinline__ double log_ratio_fast(double a, double b, const double* tab, bool& ok) {
+#if !defined(__HIP_DEVICE_COMPILE__)
+  // host: the IEEE quotient, the same positive-normal test
+  const double qh = a / b;
+  ok = std::fpclassify(b) == FP_NORMAL && b > 0.0 && std::fpclassify(qh) == FP_NORMAL && qh > 0.0;
+  return tlog_lean(qh, tab);
+#else
   double y = __builtin_amdgcn_rcp(b);
   y = __builtin_fma(y, __builtin_fma(-b, y, 1.0), y);
   const double q0 = a * y;
@@ -307,16 +331,17 @@ __device__ __forceinline__ double log_ratio_fast(double a, double b, const doubl
   // with b > 0 and q > 0 also a > 0
   ok = __builtin_amdgcn_class(b, 1 << 8) && __builtin_amdgcn_class(q, 1 << 8);
   return tlog_lean(q, tab);  // garbage, and unused, when !ok
+#endif
 }
 
-__device__ __forceinline__ double log_ratio_ieee(double a, double b) {
+__host__ __device__ __forceinline__ double log_ratio_ieee(double a, double b) {
   const double special = (a == 0.0 && b > 0.0)   ? -__builtin_inf()
                          : (b == 0.0 && a > 0.0) ? __builtin_inf()
                                                  : __builtin_nan("");
   return (a > 0.0 && b > 0.0) ? tlog(a / b) : special;
 }
 
-__device__ __forceinline__ double log_ratio(double a, double b,
+__host__ __device__ __forceinline__ double log_ratio(double a, double b,
                                             const double* tab = &kLogTable[0][0]) {
   bool ok;
   const double r = log_ratio_fast(a, b, tab, ok);
@@ -326,7 +351,7 @@ __device__ __forceinline__ double log_ratio(double a, double b,
 
 // The two log-ratios of a segment: both fast paths straight-line (so their table loads and
 // polynomials overlap), then one rarely taken branch for special values.
-__device__ __forceinline__ void log_ratio2(double a1, double b1, double a2, double b2,
+__host__ __device__ __forceinline__ void log_ratio2(double a1, double b1, double a2, double b2,
                                            const double* tab, double& d1, double& d2) {
   bool ok1, ok2;
   d1 = log_ratio_fast(a1, b1, tab, ok1);
@@ -337,7 +362,7 @@ __device__ __forceinline__ void log_ratio2(double a1, double b1, double a2, doub
   }
 }
 
-__device__ __forceinline__ Segment segment(const Endpoint& T, const Endpoint& R_, double A,
+__host__ __device__ __forceinline__ Segment segment(const Endpoint& T, const Endpoint& R_, double A,
                                            double A2, const RayL& RL, bool air,
                                            const double* tab = &kLogTable[0][0]) {
   const double speedc = 299792458.0;
@@ -366,7 +391,7 @@ __device__ __forceinline__ Segment segment(const Endpoint& T, const Endpoint& R_
 
 // Segment with both ends folded on the host (SegConst), identity (5).  sin_in is the sine of
 // the incidence inside the start end (sin(lang)); returns the sine of the receive angle.
-__device__ __forceinline__ Segment segment_const(const SegConst& S, double A, double A2, double sin_in,
+__host__ __device__ __forceinline__ Segment segment_const(const SegConst& S, double A, double A2, double sin_in,
                                                  bool air, double& v_out,
                                                  const double* tab = &kLogTable[0][0]) {
   const double v2 = sin_asin(S.ratio * sin_in);
@@ -389,7 +414,7 @@ __device__ __forceinline__ Segment segment_const(const SegConst& S, double A, do
 }
 
 // Layer-skip scans (.cc:1798-1825): top = MaxLayers-SkipLayersAbove-1, bottom = SkipLayersBelow.
-__device__ __forceinline__ int top_layer(const DevMedium& M, double txh) {
+__host__ __device__ __forceinline__ int top_layer(const DevMedium& M, double txh) {
   int skip = 0;
   for (int il = M.ml; il > -1; il--) {
     const bool hit = (txh < sel5(M.atm, il)) && (il >= 1 ? (txh >= sel5(M.atm, il - 1)) : false);
@@ -399,7 +424,7 @@ __device__ __forceinline__ int top_layer(const DevMedium& M, double txh) {
   return M.ml - skip - 1;
 }
 
-__device__ __forceinline__ int bottom_layer(const DevMedium& M, double ice_h) {
+__host__ __device__ __forceinline__ int bottom_layer(const DevMedium& M, double ice_h) {
   int skip = 0;
   for (int il = 0; il < M.ml; il++) {
     if (ice_h >= sel5(M.atm, il) && ice_h < sel5(M.atm, il + 1)) break;
@@ -409,7 +434,7 @@ __device__ __forceinline__ int bottom_layer(const DevMedium& M, double ice_h) {
 }
 
 // Fresnel amplitude transmission (.cc:285-337), thetai in radians.
-__device__ __forceinline__ void fresnel_trans(double n1, double n2, double thetai, double& tS,
+__host__ __device__ __forceinline__ void fresnel_trans(double n1, double n2, double thetai, double& tS,
                                               double& tP) {
   const double st = sin(thetai), ct = cos(thetai);
   const double a = (n1 / n2) * st;

@@ -28,6 +28,8 @@ int launch_table_multi(const DevMedium& M, const IceConsts* Ih, const airice_gri
 void table_cache_stats(int out[6]);
 int launch_rays(const DevMedium& M, const IceConsts& I, const double* launch, const double* txh,
                 int in_ice, size_t n, double* out, size_t ld, hipStream_t st);
+void rays_host(const DevMedium& M, const IceConsts& I, const double* launch, const double* txh,
+               int in_ice, size_t n, double* out, size_t ld);
 int launch_solve(const DevMedium& M, const IceConsts& I, int variant, const double* txh,
                  const double* dist, const double* depth, const double* thr, size_t n,
                  double* out, size_t ld, uint8_t* status, hipStream_t st);
@@ -57,6 +59,13 @@ int launch_single_ray(const DevMedium& M, const airice_medium* m, double depth, 
                       size_t cap, hipStream_t st);
 // RayTracingFunctions:: scalar layer (airice_rtf.hip): one call, one lane, d_out >= outputs
 int rtf_outputs(int op, int max_layers);
+int rtf_host(const DevMedium& M, int op, const double* args, size_t n_args, double* out);
+// one-query calls on the host (airice_runtime.cpp): the mode, and per-thread cached folds
+bool scalar_on_host();
+int set_scalar_mode(int mode);
+int folded_medium(const airice_medium* m, int variant, const DevMedium** out);
+int folded_ice(const airice_medium* m, int variant, double ice_h, double rx_depth,
+               const DevMedium** M, const IceConsts** I);
 int launch_rtf(const DevMedium& M, int op, const double* args, size_t n_args, double* d_out,
                hipStream_t st);
 int launch_trace(const DevMedium& M, const IceConsts& I, const double* depth, const double* ice,

@@ -63,7 +63,7 @@ constexpr long long kMaxLaunchRays = 1LL << 30;
 // The layer loop follows the reference (each layer re-derives L from the incidence angle
 // it receives, .cc:1871) with the running sine of identity (2).
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ Endpoint stop_of(const DevMedium& M, int l) {
+__host__ __device__ __forceinline__ Endpoint stop_of(const DevMedium& M, int l) {
   Endpoint r = M.stop[0];
   r = pick(l == 1, M.stop[1], r);
   r = pick(l == 2, M.stop[2], r);
@@ -75,7 +75,7 @@ __device__ __forceinline__ Endpoint stop_of(const DevMedium& M, int l) {
 // sin(asin(v) r2d d2r) = v, cos = sqrt(1 - v^2) on [0, 90] degrees).
 // ratio = n1 / n2 (folded on the host, IceConsts::n_ratio).  The two quotients have positive
 // denominators (n1, n2 > 0 and ct, sqterm >= 0, never both 0): div_pos.
-__device__ __forceinline__ void fresnel_from_sine(double n1, double n2, double ratio, double v,
+__host__ __device__ __forceinline__ void fresnel_from_sine(double n1, double n2, double ratio, double v,
                                                   double& tS, double& tP) {
   const double st = v, ct = fast_sqrt(1 - v * v);
   const double a = ratio * st;
@@ -83,19 +83,21 @@ __device__ __forceinline__ void fresnel_from_sine(double n1, double n2, double r
   double num = n1 * ct - n2 * sqterm;
   double den = n1 * ct + n2 * sqterm;
   tS = 1 + div_pos(num, den);
-  if (isnan(tS)) tS = 0;
+  if (__builtin_isnan(tS)) tS = 0;
   num = n1 * sqterm - n2 * ct;
   den = n1 * sqterm + n2 * ct;
   tP = (1 - div_pos(num, den)) * ratio;
-  if (isnan(tP)) tP = 0;
+  if (__builtin_isnan(tP)) tP = 0;
 }
 
 // Stop end of the Tx layer `top`.  Rays of one wave almost always share their Tx layer (a
 // wave covers <= 2 table rows), so the entry is read with a wave-uniform (scalar) index;
 // a wave that straddles a layer boundary falls back to per-lane selects.
-__device__ __forceinline__ TopEnd topend_of(const IceConsts& I, int top) {
+__host__ __device__ __forceinline__ TopEnd topend_of(const IceConsts& I, int top) {
+#if defined(__HIP_DEVICE_COMPILE__)
   const int tu = __builtin_amdgcn_readfirstlane(top);
   if (__ballot(top != tu) == 0) return I.topend[tu];
+#endif
   TopEnd r = I.topend[0];
 #pragma unroll
   for (int l = 1; l < kMaxLayers; ++l) {
@@ -117,7 +119,7 @@ struct RowConst {
   int any;       // top >= bot: at least one air layer
 };
 
-__device__ __forceinline__ RowConst row_const(const DevMedium& M, const IceConsts& I, double H) {
+__host__ __device__ __forceinline__ RowConst row_const(const DevMedium& M, const IceConsts& I, double H) {
   RowConst rc;
   rc.H = H;
   rc.top = top_layer(M, H);
@@ -144,7 +146,7 @@ __device__ __forceinline__ RowConst row_const(const DevMedium& M, const IceConst
 // sin(x) for the start angle's radians, x = (180 - theta) pi/180 in [0, pi/2] for every launch
 // angle in [90, 180]: odd Taylor polynomial to x^23 (truncation < 2^-59 relative on the range);
 // other arguments go to ocml's sin.
-__device__ __forceinline__ double sin_start(double x) {
+__host__ __device__ __forceinline__ double sin_start(double x) {
   if (!(x >= 0.0 && x <= 1.5707963267948966)) return sin(x);
   const double x2 = x * x;
   // (-1)^k / (2k+1)!, k = 11 .. 1, as doubles
@@ -162,7 +164,7 @@ __device__ __forceinline__ double sin_start(double x) {
 }
 
 // I.lower[il].ratio for a lane-varying il (selects)
-__device__ __forceinline__ double sel_lower_ratio(const IceConsts& I, int il) {
+__host__ __device__ __forceinline__ double sel_lower_ratio(const IceConsts& I, int il) {
   double r = I.lower[0].ratio;
 #pragma unroll
   for (int l = 1; l < kMaxLayers; ++l) r = (il == l) ? I.lower[l].ratio : r;
@@ -178,7 +180,7 @@ __device__ __forceinline__ double sel_lower_ratio(const IceConsts& I, int il) {
 // A1: the launch's A_air is exactly 1 (MultiRayAirIceRefraction.h:99, the table's medium), so
 // the products with it are dropped (exact: x * 1.0 == x).
 template <bool A1 = false>
-__device__ __forceinline__ void ray_solution_row(const DevMedium& M, const IceConsts& I,
+__host__ __device__ __forceinline__ void ray_solution_row(const DevMedium& M, const IceConsts& I,
                                                  const RowConst& rc, double theta, bool in_ice,
                                                  double* d, bool want_inc,
                                                  const double* tab = &kLogTable[0][0],
@@ -261,7 +263,7 @@ __device__ __forceinline__ void ray_solution_row(const DevMedium& M, const IceCo
 }
 
 // Per-lane form (rays, minimizer evaluations): the row constants of its own Tx height.
-__device__ __forceinline__ void ray_solution(const DevMedium& M, const IceConsts& I, double theta,
+__host__ __device__ __forceinline__ void ray_solution(const DevMedium& M, const IceConsts& I, double theta,
                                              double H, bool in_ice, double* d,
                                              bool want_inc = true) {
   const RowConst rc = row_const(M, I, H);
@@ -2818,6 +2820,20 @@ int launch_rays(const DevMedium& M, const IceConsts& I, const double* launch, co
   hipLaunchKernelGGL(rays_kernel, dim3(grid_for((long long)n)), dim3(kBlock), 0, st, M, I, launch,
                      txh, in_ice, (long long)n, out, ld, Signal{});
   return launch_ok();
+}
+
+// The one-query GetRayTracingSolutions on the host (airice_rays_host): ray_solution compiled for
+// the CPU from the same source as rays_kernel -- the same operation sequence, with the host's
+// correctly rounded sqrt and quotients in place of the device's v_rsq/v_rcp iterations (within
+// ~1 ulp of them).  A one-ray launch costs a kernel dispatch and a completion wait (~8 us); the
+// host ray takes ~1 us.
+void rays_host(const DevMedium& M, const IceConsts& I, const double* launch, const double* txh,
+               int in_ice, size_t n, double* out, size_t ld) {
+  for (size_t k = 0; k < n; ++k) {
+    double d[18];
+    ray_solution(M, I, launch[k], txh[k], in_ice != 0, d);
+    for (int c = 0; c < 18; ++c) out[c * ld + k] = d[c];
+  }
 }
 
 int launch_solve(const DevMedium& M, const IceConsts& I, int variant, const double* txh,

@@ -24,7 +24,7 @@ namespace {
 constexpr double kSpeedC = 299792458.0;  // RayTracingFunctions.h spedc
 
 // GetB_air / GetC_air layer scan (RayTracingFunctions.cc:172-213)
-__device__ int rtf_layer(const DevMedium& M, double z) {
+__host__ __device__ int rtf_layer(const DevMedium& M, double z) {
   const double zabs = fabs(z);
   int which = 0;
   for (int il = 0; il < M.ml - 1; il++) {
@@ -36,34 +36,34 @@ __device__ int rtf_layer(const DevMedium& M, double z) {
   if (zabs >= M.atm[M.ml - 1]) which = M.ml - 1;
   return which;
 }
-__device__ double rtf_B_air(const DevMedium& M, double z) { return M.B[rtf_layer(M, z)]; }
-__device__ double rtf_C_air(const DevMedium& M, double z) { return -M.negC[rtf_layer(M, z)]; }
+__host__ __device__ double rtf_B_air(const DevMedium& M, double z) { return M.B[rtf_layer(M, z)]; }
+__host__ __device__ double rtf_C_air(const DevMedium& M, double z) { return -M.negC[rtf_layer(M, z)]; }
 // Getnz_air (.cc:215-220), Getnz_ice (.cc:144-147)
-__device__ double rtf_nz_air(const DevMedium& M, double z) {
+__host__ __device__ double rtf_nz_air(const DevMedium& M, double z) {
   const double zabs = fabs(z);
   return M.A_air + rtf_B_air(M, zabs) * exp(-rtf_C_air(M, zabs) * zabs);
 }
-__device__ double rtf_nz_ice(const DevMedium& M, double z) {
+__host__ __device__ double rtf_nz_ice(const DevMedium& M, double z) {
   z = fabs(z);
   return M.A_ice + M.B_ice * exp(M.negC_ice * z);
 }
-__device__ double rtf_B(const DevMedium& M, double z, int air) { return air ? rtf_B_air(M, z) : M.B_ice; }
-__device__ double rtf_C(const DevMedium& M, double z, int air) {
+__host__ __device__ double rtf_B(const DevMedium& M, double z, int air) { return air ? rtf_B_air(M, z) : M.B_ice; }
+__host__ __device__ double rtf_C(const DevMedium& M, double z, int air) {
   return air ? rtf_C_air(M, z) : -M.negC_ice;
 }
-__device__ double rtf_nz(const DevMedium& M, double z, int air) {
+__host__ __device__ double rtf_nz(const DevMedium& M, double z, int air) {
   return air ? rtf_nz_air(M, z) : rtf_nz_ice(M, z);
 }
 
 // fDnfR (.cc:293-303)
-__device__ double rtf_fDnfR(double x, double A, double B, double C, double L) {
+__host__ __device__ double rtf_fDnfR(double x, double A, double B, double C, double L) {
   const double y = A + B * exp(C * x);
   return (L / C) * (1.0 / sqrt(A * A - L * L)) *
          (C * x - log(A * (A + B * exp(C * x)) - L * L + sqrt(A * A - L * L) * sqrt(y * y - L * L)));
 }
 
 // ftimeD (.cc:328-347); B is not used by the reference's formula
-__device__ double rtf_ftimeD(const DevMedium& M, double x, double A, double C, double Speedc,
+__host__ __device__ double rtf_ftimeD(const DevMedium& M, double x, double A, double C, double Speedc,
                              double L, int air) {
   const double n = rtf_nz(M, x, air);
   const double n2 = n * n;  // pow(Getnz(x), 2)
@@ -75,7 +75,7 @@ __device__ double rtf_ftimeD(const DevMedium& M, double x, double A, double C, d
 }
 
 // GetRayOpticalPath (.cc:349-369): the horizontal distance between two heights
-__device__ double rtf_optical_path(const DevMedium& M, double A, double Rx, double Tx, double L,
+__host__ __device__ double rtf_optical_path(const DevMedium& M, double A, double Rx, double Tx, double L,
                                    int air) {
   double x1 = +rtf_fDnfR(Rx, A, rtf_B(M, Rx, air), -rtf_C(M, Rx, air), L) -
               rtf_fDnfR(Tx, A, rtf_B(M, Tx, air), -rtf_C(M, Tx, air), L);
@@ -84,7 +84,7 @@ __device__ double rtf_optical_path(const DevMedium& M, double A, double Rx, doub
 }
 
 // GetRayPropagationTime (.cc:371-397)
-__device__ double rtf_prop_time(const DevMedium& M, double A, double Rx, double Tx, double L,
+__host__ __device__ double rtf_prop_time(const DevMedium& M, double A, double Rx, double Tx, double L,
                                 int air) {
   double t = +rtf_ftimeD(M, Rx, A, -rtf_C(M, Rx, air), kSpeedC, L, air) -
              rtf_ftimeD(M, Tx, A, -rtf_C(M, Tx, air), kSpeedC, L, air);
@@ -93,7 +93,7 @@ __device__ double rtf_prop_time(const DevMedium& M, double A, double Rx, double 
 }
 
 // The Snell part of GetLayerHitPointPar (.cc:399-454): the receive angle (radians) and L.
-__device__ void rtf_hit_L(const DevMedium& M, double n_layer1, double Rx, double Tx,
+__host__ __device__ void rtf_hit_L(const DevMedium& M, double n_layer1, double Rx, double Tx,
                           double IncidentAng, int air, double& ReceiveAngle, double& Lvalue) {
   const double SurfaceRayIncidentAngle = IncidentAng * M.d2r;
   const double nzRx = rtf_nz(M, Rx, air);
@@ -104,7 +104,7 @@ __device__ void rtf_hit_L(const DevMedium& M, double n_layer1, double Rx, double
 }
 
 // GetLayerHitPointPar (.cc:399-527): {x1, ReceiveAngle (deg), L, time}
-__device__ void rtf_hit_point(const DevMedium& M, double n_layer1, double Rx, double Tx,
+__host__ __device__ void rtf_hit_point(const DevMedium& M, double n_layer1, double Rx, double Tx,
                               double IncidentAng, int air, double out[4]) {
   const double A = air ? M.A_air : M.A_ice;
   double ReceiveAngle, Lvalue;
@@ -116,7 +116,7 @@ __device__ void rtf_hit_point(const DevMedium& M, double n_layer1, double Rx, do
 }
 
 // Layer-skip scans of GetAirPropagationPar (.cc:531-559)
-__device__ int rtf_skip_above(const DevMedium& M, double txh) {
+__host__ __device__ int rtf_skip_above(const DevMedium& M, double txh) {
   int skip = 0;
   for (int il = M.ml; il > -1; il--) {
     // ATMLAY[il-1] is read only when txh < ATMLAY[il]/100 (at il = 0 that is txh < 0)
@@ -125,7 +125,7 @@ __device__ int rtf_skip_above(const DevMedium& M, double txh) {
   }
   return skip;
 }
-__device__ int rtf_skip_below(const DevMedium& M, double ice) {
+__host__ __device__ int rtf_skip_below(const DevMedium& M, double ice) {
   int skip = 0;
   for (int il = 0; il < M.ml; il++) {
     if (ice >= M.atm[il] && ice < M.atm[il + 1]) il = 100;
@@ -136,7 +136,7 @@ __device__ int rtf_skip_below(const DevMedium& M, double ice) {
 
 // GetAirPropagationPar (.cc:529-659): out[4*MaxLayers + 1], per layer {THD, Recv, L, t}, count
 // at [4*MaxLayers]
-__device__ int rtf_air_prop(const DevMedium& M, double LaunchAngleAir, double AirTxHeight,
+__host__ __device__ int rtf_air_prop(const DevMedium& M, double LaunchAngleAir, double AirTxHeight,
                             double IceLayerHeight, double* out) {
   const int SkipLayersAbove = rtf_skip_above(M, AirTxHeight);
   const int SkipLayersBelow = rtf_skip_below(M, IceLayerHeight);
@@ -170,7 +170,7 @@ __device__ int rtf_air_prop(const DevMedium& M, double LaunchAngleAir, double Ai
 }
 
 // GetIcePropagationPar (.cc:661-681)
-__device__ void rtf_ice_prop(const DevMedium& M, double AntennaDepth, double Lvalue,
+__host__ __device__ void rtf_ice_prop(const DevMedium& M, double AntennaDepth, double Lvalue,
                              double out[4]) {
   const double nzStopDepth = rtf_nz_ice(M, AntennaDepth);
   out[0] = rtf_optical_path(M, M.A_ice, AntennaDepth, 0.0, Lvalue, 0);
@@ -180,7 +180,7 @@ __device__ void rtf_ice_prop(const DevMedium& M, double AntennaDepth, double Lva
 }
 
 // MinimizeforLaunchAngle (.cc:683-731)
-__device__ double rtf_min_launch(const DevMedium& M, double x, double AirTxHeight,
+__host__ __device__ double rtf_min_launch(const DevMedium& M, double x, double AirTxHeight,
                                  double IceLayerHeight, double AntennaDepth, double D) {
   double air[4 * kMaxLayers + 1];
   const int nf = rtf_air_prop(M, x, AirTxHeight, IceLayerHeight, air);
@@ -213,7 +213,7 @@ struct RtfBrent {
 };
 
 template <class F>
-__device__ RtfBrent gsl_brent(F f, double x_lo, double x_hi, double tolerance, int max_iter) {
+__host__ __device__ RtfBrent gsl_brent(F f, double x_lo, double x_hi, double tolerance, int max_iter) {
   const double kEps = 2.2204460492503131e-16;  // GSL_DBL_EPSILON
   RtfBrent R{0.0, 0, 0};
   if (x_lo > x_hi) {
@@ -225,10 +225,10 @@ __device__ RtfBrent gsl_brent(F f, double x_lo, double x_hi, double tolerance, i
   double a = 0, b = 0, c = 0, d = 0, e = 0, fa = 0, fb = 0, fc = 0;
   const double f_lower = f(x_lo);
   double f_upper = 0;
-  bool ok = isfinite(f_lower);
+  bool ok = __builtin_isfinite(f_lower);
   if (ok) {
     f_upper = f(x_hi);
-    ok = isfinite(f_upper);
+    ok = __builtin_isfinite(f_upper);
   }
   if (!ok) {
     R.status |= AIRICE_SOLVE_NONFINITE_END;
@@ -313,7 +313,7 @@ __device__ RtfBrent gsl_brent(F f, double x_lo, double x_hi, double tolerance, i
       else
         lb += (m > 0 ? +tol : -tol);
       const double fnew = f(lb);
-      if (!isfinite(fnew)) {
+      if (!__builtin_isfinite(fnew)) {
         R.status |= AIRICE_SOLVE_STALE_MID;
       } else {
         lfb = fnew;
@@ -347,7 +347,7 @@ __device__ RtfBrent gsl_brent(F f, double x_lo, double x_hi, double tolerance, i
 }
 
 // Air2IceRayTracing CLI solve (Air2IceRayTracing.C:56-185; StoreRayPath is false there).
-__device__ void rtf_air2ice(const DevMedium& M, double AirTxHeight, double HorizontalDistance,
+__host__ __device__ void rtf_air2ice(const DevMedium& M, double AirTxHeight, double HorizontalDistance,
                             double IceLayerHeight, double AntennaDepth, double* o) {
   const double StraightAngle =
       180 - (atan(HorizontalDistance / (AirTxHeight - IceLayerHeight + AntennaDepth)) * M.r2d);
@@ -362,7 +362,7 @@ __device__ void rtf_air2ice(const DevMedium& M, double AirTxHeight, double Horiz
       const int nf = rtf_air_prop(M, startanglelim, AirTxHeight, IceLayerHeight, air);
       double thd = 0;
       for (int i = 0; i < nf; i++) thd += air[i * 4];
-      if ((!isnan(thd) && thd > 0) || startanglelim > endanglelim - 1) {
+      if ((!__builtin_isnan(thd) && thd > 0) || startanglelim > endanglelim - 1) {
         checknan = true;
       } else {
         startanglelim = startanglelim + 0.05;
@@ -411,7 +411,7 @@ __device__ void rtf_air2ice(const DevMedium& M, double AirTxHeight, double Horiz
 // expressions plus the geometric path, 5-wide outputs {THD, Recv deg, L, t, geo} ----------------
 
 // fpathD (.cc:434-447), the reference's expression
-__device__ double mr_fpathD(double x, double A, double B, double C, double L) {
+__host__ __device__ double mr_fpathD(double x, double A, double B, double C, double L) {
   return (log((A + B * exp(C * x)) *
               (sqrt((A * A + 2 * A * B * exp(C * x) + B * B * exp(2 * C * x) - L * L) /
                     ((A + B * exp(C * x)) * (A + B * exp(C * x)))) +
@@ -429,7 +429,7 @@ __device__ double mr_fpathD(double x, double A, double B, double C, double L) {
 }
 
 // GetRayGeometricPath (.cc:494-513)
-__device__ double mr_geo_path(const DevMedium& M, double A, double Rx, double Tx, double L,
+__host__ __device__ double mr_geo_path(const DevMedium& M, double A, double Rx, double Tx, double L,
                               int air) {
   double g = mr_fpathD(Rx, A, rtf_B(M, Rx, air), -rtf_C(M, Rx, air), L) -
              mr_fpathD(Tx, A, rtf_B(M, Tx, air), -rtf_C(M, Tx, air), L);
@@ -438,7 +438,7 @@ __device__ double mr_geo_path(const DevMedium& M, double A, double Rx, double Tx
 }
 
 // GetLayerHitPointPar (.cc:521-646): {x1, ReceiveAngle (deg), L, time, x1_Geo}
-__device__ void mr_hit_point(const DevMedium& M, double n_layer1, double Rx, double Tx,
+__host__ __device__ void mr_hit_point(const DevMedium& M, double n_layer1, double Rx, double Tx,
                              double IncidentAng, int air, double out[5]) {
   rtf_hit_point(M, n_layer1, Rx, Tx, IncidentAng, air, out);
   out[4] = mr_geo_path(M, air ? M.A_air : M.A_ice, Rx, Tx, out[2], air);
@@ -447,7 +447,7 @@ __device__ void mr_hit_point(const DevMedium& M, double n_layer1, double Rx, dou
 // GetAirPropagationPar (.cc:661-804): out[5*MaxLayers + 2], per layer {THD, Recv, L, t, geo},
 // the filled-layer count at [5*MaxLayers+1] ([5*MaxLayers] is never written by the reference;
 // 0 here)
-__device__ int mr_air_prop(const DevMedium& M, double LaunchAngleAir, double AirTxHeight,
+__host__ __device__ int mr_air_prop(const DevMedium& M, double LaunchAngleAir, double AirTxHeight,
                            double IceLayerHeight, double* out) {
   const int SkipLayersAbove = rtf_skip_above(M, AirTxHeight);
   const int SkipLayersBelow = rtf_skip_below(M, IceLayerHeight);
@@ -482,14 +482,14 @@ __device__ int mr_air_prop(const DevMedium& M, double LaunchAngleAir, double Air
 }
 
 // GetIcePropagationPar (.cc:807-869), TransitionBoundary == 0 (.h:70)
-__device__ void mr_ice_prop(const DevMedium& M, double AntennaDepth, double Lvalue,
+__host__ __device__ void mr_ice_prop(const DevMedium& M, double AntennaDepth, double Lvalue,
                             double out[5]) {
   rtf_ice_prop(M, AntennaDepth, Lvalue, out);
   out[4] = mr_geo_path(M, M.A_ice, AntennaDepth, 0.0, Lvalue, 0);
 }
 
 // MinimizeforLaunchAngle (.cc:873-917)
-__device__ double mr_min_launch(const DevMedium& M, double x, double AirTxHeight,
+__host__ __device__ double mr_min_launch(const DevMedium& M, double x, double AirTxHeight,
                                 double IceLayerHeight, double AntennaDepth, double D) {
   double air[5 * kMaxLayers + 2];
   const int nf = mr_air_prop(M, x, AirTxHeight, IceLayerHeight, air);
@@ -626,10 +626,17 @@ __device__ double min_launch_wave(const DevMedium& M, double x, double AirTxHeig
   return D - (thd_ice + thd_air);
 }
 
+}  // namespace
+
 struct RtfCall {
   int op, n_out;
   double a[8];
 };
+constexpr int kRtfMaxOut = AIRICE_RTF_AIR2ICE_FIELDS > 5 * kMaxLayers + 2 ? AIRICE_RTF_AIR2ICE_FIELDS
+                                                                         : 5 * kMaxLayers + 2;
+__host__ __device__ void rtf_eval_one(const DevMedium& M, const RtfCall& c, double* r);
+
+namespace {
 
 __global__ void rtf_kernel(DevMedium M, RtfCall c, double* __restrict__ out, Signal sig) {
   prefetch_kernargs<sizeof(DevMedium) + sizeof(RtfCall)>();
@@ -654,9 +661,18 @@ __global__ void rtf_kernel(DevMedium M, RtfCall c, double* __restrict__ out, Sig
     return;
   }
   if (threadIdx.x != 0 || blockIdx.x != 0) return;
-  double r[AIRICE_RTF_AIR2ICE_FIELDS > 5 * kMaxLayers + 2 ? AIRICE_RTF_AIR2ICE_FIELDS
-                                                         : 5 * kMaxLayers + 2];
-  for (int i = 0; i < (int)(sizeof(r) / sizeof(r[0])); i++) r[i] = 0;
+  double r[kRtfMaxOut];
+  rtf_eval_one(M, c, r);
+  for (int i = 0; i < c.n_out; i++) out[i] = r[i];
+  signal_done(sig);
+}
+
+}  // namespace
+
+// One call of any op on one lane (the kernel's lane 0 and the host form, rtf_host): r receives
+// kRtfMaxOut values, zeros past the op's outputs.
+__host__ __device__ void rtf_eval_one(const DevMedium& M, const RtfCall& c, double* r) {
+  for (int i = 0; i < kRtfMaxOut; i++) r[i] = 0;
   switch (c.op) {
     case AIRICE_RTF_HIT_POINT:
       rtf_hit_point(M, c.a[0], c.a[1], c.a[2], c.a[3], (int)c.a[4], r);
@@ -706,11 +722,7 @@ __global__ void rtf_kernel(DevMedium M, RtfCall c, double* __restrict__ out, Sig
     default:
       break;
   }
-  for (int i = 0; i < c.n_out; i++) out[i] = r[i];
-  signal_done(sig);
 }
-
-}  // namespace
 
 int rtf_outputs(int op, int max_layers) {
   switch (op) {
@@ -739,6 +751,21 @@ int rtf_outputs(int op, int max_layers) {
     default:
       return -1;
   }
+}
+
+// The one call on the host (airice_rtf_eval's default for these one-query entry points): the
+// same expressions compiled for the CPU (the host's libm in place of ocml: the same functions to
+// within an ulp or so), with no kernel dispatch and completion wait (~8 us of a GPU call).
+int rtf_host(const DevMedium& M, int op, const double* args, size_t n_args, double* out) {
+  RtfCall c;
+  c.op = op;
+  c.n_out = rtf_outputs(op, M.ml);
+  if (c.n_out < 0) return AIRICE_EINVAL;
+  for (int i = 0; i < 8; i++) c.a[i] = (size_t)i < n_args ? args[i] : 0.0;
+  double r[kRtfMaxOut];
+  rtf_eval_one(M, c, r);
+  for (int i = 0; i < c.n_out; i++) out[i] = r[i];
+  return AIRICE_OK;
 }
 
 int launch_rtf(const DevMedium& M, int op, const double* args, size_t n_args, double* d_out,

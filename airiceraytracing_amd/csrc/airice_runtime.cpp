@@ -123,6 +123,72 @@ void build_ice_consts(const DevMedium& M, double ice_h, double rx_depth, IceCons
   out->iceseg = make_segconst(out->ice0, rx);
 }
 
+// ---- one-query calls on the host ---------------------------------------------------------
+// Where the one-query ray and ray-layer calls run (airice_scalar_mode): AIRICE_SCALAR_HOST (the
+// default) or AIRICE_SCALAR_DEVICE (the one-wave kernels through the scalar slot); the environment
+// variable AIRICE_SCALAR=device sets the initial mode.
+static std::atomic<int> g_scalar_mode{-1};
+int set_scalar_mode(int mode) {
+  int prev = g_scalar_mode.load();
+  if (prev < 0) prev = scalar_on_host() ? AIRICE_SCALAR_HOST : AIRICE_SCALAR_DEVICE;
+  if (mode == AIRICE_SCALAR_HOST || mode == AIRICE_SCALAR_DEVICE) g_scalar_mode.store(mode);
+  return prev;
+}
+bool scalar_on_host() {
+  int v = g_scalar_mode.load(std::memory_order_relaxed);
+  if (v < 0) {
+    const char* e = getenv("AIRICE_SCALAR");
+    v = (e != nullptr && std::strcmp(e, "device") == 0) ? AIRICE_SCALAR_DEVICE : AIRICE_SCALAR_HOST;
+    int expect = -1;
+    g_scalar_mode.compare_exchange_strong(expect, v);
+    v = g_scalar_mode.load();
+  }
+  return v == AIRICE_SCALAR_HOST;
+}
+
+// The host folds of the last medium (and ice height / antenna depth) a thread's one-query calls
+// used: a repeated call with the same medium skips build_dev_medium / build_ice_consts (~20
+// exponentials).  Keyed by the medium's bytes (the namespace data a drop-in call folds in).
+namespace {
+struct FoldCache {
+  airice_medium key{};
+  int variant = -1;
+  DevMedium M{};
+  bool have_i = false;
+  double ice = 0, rx = 0;
+  IceConsts I{};
+};
+thread_local FoldCache t_fold;
+}  // namespace
+
+int folded_medium(const airice_medium* m, int variant, const DevMedium** out) {
+  FoldCache& c = t_fold;
+  if (c.variant != variant || std::memcmp(&c.key, m, sizeof(*m)) != 0) {
+    c.variant = -1;
+    c.have_i = false;
+    if (int rc = build_dev_medium(m, variant, &c.M)) return rc;
+    c.key = *m;
+    c.variant = variant;
+  }
+  *out = &c.M;
+  return AIRICE_OK;
+}
+
+int folded_ice(const airice_medium* m, int variant, double ice_h, double rx_depth,
+               const DevMedium** M, const IceConsts** I) {
+  if (int rc = folded_medium(m, variant, M)) return rc;
+  FoldCache& c = t_fold;
+  if (!c.have_i || c.ice != ice_h || c.rx != rx_depth ||
+      (std::signbit(c.ice) != std::signbit(ice_h)) || (std::signbit(c.rx) != std::signbit(rx_depth))) {
+    build_ice_consts(c.M, ice_h, rx_depth, &c.I);
+    c.ice = ice_h;
+    c.rx = rx_depth;
+    c.have_i = true;
+  }
+  *I = &c.I;
+  return AIRICE_OK;
+}
+
 // ---- kernel timer (bench only) ---------------------------------------------------------
 std::atomic<bool> g_ktimer_on{false};
 static std::mutex g_kt_mu;
@@ -490,6 +556,26 @@ int airice_table_host(const airice_medium* m, const airice_grid* g, int32_t row_
   return rc;
 }
 
+int airice_rays_host(const airice_medium* m, const double* launch_deg, const double* txh,
+                     double ice_h_m, double depth_m, int32_t in_ice, size_t n, double* out,
+                     size_t ld) {
+  if (m == nullptr || out == nullptr || (n > 0 && (launch_deg == nullptr || txh == nullptr))) {
+    set_error("null argument");
+    return AIRICE_EINVAL;
+  }
+  if (ld < n) {
+    set_error("ld < n");
+    return AIRICE_EINVAL;
+  }
+  const DevMedium* M = nullptr;
+  const IceConsts* I = nullptr;
+  if (int rc = airice::folded_ice(m, AIRICE_VARIANT_MULTIRAY, ice_h_m, -depth_m, &M, &I)) return rc;
+  airice::rays_host(*M, *I, launch_deg, txh, in_ice, n, out, ld);
+  return AIRICE_OK;
+}
+
+int airice_scalar_mode(int mode) { return airice::set_scalar_mode(mode); }
+
 int airice_rays_launch(const airice_medium* m, const double* d_launch, const double* d_txh,
                        double ice_h_m, double depth_m, int32_t in_ice, size_t n, double* d_out,
                        size_t ld, void* stream) {
@@ -680,6 +766,28 @@ int airice_rtf_eval(const airice_medium* m, int op, const double* args, size_t n
 
 int airice_rtf_eval_variant(const airice_medium* m, int variant, int op, const double* args,
                             size_t n_args, double* out, size_t n_out) {
+  if (airice::scalar_on_host()) {
+    if (m == nullptr || out == nullptr || (n_args > 0 && args == nullptr)) {
+      set_error("null argument");
+      return AIRICE_EINVAL;
+    }
+    if (variant != AIRICE_VARIANT_MULTIRAY && variant != AIRICE_VARIANT_PYWRAPPER) {
+      set_error("unknown variant %d", variant);
+      return AIRICE_EINVAL;
+    }
+    const DevMedium* M = nullptr;
+    if (int rc = airice::folded_medium(m, variant, &M)) return rc;
+    const int need = airice::rtf_outputs(op, M->ml);
+    if (need < 0) {
+      set_error("unknown RayTracingFunctions op %d", op);
+      return AIRICE_EINVAL;
+    }
+    if (n_out < (size_t)need || n_args > 8) {
+      set_error("rtf op %d: %zu outputs (need %d), %zu args (max 8)", op, n_out, need, n_args);
+      return AIRICE_EINVAL;
+    }
+    return airice::rtf_host(*M, op, args, n_args, out);
+  }
   if (m == nullptr || out == nullptr || (n_args > 0 && args == nullptr)) {
     set_error("null argument");
     return AIRICE_EINVAL;

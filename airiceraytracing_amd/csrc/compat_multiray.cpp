@@ -393,6 +393,12 @@ void Air2IceRayTracing(double AirTxHeight, double HorizontalDistance, double Ice
 void GetRayTracingSolutions(double RayLaunchAngleInAir, double AirTxHeight, double IceLayerHeight,
                             double AntennaDepth, double dummy[20], bool& InIce) {
   const airice_medium m = medium();
+  if (airice_scalar_mode(-1) == AIRICE_SCALAR_HOST) {  // one ray: on the host (airice_rays_host)
+    if (airice_rays_host(&m, &RayLaunchAngleInAir, &AirTxHeight, IceLayerHeight, AntennaDepth,
+                         InIce ? 1 : 0, 1, dummy, 1) != AIRICE_OK)
+      die("GetRayTracingSolutions");
+    return;
+  }
   airice::ScalarCall call;
   if (!call.ok()) die("GetRayTracingSolutions");
   airice::ScalarSlot& s = call.slot();

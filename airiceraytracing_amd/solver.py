@@ -31,6 +31,23 @@ def make_grid(antenna_depth_cm: float, ice_height_cm: float, height_step: float 
     return g
 
 
+class scalar_mode:
+    """Where the one-query ray and ray-layer calls run (airice_scalar_mode), for a ``with`` block:
+    _lib.SCALAR_HOST (the library's default) or _lib.SCALAR_DEVICE."""
+
+    def __init__(self, mode: int):
+        self.mode = mode
+        self.prev = None
+
+    def __enter__(self):
+        self.prev = lib().airice_scalar_mode(self.mode)
+        return self
+
+    def __exit__(self, *exc):
+        lib().airice_scalar_mode(self.prev)
+        return False
+
+
 def _stream_handle(stream):
     if stream is None:
         return None
@@ -123,6 +140,17 @@ class AirIceSolver:
                                        ice_h, depth, int(in_ice), n, ptr(out),
                                        n if ld is None else ld, _stream_handle(stream)),
               "airice_rays_launch")
+
+    def rays_host(self, launch_deg, txh, ice_h: float, depth: float, in_ice: bool) -> np.ndarray:
+        """airice_rays_host: GetRayTracingSolutions for host arrays on the CPU (the one-query
+        drop-in's path, same source as the device kernels); (18, n) doubles."""
+        a = np.ascontiguousarray(launch_deg, dtype=np.float64).ravel()
+        h = np.ascontiguousarray(np.broadcast_to(txh, a.shape), dtype=np.float64).ravel()
+        out = np.empty((_lib.RAY_FIELDS, a.size), dtype=np.float64)
+        check(lib().airice_rays_host(ctypes.byref(self.medium), ptr(a), ptr(h), ice_h, depth,
+                                     int(in_ice), a.size, ptr(out), max(a.size, 1)),
+              "airice_rays_host")
+        return out
 
     # ------------------------------------------------------------------ minimizer
     def solve_device(self, txh, dist, depth, ice_h: float, out, status=None,
@@ -239,8 +267,9 @@ class AirIceSolver:
               "airice_trace_ice_to_air_launch")
 
     def rtf_eval(self, op: int, args) -> np.ndarray:
-        """One RayTracingFunctions:: scalar function on the GPU (AIRICE_RTF_*, include/airice.h),
-        in the reference's output layout."""
+        """One RayTracingFunctions:: scalar function (AIRICE_RTF_*, include/airice.h) where
+        scalar_mode() says -- the host by default, else the GPU -- in the reference's output
+        layout."""
         a = np.ascontiguousarray(args, dtype=np.float64)
         n = lib().airice_rtf_outputs(op, int(self.medium.max_layers))
         if n < 0:

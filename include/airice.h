@@ -145,6 +145,25 @@ int airice_rays_launch(const airice_medium *m, const double *d_launch_deg, const
                        double ice_h_m, double depth_m, int32_t in_ice, size_t n, double *d_out,
                        size_t ld, void *stream);
 
+/* The same rays on the host (CPU), from the same source as the device kernels with the host's
+ * correctly rounded sqrt and quotients (within ~1 ulp of the device's): the one-query
+ * GetRayTracingSolutions of the C++ drop-in runs here, ~1 us against a ~10 us kernel round trip.
+ * Host arrays; out: 18 double columns, stride ld. */
+int airice_rays_host(const airice_medium *m, const double *launch_deg, const double *txh,
+                     double ice_h_m, double depth_m, int32_t in_ice, size_t n, double *out,
+                     size_t ld);
+
+/* Where the one-query calls of the C++ drop-ins run -- GetRayTracingSolutions and the ray layer
+ * (airice_rtf_eval / _variant: RayTracingFunctions::, MultiRayAirIceRefraction:: and
+ * AirIceRayTracing:: fDnfR ... MinimizeforLaunchAngle): AIRICE_SCALAR_HOST (default) or
+ * AIRICE_SCALAR_DEVICE (a one-wave kernel per call).  The environment variable
+ * AIRICE_SCALAR=device selects the device at start.  Returns the previous mode; any other value
+ * only queries it.  One-query solves (Air2IceRayTracing, the CoREAS entry, Py_TraceIceToAir) and
+ * every batch entry point run on the device either way. */
+#define AIRICE_SCALAR_HOST 0
+#define AIRICE_SCALAR_DEVICE 1
+int airice_scalar_mode(int mode);
+
 /* --- minimizer (Air2IceRayTracing) --------------------------------------- */
 /* Batched launch-angle solve.  Inputs in metres: Tx height, horizontal distance, Rx
  * depth (negative = below the ice surface); ice height uniform.  d_straight_angle is
@@ -280,9 +299,10 @@ void Py_TraceIceToAir(double AntennaDepth, double IceLayerHeight, double AirTxHe
                       double HorizontalDistance, double ArrayParameters[10]);
 
 /* --- RayTracingFunctions:: scalar layer (RayTracingFunctions.cc, the cfg1 CLI's library) --- */
-/* One call evaluated on the device with the reference's expressions (pi 3.1415927); host
- * arguments and outputs, synchronous.  For the RayTracingFunctions.h drop-in
- * (include/RayTracingFunctions.h); batches belong on the table / solve / single-ray paths. */
+/* One call evaluated with the reference's expressions (pi 3.1415927) on the host, or on the
+ * device (airice_scalar_mode); host arguments and outputs, synchronous.  For the
+ * RayTracingFunctions.h drop-in (include/RayTracingFunctions.h); batches belong on the table /
+ * solve / single-ray paths. */
 #define AIRICE_RTF_HIT_POINT 0        /* GetLayerHitPointPar (.cc:399-527)
                                          args {n_layer1, RxDepth, TxDepth, IncidentAng, AirOrIce}
                                          -> {THD, ReceiveAngle deg, L, time s} */

@@ -103,11 +103,15 @@ def test_cpp_caller_against_oracle(tmp_path, oracle_medium):
 INNER = os.path.join(ROOT, "tests", "cpp", "multiray_inner_driver")
 
 
-def _run_driver(exe, tmp_path):
+def _run_driver(exe, tmp_path, scalar="host"):
+    """scalar: where the one-query ray and ray-layer calls run (AIRICE_SCALAR: the host by
+    default, or the one-wave device kernels)."""
     assert os.path.exists(exe), "build with __graft_entry__.build()"
     with open(ATMOSPHERE_GZ, "rb") as f:
         (tmp_path / "Atmosphere.dat").write_bytes(gzip.decompress(f.read()))
-    out = subprocess.run([exe], cwd=tmp_path, capture_output=True, text=True, timeout=120)
+    env = dict(os.environ, AIRICE_SCALAR=scalar)
+    out = subprocess.run([exe], cwd=tmp_path, capture_output=True, text=True, timeout=120,
+                         env=env)
     assert out.returncode == 0, out.stderr
     txt = re.sub(r"-?\b(nan|inf)\b", lambda mm: {"nan": "NaN", "-nan": "NaN", "inf": "Infinity",
                                                    "-inf": "-Infinity"}[mm.group(0)], out.stdout)
@@ -124,12 +128,14 @@ def _close(got, ref, rtol=1e-9, floor=1e-12):
 
 
 @pytest.mark.gpu
-def test_cpp_inner_api_against_oracle(tmp_path, oracle_medium):
+@pytest.mark.parametrize("scalar", ["host", "device"])
+def test_cpp_inner_api_against_oracle(tmp_path, oracle_medium, scalar):
     """Every MultiRayAirIceRefraction.h function of the reference (.h:84-204) driven by a C++
-    caller (tests/cpp/multiray_inner_driver.cpp): the ray layer on the GPU within 1e-9 of the
-    oracle, the table walks on the host bit for bit, the exported _Table (with its antenna remap)
-    bit-identical to the batched GPU lookup."""
-    r = _run_driver(INNER, tmp_path)
+    caller (tests/cpp/multiray_inner_driver.cpp): the ray layer -- on the host (the default for
+    one-query calls) and on the GPU (AIRICE_SCALAR=device) -- within 1e-9 of the oracle, the table
+    walks on the host bit for bit, the exported _Table (with its antenna remap) bit-identical to
+    the batched GPU lookup."""
+    r = _run_driver(INNER, tmp_path, scalar)
     m = oracle_medium
     ML = m.max_layers
     # namespace data

@@ -51,11 +51,14 @@ def _medium():
 
 
 @pytest.mark.gpu
-def test_rtf_cpp_caller(tmp_path):
+@pytest.mark.parametrize("scalar", ["host", "device"])
+def test_rtf_cpp_caller(tmp_path, scalar):
+    """The C++ caller with the one-query calls on the host (default) and on the GPU."""
     assert os.path.exists(DRIVER), "build with __graft_entry__.build()"
     with open(ATMOSPHERE_GZ, "rb") as f:
         (tmp_path / "Atmosphere.dat").write_bytes(gzip.decompress(f.read()))
-    out = subprocess.run([DRIVER], cwd=tmp_path, capture_output=True, text=True, timeout=120)
+    out = subprocess.run([DRIVER], cwd=tmp_path, capture_output=True, text=True, timeout=120,
+                         env=dict(os.environ, AIRICE_SCALAR=scalar))
     assert out.returncode == 0, out.stderr
     txt = re.sub(r"-?\bnan\b", "NaN", out.stdout)
     r = json.loads(txt)
@@ -91,10 +94,59 @@ def test_rtf_cpp_caller(tmp_path):
     assert abs(r["c_air_edit"][0] - (air[0] + air[4] + air[8])) > 1e-6
 
 
+def _rtf_cases(m, n=150, seed=3):
+    from airiceraytracing_amd import _lib
+    rng = np.random.default_rng(seed)
+    cases = []
+    for _ in range(n):
+        txh = rng.uniform(3001, 99000)
+        ice = rng.choice([3000.0, rng.uniform(0, 3500)])
+        la = rng.uniform(91, 180)
+        air = int(rng.integers(0, 2))
+        if air:
+            tx, rx = rng.uniform(0, 60000), rng.uniform(0, 60000)
+            n1 = oracle.getnz_air(m, tx) * rng.uniform(0.9999, 1.0001)
+        else:
+            tx, rx = -rng.uniform(0, 300), -rng.uniform(0, 300)
+            n1 = rng.uniform(1.0, 1.78)
+        L = rng.uniform(0, 1.0)
+        cases += [
+            (_lib.RTF_HIT_POINT, [n1, rx, tx, rng.uniform(0, 89.9), air]),
+            (_lib.RTF_AIR_PROPAGATION, [la, txh, ice]),
+            (_lib.RTF_MIN_LAUNCH, [la, txh, ice, rng.uniform(0, 300), rng.uniform(0, 50000)]),
+            (_lib.MR_AIR_PROPAGATION, [la, txh, ice]),
+            (_lib.MR_MIN_LAUNCH, [la, txh, ice, rng.uniform(0, 300), rng.uniform(0, 50000)]),
+        ]
+    return cases
+
+
 @pytest.mark.gpu
-def test_rtf_ops_random(oracle_medium):
+def test_host_matches_device(oracle_medium):
+    """The one-query ray layer on the host (the default) against the same op on the GPU: the same
+    expressions with the host's libm in place of ocml, so within a few ulps of each other."""
     from airiceraytracing_amd import AirIceSolver, _lib
+    from airiceraytracing_amd.solver import scalar_mode
     s = AirIceSolver()
+    worst = 0.0
+    for op, args in _rtf_cases(oracle_medium, 60, seed=8):
+        host = s.rtf_eval(op, args)
+        with scalar_mode(_lib.SCALAR_DEVICE):
+            dev = s.rtf_eval(op, args)
+        _close(host, dev, floor=1e-6, rtol=1e-12)
+        fin = np.isfinite(dev) & (np.abs(dev) > 1e-6)
+        if fin.any():
+            worst = max(worst, float(np.max(np.abs(host[fin] - dev[fin]) / np.abs(dev[fin]))))
+    assert worst < 1e-12, worst
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("scalar", ["host", "device"])
+def test_rtf_ops_random(oracle_medium, scalar):
+    from airiceraytracing_amd import AirIceSolver, _lib
+    from airiceraytracing_amd.solver import scalar_mode
+    s = AirIceSolver()
+    mode = scalar_mode(_lib.SCALAR_HOST if scalar == "host" else _lib.SCALAR_DEVICE)
+    mode.__enter__()
     m = oracle_medium
     rng = np.random.default_rng(3)
     n = 150
@@ -123,8 +175,11 @@ def test_rtf_ops_random(oracle_medium):
                                -rng.uniform(1e-4, 0.02), 299792458.0, L, air]),
             (_lib.RTF_MIN_LAUNCH, [la, txh, ice, rng.uniform(0, 300), rng.uniform(0, 50000)]),
         ]
-    for op, args in cases:
-        got = s.rtf_eval(op, args)
-        ref = oracle.rtf_eval(m, op, args)
-        floor = 1e-15 if op in (_lib.RTF_PROPAGATION_TIME, _lib.RTF_FTIMED) else 1e-6
-        _close(got, ref, floor=floor)
+    try:
+        for op, args in cases:
+            got = s.rtf_eval(op, args)
+            ref = oracle.rtf_eval(m, op, args)
+            floor = 1e-15 if op in (_lib.RTF_PROPAGATION_TIME, _lib.RTF_FTIMED) else 1e-6
+            _close(got, ref, floor=floor)
+    finally:
+        mode.__exit__()
