@@ -30,6 +30,14 @@ int launch_rays(const DevMedium& M, const IceConsts& I, const double* launch, co
                 int in_ice, size_t n, double* out, size_t ld, hipStream_t st);
 void rays_host(const DevMedium& M, const IceConsts& I, const double* launch, const double* txh,
                int in_ice, size_t n, double* out, size_t ld);
+// one query of the minimizer entry points on the host (airice_kernels.hip)
+int solve_host_one(const DevMedium& M, const IceConsts& I, int variant, const double* in,
+                   bool has_thr, double* out, uint8_t* status);
+int hdtip_host_one(const DevMedium& M, const IceConsts& I, double ice_cm, const double* in,
+                   double* out9, uint8_t* ok);
+int trace_host_one(const DevMedium& M, const IceConsts& I, const double* in, double* out10);
+int lookup_fallback_host_one(const DevMedium& M, const IceConsts& I, double ice_cm,
+                             const double* in, double* out9, uint8_t* ok, const uint8_t* flags);
 int launch_solve(const DevMedium& M, const IceConsts& I, int variant, const double* txh,
                  const double* dist, const double* depth, const double* thr, size_t n,
                  double* out, size_t ld, uint8_t* status, hipStream_t st);
@@ -66,6 +74,12 @@ int set_scalar_mode(int mode);
 int folded_medium(const airice_medium* m, int variant, const DevMedium** out);
 int folded_ice(const airice_medium* m, int variant, double ice_h, double rx_depth,
                const DevMedium** M, const IceConsts** I);
+// one query of a minimizer entry point on the host, from an airice_medium (folds cached)
+int solve_query_host(const airice_medium* m, int variant, double ice_h, const double* in,
+                     bool has_thr, double* out, uint8_t* status);
+int hdtip_query_host(const airice_medium* m, double ice_cm, const double* in, double* out9,
+                     uint8_t* ok);
+int trace_query_host(const airice_medium* m, const double* in, double* out10);
 int launch_rtf(const DevMedium& M, int op, const double* args, size_t n_args, double* d_out,
                hipStream_t st);
 int launch_trace(const DevMedium& M, const IceConsts& I, const double* depth, const double* ice,

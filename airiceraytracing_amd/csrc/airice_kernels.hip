@@ -649,7 +649,7 @@ struct AirPath {
 };
 
 
-__device__ __forceinline__ AirPath make_air_path(const DevMedium& M, double H, double ice) {
+__host__ __device__ __forceinline__ AirPath make_air_path(const DevMedium& M, double H, double ice) {
   AirPath P;
   P.top = top_layer(M, H);
   P.bot = bottom_layer(M, ice);
@@ -661,7 +661,7 @@ __device__ __forceinline__ AirPath make_air_path(const DevMedium& M, double H, d
 }
 
 // sin of the receive angle of the first layer (GetLayerHitPointPar .cc:562-589).
-__device__ __forceinline__ double first_layer_v2(const DevMedium& M, double n_tx, double n_rtop,
+__host__ __device__ __forceinline__ double first_layer_v2(const DevMedium& M, double n_tx, double n_rtop,
                                                  double theta) {
   const double v1 = sin_start((180 - theta) * M.d2r);
   return sin_asin((n_tx * sin_asin(v1)) / n_rtop);
@@ -672,15 +672,15 @@ struct Slim {
   double y2, Ay, Cx, invC;
 };
 
-__device__ __forceinline__ Slim slim(const Endpoint& p) { return Slim{p.y2, p.Ay, p.Cx, p.invC}; }
+__host__ __device__ __forceinline__ Slim slim(const Endpoint& p) { return Slim{p.y2, p.Ay, p.Cx, p.invC}; }
 
-__device__ __forceinline__ Slim pick(bool c, const Slim& a, const Slim& b) {
+__host__ __device__ __forceinline__ Slim pick(bool c, const Slim& a, const Slim& b) {
   return Slim{c ? a.y2 : b.y2, c ? a.Ay : b.Ay, c ? a.Cx : b.Cx, c ? a.invC : b.invC};
 }
 
 // Slim air endpoint at x >= 0 (Tx heights and ice heights are non-negative; a negative x
 // would need y(x) != n(|x|), handled by the full Endpoint path).
-__device__ __forceinline__ Slim air_slim(const DevMedium& M, double x, double& n) {
+__host__ __device__ __forceinline__ Slim air_slim(const DevMedium& M, double x, double& n) {
   const double zabs = fabs(x);
   const int l = air_layer(M, zabs);
   const double B = sel5(M.B, l), C = sel5(M.negC, l);
@@ -690,7 +690,7 @@ __device__ __forceinline__ Slim air_slim(const DevMedium& M, double x, double& n
   return Slim{y * y, M.A_air * y, C * x, 1.0 / C};
 }
 
-__device__ __forceinline__ Slim stop_slim(const DevMedium& M, int l) {
+__host__ __device__ __forceinline__ Slim stop_slim(const DevMedium& M, int l) {
   Slim r = slim(M.stop[0]);
   r = pick(l == 1, slim(M.stop[1]), r);
   r = pick(l == 2, slim(M.stop[2]), r);
@@ -699,9 +699,11 @@ __device__ __forceinline__ Slim stop_slim(const DevMedium& M, int l) {
 }
 
 // Start endpoint of air layer l (scalar reads when l is wave-uniform, as start_slim below).
-__device__ __forceinline__ Endpoint start_endpoint(const DevMedium& M, int l) {
+__host__ __device__ __forceinline__ Endpoint start_endpoint(const DevMedium& M, int l) {
+#if defined(__HIP_DEVICE_COMPILE__)
   const int lu = __builtin_amdgcn_readfirstlane(l);
   if (__ballot(l != lu) == 0) return M.start[lu];
+#endif
   Endpoint r = M.start[0];
   r = pick(l == 1, M.start[1], r);
   r = pick(l == 2, M.start[2], r);
@@ -711,9 +713,11 @@ __device__ __forceinline__ Endpoint start_endpoint(const DevMedium& M, int l) {
 
 // Start end of air layer l: a scalar read when l is the same on every lane of the wave (a batch
 // with one ice height), per-lane selects otherwise.
-__device__ __forceinline__ Slim start_slim(const DevMedium& M, int l) {
+__host__ __device__ __forceinline__ Slim start_slim(const DevMedium& M, int l) {
+#if defined(__HIP_DEVICE_COMPILE__)
   const int lu = __builtin_amdgcn_readfirstlane(l);
   if (__ballot(l != lu) == 0) return slim(M.start[lu]);
+#endif
   Slim r = slim(M.start[0]);
   r = pick(l == 1, slim(M.start[1]), r);
   r = pick(l == 2, slim(M.start[2]), r);
@@ -721,7 +725,7 @@ __device__ __forceinline__ Slim start_slim(const DevMedium& M, int l) {
   return r;
 }
 
-__device__ __forceinline__ double stop_n(const DevMedium& M, int l) {
+__host__ __device__ __forceinline__ double stop_n(const DevMedium& M, int l) {
   double r = M.stop[0].n;
   r = (l == 1) ? M.stop[1].n : r;
   r = (l == 2) ? M.stop[2].n : r;
@@ -732,7 +736,7 @@ __device__ __forceinline__ double stop_n(const DevMedium& M, int l) {
 
 // fDnfR(R) - fDnfR(T) with one logarithm when both ends share C (identity (5)).
 // tab: the log table (the roots kernel's LDS copy, else the global one).
-__device__ __forceinline__ double delta_D(const Slim& T, const Slim& R, const RayL& RL,
+__host__ __device__ __forceinline__ double delta_D(const Slim& T, const Slim& R, const RayL& RL,
                                           const double* tab = &kLogTable[0][0]) {
   const double syR = fast_sqrt(R.y2 - RL.LL), syT = fast_sqrt(T.y2 - RL.LL);
   const double d1 = log_ratio(R.Ay - RL.LL + RL.sAL * syR, T.Ay - RL.LL + RL.sAL * syT, tab);
@@ -751,7 +755,7 @@ struct Query {
 
 // Sum of per-layer horizontal distances in air for launch angle theta (THD only: the time
 // and geometric-path terms do not enter f).  Returns L0 through the reference.
-__device__ __forceinline__ double air_thd(const DevMedium& M, const Query& q, double theta,
+__host__ __device__ __forceinline__ double air_thd(const DevMedium& M, const Query& q, double theta,
                                           double& L0, const double* tab) {
   if (q.top < q.bot) {  // no layer: the reference reads unset output slots (UB)
     L0 = __builtin_nan("");
@@ -791,7 +795,7 @@ __device__ __forceinline__ double air_thd(const DevMedium& M, const Query& q, do
 
 // delta_D at two ray parameters (two launch angles) on the same segment: the two chains in one
 // straight-line block, so each hides the other's latency; every value as delta_D forms it.
-__device__ __forceinline__ void delta_D2(const Slim& T, const Slim& R, const RayL& Ra,
+__host__ __device__ __forceinline__ void delta_D2(const Slim& T, const Slim& R, const RayL& Ra,
                                          const RayL& Rb, const double* tab, double& xa,
                                          double& xb) {
   const double syRa = fast_sqrt(R.y2 - Ra.LL), syTa = fast_sqrt(T.y2 - Ra.LL);
@@ -806,7 +810,7 @@ __device__ __forceinline__ void delta_D2(const Slim& T, const Slim& R, const Ray
 // MinimizeforLaunchAngle's THD in air and in the ice at two angles (the root finder's bracket
 // ends f(lo), f(hi)), as air_thd + the ice term of solve_root's evaluation site computes each:
 // the same operations in the same order per angle, the two angles' chains interleaved.
-__device__ __forceinline__ void eval_thd2(const DevMedium& M, const IceConsts& I, const Query& q,
+__host__ __device__ __forceinline__ void eval_thd2(const DevMedium& M, const IceConsts& I, const Query& q,
                                           double ta, double tb, const double* tab,
                                           double& air_a, double& ice_a, double& air_b,
                                           double& ice_b) {
@@ -917,7 +921,7 @@ struct Geometry {
   double depth_pos;         // MinforLAng_params.antennadepth
 };
 
-__device__ __forceinline__ Geometry shift(double H, double D, double ice, double depth) {
+__host__ __device__ __forceinline__ Geometry shift(double H, double D, double ice, double depth) {
   Geometry g;
   g.H = H;
   g.D = D;
@@ -950,8 +954,11 @@ enum { PH_PROBE = 0, PH_FLO = 1, PH_FHI = 2, PH_EST = 3, PH_G1 = 4, PH_G2 = 5, P
 #if AIRICE_SORTED_STATS
 // debug build: wave-level executions of the root finder's blocks (tools/solve_blocks.py): the
 // first active lane of each execution counts it, so a block that several lanes of a wave run
-// together counts once -- the count of the wave's instruction streams through it
+// together counts once -- the count of the wave's instruction streams through it (device code
+// only: the host form of the root finder counts nothing)
 __device__ unsigned long long g_dbg_exec[16];
+#endif
+#if AIRICE_SORTED_STATS && defined(__HIP_DEVICE_COMPILE__)
 #define DBG_EXEC(i)                                                                 \
   do {                                                                              \
     if ((int)(threadIdx.x & 63) == __builtin_ctzll(__ballot(1))) atomicAdd(&g_dbg_exec[i], 1ull); \
@@ -961,6 +968,39 @@ __device__ unsigned long long g_dbg_exec[16];
   do {              \
   } while (0)
 #endif
+
+// Quotients and the first guess's tangent that only steer the search (the root comes from GSL's
+// bisection replay): v_rcp_f64 (~2^-24 relative) and the fast single-precision tangent on the
+// device, the plain forms on the host.
+__host__ __device__ __forceinline__ double rcp_steer(double x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __builtin_amdgcn_rcp(x);
+#else
+  return 1.0 / x;
+#endif
+}
+// isfinite / isnan as each pass has them (ocml's on the device: the kernels' code is unchanged)
+__host__ __device__ __forceinline__ bool k_isfinite(double x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return isfinite(x);
+#else
+  return std::isfinite(x);
+#endif
+}
+__host__ __device__ __forceinline__ bool k_isnan(double x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return isnan(x);
+#else
+  return std::isnan(x);
+#endif
+}
+__host__ __device__ __forceinline__ float tanf_steer(float x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __tanf(x);
+#else
+  return std::tan(x);
+#endif
+}
 
 // The root finder of one query as a state machine with a single evaluation site (RootSearch):
 // begin() sets up the bracket and the probe, next_point() runs the evaluation-free bisection
@@ -994,12 +1034,12 @@ struct RootSearch {
   int t_lean;
 #endif
 
-  __device__ __forceinline__ double& dlt() { return x1; }
+  __host__ __device__ __forceinline__ double& dlt() { return x1; }
 
   // Air2IceRayTracing's set-up (.cc:1487-1509): the query's endpoints, the bracket [thR - 16, thR]
   // and the 0.05-degree probe.  An uninitialised solver state (non-finite bracket end) is modelled
   // as zeros.
-  __device__ __forceinline__ void begin(const DevMedium& M, const IceConsts& I, const Geometry& g,
+  __host__ __device__ __forceinline__ void begin(const DevMedium& M, const IceConsts& I, const Geometry& g,
                                         double thR, bool exact_) {
     status = 0;
     exact = exact_;
@@ -1086,7 +1126,7 @@ struct RootSearch {
     n_inside = 0;
   }
 
-  __device__ __forceinline__ void guard(double x, double f) {
+  __host__ __device__ __forceinline__ void guard(double x, double f) {
     if (!(fabs(f) >= tau) || !(x > gL && x < gR)) return;
     if ((f < 0.0) == (fL < 0.0)) {
       gL = x;
@@ -1098,7 +1138,7 @@ struct RootSearch {
   }
 
   // gsl_root_test_interval(lo, hi, 0, 1e-9) and the driver's max_iter (.cc:355-371)
-  __device__ __forceinline__ void finish(bool frozen) {
+  __host__ __device__ __forceinline__ void finish(bool frozen) {
     const double tol = 0.000000001;
     bool cont;
     if (lo > hi) {
@@ -1116,9 +1156,9 @@ struct RootSearch {
 
   // gsl_root_fsolver_set's second end, f(hi) (fL holds f(lo)): the bracket state, the guards and
   // the secant search's first guess
-  __device__ __forceinline__ void on_fhi(const DevMedium& M, double f) {
+  __host__ __device__ __forceinline__ void on_fhi(const DevMedium& M, double f) {
     phase = PH_BISECT;
-    if (!isfinite(f)) {
+    if (!k_isfinite(f)) {
       status |= AIRICE_SOLVE_NONFINITE_END;
     } else {
       f_lower = fL;
@@ -1133,8 +1173,8 @@ struct RootSearch {
           if ((fL < 0.0) == (fR < 0.0)) {
             gL = hi;  // no sign change: every midpoint has the ends' sign
           } else {
-            const float ul = __tanf((float)((180 - lo) * M.d2r));
-            const float uh = __tanf((float)((180 - hi) * M.d2r));
+            const float ul = tanf_steer((float)((180 - lo) * M.d2r));
+            const float uh = tanf_steer((float)((180 - hi) * M.d2r));
             const float un = uh - (float)fR * ((uh - ul) / (float)(fR - fL));
             x1 = hi;
             f1 = fR;
@@ -1151,14 +1191,14 @@ struct RootSearch {
   // f(lo) and f(hi) in one pass (eval_thd2: two independent chains per lane, ~1.3x the time of one
   // evaluation instead of 2x); a lane that is probing reaches PH_FLO in the loop and evaluates the
   // ends there
-  __device__ __forceinline__ void ends_paired(const DevMedium& M, const IceConsts& I,
+  __host__ __device__ __forceinline__ void ends_paired(const DevMedium& M, const IceConsts& I,
                                               const double* tab) {
     if (phase != PH_FLO) return;
     double air_a, ice_a, air_b, ice_b;
     eval_thd2(M, I, q, lo, hi, tab, air_a, ice_a, air_b, ice_b);
     const double fa = (q.dist - (ice_a + air_a));
     ++n_eval;
-    if (!isfinite(fa)) {
+    if (!k_isfinite(fa)) {
       status |= AIRICE_SOLVE_NONFINITE_END;
       phase = PH_BISECT;
     } else {
@@ -1170,7 +1210,7 @@ struct RootSearch {
 
   // The evaluation-free bisection steps and the next point to evaluate.  False: the query is done
   // (phase PH_DONE) without another evaluation.
-  __device__ __forceinline__ bool next_point(const DevMedium& M, double& x) {
+  __host__ __device__ __forceinline__ bool next_point(const DevMedium& M, double& x) {
     const double tol = 0.000000001;
     if (phase == PH_BISECT) {
       DBG_EXEC(1);
@@ -1247,14 +1287,14 @@ struct RootSearch {
       DBG_EXEC(11);
       // the secant point only steers the search (the root comes from GSL's bisection replay), so
       // its quotient takes v_rcp_f64 (~2^-24 relative) instead of the IEEE division
-      x = (est == 0) ? x2 : x2 - f2 * ((x2 - x1) * __builtin_amdgcn_rcp(f2 - f1));
+      x = (est == 0) ? x2 : x2 - f2 * ((x2 - x1) * rcp_steer(f2 - f1));
       // theta(f) through (x0, f0), (x1, f1), (x2, f2) in Newton form, at f = 0: the secant step
       // minus f1 f2 times the second divided difference (the search only steers; a point outside
       // the guards falls back to their midpoint below)
       if (est >= 1) {
-        const double d1 = (x2 - x1) * __builtin_amdgcn_rcp(f2 - f1);
-        const double d0 = (x1 - x0) * __builtin_amdgcn_rcp(f1 - f0);
-        x += f1 * f2 * ((d1 - d0) * __builtin_amdgcn_rcp(f2 - f0));
+        const double d1 = (x2 - x1) * rcp_steer(f2 - f1);
+        const double d0 = (x1 - x0) * rcp_steer(f1 - f0);
+        x += f1 * f2 * ((d1 - d0) * rcp_steer(f2 - f0));
       }
       if (!(x > gL && x < gR)) x = 0.5 * (gL + gR);  // safeguard: the guards' midpoint
     } else if (phase == PH_G1) {
@@ -1270,14 +1310,14 @@ struct RootSearch {
   // f = D - THD at x, the point next_point() returned.  REUSE_PROBE: a probing lane's last probe
   // evaluation (at x = lo, the point gsl_root_fsolver_set evaluates next) is taken as f(lo).
   template <bool REUSE_PROBE>
-  __device__ __forceinline__ void update(const DevMedium& M, double x, double thd_air,
+  __host__ __device__ __forceinline__ void update(const DevMedium& M, double x, double thd_air,
                                          double thd_ice) {
     ++n_eval;
     n_inside += (phase == PH_BISECT);
     const double f = (q.dist - (thd_ice + thd_air));
     if (phase == PH_PROBE) {
       DBG_EXEC(5);
-      if ((!isnan(thd_air) && thd_air > 0) || lo > hi - 0.1) {
+      if ((!k_isnan(thd_air) && thd_air > 0) || lo > hi - 0.1) {
         if (hi < 90.001 && hi > 90.00) hi = 90.05;
         phase = PH_FLO;
         if (lo > hi) {
@@ -1288,7 +1328,7 @@ struct RootSearch {
           // this trip evaluated f at x = lo, the point gsl_root_fsolver_set evaluates next
           // (f(lo)): the same point and arithmetic, so its value is PH_FLO's result and the lane
           // goes on to f(hi) one trip earlier
-          if (!isfinite(f)) {
+          if (!k_isfinite(f)) {
             status |= AIRICE_SOLVE_NONFINITE_END;
             phase = PH_BISECT;
           } else {
@@ -1302,7 +1342,7 @@ struct RootSearch {
       }
     } else if (phase == PH_FLO) {
       DBG_EXEC(6);
-      if (!isfinite(f)) {
+      if (!k_isfinite(f)) {
         status |= AIRICE_SOLVE_NONFINITE_END;
         phase = PH_BISECT;
       } else {
@@ -1323,11 +1363,11 @@ struct RootSearch {
       x2 = x;
       f2 = f;
       ++est;
-      if (!isfinite(f)) {
+      if (!k_isfinite(f)) {
         phase = PH_BISECT;
       } else if (fabs(f) < tau) {
         // at the root: guards a few tau either side, scaled by the local secant slope
-        const double sl = (x2 - x1) * __builtin_amdgcn_rcp(f2 - f1);  // dtheta / df
+        const double sl = (x2 - x1) * rcp_steer(f2 - f1);  // dtheta / df
         const double a = (x2 - x1) * (f1 - f0), b = (x1 - x0) * (f2 - f1);  // (before dlt takes x1)
         dlt() = 4.0 * tau * fabs(sl);
         const bool room = dlt() > 0.0 && dlt() < (gR - gL);
@@ -1355,14 +1395,14 @@ struct RootSearch {
       }
     } else if (phase == PH_G1 || phase == PH_G2) {
       DBG_EXEC(9);
-      if (isfinite(f)) guard(x, f);
+      if (k_isfinite(f)) guard(x, f);
       phase = phase == PH_G1 ? PH_G2 : PH_BISECT;
     } else {  // PH_BISECT: gsl_root_fsolver_iterate at a midpoint between the guards
       DBG_EXEC(10);
-      if (!exact && isfinite(f)) guard(x, f);
+      if (!exact && k_isfinite(f)) guard(x, f);
       ++iter;
       bool frozen = false;
-      if (!isfinite(f)) {
+      if (!k_isfinite(f)) {
         // EBADFUNC leaves the state unchanged: every later iterate repeats this one, so the
         // driver ends at max_iter with the same root.
         status |= AIRICE_SOLVE_STALE_MID | AIRICE_SOLVE_MAXITER;
@@ -1381,11 +1421,11 @@ struct RootSearch {
     }
   }
 
-  __device__ __forceinline__ double root() const { return root_zero ? 0.0 : 0.5 * (lo + hi); }
+  __host__ __device__ __forceinline__ double root() const { return root_zero ? 0.0 : 0.5 * (lo + hi); }
 };
 
 // MinimizeforLaunchAngle's f terms at theta (.cc:873-917): THD in air and in the ice.
-__device__ __forceinline__ void eval_thd(const DevMedium& M, const IceConsts& I, const Query& q,
+__host__ __device__ __forceinline__ void eval_thd(const DevMedium& M, const IceConsts& I, const Query& q,
                                          double theta, const double* tab, double& thd_air,
                                          double& thd_ice) {
   double L;
@@ -1404,7 +1444,7 @@ __device__ __forceinline__ void eval_thd(const DevMedium& M, const IceConsts& I,
 // evaluation instead of waiting for each other (the probe runs in ~7% of queries).
 // WAVE: one query per wave (scalar_solve_kernel), each evaluation spread over the lanes.
 template <bool WAVE = false>
-__device__ __forceinline__ SolveResult solve_root(const DevMedium& M, const IceConsts& I,
+__host__ __device__ __forceinline__ SolveResult solve_root(const DevMedium& M, const IceConsts& I,
                                                   const Geometry& g, double thR, bool exact,
                                                   const double* tab) {
 #if AIRICE_SCALAR_STAMP
@@ -1493,7 +1533,7 @@ struct Solved {
 };
 
 // Outputs at the root (GetAirPropagationPar + GetIcePropagationPar, .cc:1524-1566).
-__device__ __forceinline__ Solved evaluate_root(const DevMedium& M, const IceConsts& I,
+__host__ __device__ __forceinline__ Solved evaluate_root(const DevMedium& M, const IceConsts& I,
                                                 const Geometry& g, double x, int status,
                                                 const double* tab) {
   Solved S;
@@ -1615,7 +1655,7 @@ struct WaveRoot {
   Geometry g;  // the query, as load_query gave it to the root finder
 };
 
-__device__ __forceinline__ double straight_angle(const DevMedium& M, double H, double D, double ice,
+__host__ __device__ __forceinline__ double straight_angle(const DevMedium& M, double H, double D, double ice,
                                                  double depth) {
   double thR = 0;
   if (depth < 0) thR = 180 - (atan(D / (H - ice - depth)) * M.r2d);
@@ -1643,7 +1683,7 @@ struct QueryArgs {
 // inl: a one-query call whose inputs arrived in the kernel arguments (Signal::in, the same values
 // as Q's arrays hold), read from there instead of from host memory.
 template <int IN>
-__device__ __forceinline__ Geometry load_query(const DevMedium& M, const QueryArgs& Q, long long k,
+__host__ __device__ __forceinline__ Geometry load_query(const DevMedium& M, const QueryArgs& Q, long long k,
                                                double& thR, const Signal* inl = nullptr) {
   const double qa = inl ? inl->in[0] : Q.a[k];
   const double qb = inl ? inl->in[1] : Q.b[k];
@@ -1737,7 +1777,7 @@ constexpr long long kGroupMin = 65536;
 
 // Stage 2 of the lookup fallback with the root handed over in registers (lookup_fallback_kernel):
 // defined below.
-__device__ __forceinline__ void fallback_out_direct(const DevMedium& M, const IceConsts& I,
+__host__ __device__ __forceinline__ void fallback_out_direct(const DevMedium& M, const IceConsts& I,
                                                     const QueryArgs& Q, double* __restrict__ out,
                                                     size_t ld, uint8_t* __restrict__ ok,
                                                     long long k, const double* tab,
@@ -1970,7 +2010,7 @@ __global__ __launch_bounds__(kSortedBlock, kRootsWaves) void roots_sorted_kernel
 }
 
 // Stage 1's result of query k for stage 2.
-__device__ __forceinline__ void parked(const SortedPark& sp, const double* root_slot,
+__host__ __device__ __forceinline__ void parked(const SortedPark& sp, const double* root_slot,
                                        const double* status_slot, long long k, double& x, int& st) {
   if (sp.rec != nullptr) {
     const double2 p = sp.rec[sp.inv[k]];
@@ -1982,7 +2022,7 @@ __device__ __forceinline__ void parked(const SortedPark& sp, const double* root_
   }
 }
 
-__device__ __forceinline__ bool check_solution(double thd, double D) {
+__host__ __device__ __forceinline__ bool check_solution(double thd, double D) {
   // CheckSolution (.cc:978-983, AirIceRayTracing.cc:916-921)
   bool good = false;
   if ((fabs(thd - D) / D < 0.01 && D <= 100) || (fabs(thd - D) < 1 && D > 100)) good = true;
@@ -2006,10 +2046,10 @@ __device__ __forceinline__ void stage_log_table(double (*s)[2]) {
 // WAVE (one-query kernel): every lane runs the body with the root in wr; evaluate_root_wave
 // spreads the evaluation over the wave and lane 0 writes the outputs.
 // Stage-2 output stores (non-temporal stores measured no faster)
-__device__ __forceinline__ void put_out(double* p, double v) { *p = v; }
+__host__ __device__ __forceinline__ void put_out(double* p, double v) { *p = v; }
 
 template <int VARIANT, bool WAVE = false>
-__device__ __forceinline__ void solve_out_body(const DevMedium& M, const IceConsts& I,
+__host__ __device__ __forceinline__ void solve_out_body(const DevMedium& M, const IceConsts& I,
                                                const QueryArgs& Q, double* __restrict__ out,
                                                size_t ld, uint8_t* __restrict__ status,
                                                long long k, const double* tab,
@@ -2020,8 +2060,13 @@ __device__ __forceinline__ void solve_out_body(const DevMedium& M, const IceCons
   double x = wr.root;
   int st = wr.status;
   if (!WAVE) parked(sp, out + 10 * ld + k, out + 0 * ld + k, k, x, st);
-  const Solved S = WAVE ? evaluate_root_wave(M, I, g, x, st, tab) : evaluate_root(M, I, g, x, st, tab);
-  if (WAVE && threadIdx.x != 0) return;
+  Solved S;
+  if constexpr (WAVE) {
+    S = evaluate_root_wave(M, I, g, x, st, tab);
+    if (threadIdx.x != 0) return;
+  } else {
+    S = evaluate_root(M, I, g, x, st, tab);
+  }
   const double thd = S.thd_ice + S.thd_air;
   const double tt = S.t_ice + S.t_air;
   put_out(out + 0 * ld + k, g.H);
@@ -2069,7 +2114,7 @@ __global__ __launch_bounds__(kBlock) void solve_out_kernel(DevMedium M, IceConst
 
 // Stage 2 of GetHorizontalDistanceToIntersectionPoint (.cc:945-989): 9 outputs (cm, rad) + bool.
 template <bool WAVE = false>
-__device__ __forceinline__ void hdtip_out_body(const DevMedium& M, const IceConsts& I,
+__host__ __device__ __forceinline__ void hdtip_out_body(const DevMedium& M, const IceConsts& I,
                                                const QueryArgs& Q, double* __restrict__ out,
                                                size_t ld, uint8_t* __restrict__ ok, long long k,
                                                const double* tab, WaveRoot wr = WaveRoot{0.0, 0},
@@ -2079,8 +2124,13 @@ __device__ __forceinline__ void hdtip_out_body(const DevMedium& M, const IceCons
   double x = wr.root;
   int st = wr.status;
   if (!WAVE) parked(sp, out + 4 * ld + k, out + 0 * ld + k, k, x, st);
-  const Solved S = WAVE ? evaluate_root_wave(M, I, g, x, st, tab) : evaluate_root(M, I, g, x, st, tab);
-  if (WAVE && threadIdx.x != 0) return;
+  Solved S;
+  if constexpr (WAVE) {
+    S = evaluate_root_wave(M, I, g, x, st, tab);
+    if (threadIdx.x != 0) return;
+  } else {
+    S = evaluate_root(M, I, g, x, st, tab);
+  }
   const double thd = S.thd_ice + S.thd_air;
   double tS, tP;
   fresnel_from_sine(S.ice_n, I.ice0.n, S.ice_n / I.ice0.n, sin_start(S.inc * M.d2r), tS, tP);
@@ -2114,7 +2164,7 @@ __global__ __launch_bounds__(kBlock) void hdtip_out_kernel(DevMedium M, IceConst
 // DIRECT (lane form): the query and its root arrive in wr (the fused fallback pass) instead of
 // being reloaded and read back from the parked slots.
 template <bool WAVE = false, bool DIRECT = false>
-__device__ __forceinline__ void lookup_fallback_out_body(const DevMedium& M, const IceConsts& I,
+__host__ __device__ __forceinline__ void lookup_fallback_out_body(const DevMedium& M, const IceConsts& I,
                                                          const QueryArgs& Q,
                                                          double* __restrict__ out, size_t ld,
                                                          uint8_t* __restrict__ ok, long long k,
@@ -2125,8 +2175,13 @@ __device__ __forceinline__ void lookup_fallback_out_body(const DevMedium& M, con
   const Geometry g = (WAVE || DIRECT) ? wr.g : load_query<IN_CM100>(M, Q, k, thR);
   const double x = (WAVE || DIRECT) ? wr.root : out[4 * ld + k];
   const int st = (WAVE || DIRECT) ? wr.status : (int)out[0 * ld + k];
-  const Solved S = WAVE ? evaluate_root_wave(M, I, g, x, st, tab) : evaluate_root(M, I, g, x, st, tab);
-  if (WAVE && threadIdx.x != 0) return;
+  Solved S;
+  if constexpr (WAVE) {
+    S = evaluate_root_wave(M, I, g, x, st, tab);
+    if (threadIdx.x != 0) return;
+  } else {
+    S = evaluate_root(M, I, g, x, st, tab);
+  }
   const double thd = S.thd_ice + S.thd_air;
   double tS, tP;
   fresnel_from_sine(S.ice_n, I.ice0.n, S.ice_n / I.ice0.n, sin_start(S.inc * M.d2r), tS, tP);
@@ -2144,7 +2199,7 @@ __device__ __forceinline__ void lookup_fallback_out_body(const DevMedium& M, con
   ok[k] = good ? 1 : 0;
 }
 
-__device__ __forceinline__ void fallback_out_direct(const DevMedium& M, const IceConsts& I,
+__host__ __device__ __forceinline__ void fallback_out_direct(const DevMedium& M, const IceConsts& I,
                                                     const QueryArgs& Q, double* __restrict__ out,
                                                     size_t ld, uint8_t* __restrict__ ok,
                                                     long long k, const double* tab,
@@ -2154,7 +2209,7 @@ __device__ __forceinline__ void fallback_out_direct(const DevMedium& M, const Ic
 
 // Stage 2 of the pythonwrapper TraceIceToAir (TraceIceToAir.C:5-73), rows of 10.
 template <bool WAVE = false>
-__device__ __forceinline__ void trace_out_body(const DevMedium& M, const IceConsts& I,
+__host__ __device__ __forceinline__ void trace_out_body(const DevMedium& M, const IceConsts& I,
                                                const QueryArgs& Q, double* __restrict__ out10,
                                                long long k, const double* tab,
                                                WaveRoot wr = WaveRoot{0.0, 0},
@@ -2165,8 +2220,13 @@ __device__ __forceinline__ void trace_out_body(const DevMedium& M, const IceCons
   double x = wr.root;
   int st = wr.status;
   if (!WAVE) parked(sp, o + 5, o + 9, k, x, st);
-  const Solved S = WAVE ? evaluate_root_wave(M, I, g, x, st, tab) : evaluate_root(M, I, g, x, st, tab);
-  if (WAVE && threadIdx.x != 0) return;
+  Solved S;
+  if constexpr (WAVE) {
+    S = evaluate_root_wave(M, I, g, x, st, tab);
+    if (threadIdx.x != 0) return;
+  } else {
+    S = evaluate_root(M, I, g, x, st, tab);
+  }
   const double thd = S.thd_ice + S.thd_air;
   const double aoi = k_asin((S.ice_n / I.ice0.n) * sin_start(S.inc * M.d2r)) * M.r2d;
   if (check_solution(thd, g.D)) {
@@ -2254,6 +2314,76 @@ __global__ __launch_bounds__(64) void scalar_solve_kernel(DevMedium M, IceConsts
   out[27 * ld] = (double)r.t_post;
 #endif
   signal_done(sig);
+}
+
+// One query of a minimizer entry point on the host (AIRICE_SCALAR_HOST, the default of the
+// one-query C++ / ctypes drop-ins): the root finder and the entry point's stage-2 body compiled
+// for the CPU from the same source as the batch kernels (the host's correctly rounded sqrt and
+// quotients in place of the device iterations).  The root is the GSL bisection's, decided by the
+// signs of f at its midpoints, so it is the device's; the outputs at it agree to an ulp or so.
+// Q: the query at index 0 (host pointers); park: where stage 1 parks (root, status) for the body,
+// as the launcher of the batch path sets it.
+template <int IN, int OUT>
+static void solve_one_host_t(const DevMedium& M, const IceConsts& I, const QueryArgs& Q,
+                             const Park& park, double* out, size_t ld, uint8_t* flag) {
+  const double* tab = &kLogTable[0][0];
+  if (IN == IN_CM100 && !(Q.mask[0] & AIRICE_LOOKUP_FALLBACK)) return;
+  double thR;
+  const Geometry g = load_query<IN>(M, Q, 0, thR);
+  const SolveResult r = solve_root<false>(M, I, g, thR, park.exact != 0, tab);
+  if constexpr (OUT == OUT_FALLBACK) {
+    fallback_out_direct(M, I, Q, out, ld, flag, 0, tab, g, r.root, r.status);
+  } else {
+    park.root[0] = r.root;
+    park.status[0] = (double)r.status;
+    if constexpr (OUT == OUT_SOLVE_MR)
+      solve_out_body<AIRICE_VARIANT_MULTIRAY>(M, I, Q, out, ld, flag, 0, tab);
+    if constexpr (OUT == OUT_SOLVE_PY)
+      solve_out_body<AIRICE_VARIANT_PYWRAPPER>(M, I, Q, out, ld, flag, 0, tab);
+    if constexpr (OUT == OUT_HDTIP) hdtip_out_body(M, I, Q, out, ld, flag, 0, tab);
+    if constexpr (OUT == OUT_TRACE) trace_out_body(M, I, Q, out, 0, tab);
+  }
+}
+
+// Air2IceRayTracing, one query (in: txh, dist, depth [, straight angle]): out17 / out15 with
+// ld = 1 (as launch_solve parks and writes), status bits.
+int solve_host_one(const DevMedium& M, const IceConsts& I, int variant, const double* in,
+                   bool has_thr, double* out, uint8_t* status) {
+  const QueryArgs Q{in, in + 1, in + 2, has_thr ? in + 3 : nullptr, I.ice_h, 1};
+  const Park park{out + 10, out, 1, bisect_exact(), nullptr};
+  if (variant == AIRICE_VARIANT_PYWRAPPER)
+    solve_one_host_t<IN_M, OUT_SOLVE_PY>(M, I, Q, park, out, 1, status);
+  else
+    solve_one_host_t<IN_M, OUT_SOLVE_MR>(M, I, Q, park, out, 1, status);
+  return AIRICE_OK;
+}
+
+// GetHorizontalDistanceToIntersectionPoint, one query (in: src, dist, depth in cm).
+int hdtip_host_one(const DevMedium& M, const IceConsts& I, double ice_cm, const double* in,
+                   double* out9, uint8_t* ok) {
+  const QueryArgs Q{in, in + 1, in + 2, nullptr, ice_cm, 1};
+  const Park park{out9 + 4, out9, 1, bisect_exact(), nullptr};
+  solve_one_host_t<IN_CM, OUT_HDTIP>(M, I, Q, park, out9, 1, ok);
+  return AIRICE_OK;
+}
+
+// TraceIceToAir, one query (in: depth, ice, txh, dist).
+int trace_host_one(const DevMedium& M, const IceConsts& I, const double* in, double* out10) {
+  const QueryArgs Q{in, in + 1, in + 2, in + 3, 0.0, 1};
+  const Park park{out10 + 5, out10 + 9, 10, bisect_exact(), nullptr};
+  solve_one_host_t<IN_TRACE, OUT_TRACE>(M, I, Q, park, out10, 0, nullptr);
+  return AIRICE_OK;
+}
+
+// The table lookup's minimizer fallback for one flagged query (in: src, dist, depth in cm; ok and
+// flags as the lookup left them).
+int lookup_fallback_host_one(const DevMedium& M, const IceConsts& I, double ice_cm,
+                             const double* in, double* out9, uint8_t* ok, const uint8_t* flags) {
+  const double ice_arg = (ice_cm / 100) * 100;  // as launch_lookup_fallback (.cc:1309, 1419)
+  const QueryArgs Q{in, in + 1, in + 2, nullptr, ice_arg, 1, flags};
+  const Park park{out9 + 4, out9, 1, bisect_exact(), nullptr};
+  solve_one_host_t<IN_CM100, OUT_FALLBACK>(M, I, Q, park, out9, 1, ok);
+  return AIRICE_OK;
 }
 
 // ---------------------------------------------------------------------------

@@ -189,6 +189,29 @@ int folded_ice(const airice_medium* m, int variant, double ice_h, double rx_dept
   return AIRICE_OK;
 }
 
+int solve_query_host(const airice_medium* m, int variant, double ice_h, const double* in,
+                     bool has_thr, double* out, uint8_t* status) {
+  const DevMedium* M = nullptr;
+  const IceConsts* I = nullptr;
+  if (int rc = folded_ice(m, variant, ice_h, 0.0, &M, &I)) return rc;
+  return solve_host_one(*M, *I, variant, in, has_thr, out, status);
+}
+
+int hdtip_query_host(const airice_medium* m, double ice_cm, const double* in, double* out9,
+                     uint8_t* ok) {
+  const DevMedium* M = nullptr;
+  const IceConsts* I = nullptr;
+  if (int rc = folded_ice(m, AIRICE_VARIANT_MULTIRAY, ice_cm / 100, 0.0, &M, &I)) return rc;
+  return hdtip_host_one(*M, *I, ice_cm, in, out9, ok);
+}
+
+int trace_query_host(const airice_medium* m, const double* in, double* out10) {
+  const DevMedium* M = nullptr;
+  const IceConsts* I = nullptr;
+  if (int rc = folded_ice(m, AIRICE_VARIANT_PYWRAPPER, 0.0, 0.0, &M, &I)) return rc;
+  return trace_host_one(*M, *I, in, out10);
+}
+
 // ---- kernel timer (bench only) ---------------------------------------------------------
 std::atomic<bool> g_ktimer_on{false};
 static std::mutex g_kt_mu;
@@ -340,6 +363,17 @@ int ScalarCall::sync() {
 
 int lookup_fallback_one(const airice_medium* m, double src_cm, double dist_cm, double depth_cm,
                         double ice_cm, bool good, int flags, double out9[9], bool* ok) {
+  if (scalar_on_host()) {
+    const DevMedium* Mh = nullptr;
+    const IceConsts* Ih = nullptr;
+    if (int rc = folded_ice(m, AIRICE_VARIANT_MULTIRAY, ice_cm / 100, 0.0, &Mh, &Ih)) return rc;
+    const double in[3] = {src_cm, dist_cm, depth_cm};
+    uint8_t okb = good ? 1 : 0;
+    const uint8_t fl = (uint8_t)flags;
+    if (int rc = lookup_fallback_host_one(*Mh, *Ih, ice_cm, in, out9, &okb, &fl)) return rc;
+    *ok = okb != 0;
+    return AIRICE_OK;
+  }
   DevMedium M;
   int rc = build_dev_medium(m, AIRICE_VARIANT_MULTIRAY, &M);
   if (rc) return rc;
@@ -621,6 +655,22 @@ int airice_solve_host(const airice_medium* m, int variant, double ice_h_m, const
     return AIRICE_EINVAL;
   }
   const int fields = variant == AIRICE_VARIANT_PYWRAPPER ? AIRICE_PYSOLVE_FIELDS : AIRICE_SOLVE_FIELDS;
+  if (n == 1 && airice::scalar_on_host()) {  // one query: on the host (airice_scalar_mode)
+    if (variant != AIRICE_VARIANT_MULTIRAY && variant != AIRICE_VARIANT_PYWRAPPER) {
+      set_error("unknown variant %d", variant);
+      return AIRICE_EINVAL;
+    }
+    const double in[4] = {txh[0], dist[0], depth[0],
+                          straight_angle != nullptr ? straight_angle[0] : 0.0};
+    double o[AIRICE_SOLVE_FIELDS];
+    uint8_t st = 0;
+    if (int rc = airice::solve_query_host(m, variant, ice_h_m, in, straight_angle != nullptr, o,
+                                          &st))
+      return rc;
+    for (int c = 0; c < fields; ++c) out[(size_t)c * ld] = o[c];
+    if (status) status[0] = st;
+    return AIRICE_OK;
+  }
   // one device block: txh | dist | depth | [straight angle] | out (fields x ld) | status
   const size_t nin = straight_angle != nullptr ? 4 : 3;
   DevBuffer buf;
@@ -867,6 +917,10 @@ int airice_trace_ice_to_air_launch(const airice_medium* m, const double* d_depth
 int airice_trace_ice_to_air_host(const airice_medium* m, const double* depth, const double* ice,
                                  const double* txh, const double* dist, size_t n, double* out10) {
   if (n == 0) return AIRICE_OK;
+  if (n == 1 && airice::scalar_on_host()) {  // one query: on the host (airice_scalar_mode)
+    const double in[4] = {depth[0], ice[0], txh[0], dist[0]};
+    return airice::trace_query_host(m, in, out10);
+  }
   DevBuffer mem;
   HIP_TRY(mem.alloc(sizeof(double) * 14 * n));
   double* buf = static_cast<double*>(mem.p);

@@ -375,6 +375,13 @@ double MinimizeforLaunchAngle(double x, void* params) {
 void Air2IceRayTracing(double AirTxHeight, double HorizontalDistance, double IceLayerHeight,
                        double AntennaDepth, double StraightAngle, double dummy[20]) {
   const airice_medium m = medium();
+  if (airice::scalar_on_host()) {  // one query: on the host (airice_scalar_mode)
+    const double in[4] = {AirTxHeight, HorizontalDistance, AntennaDepth, StraightAngle};
+    if (airice::solve_query_host(&m, AIRICE_VARIANT_MULTIRAY, IceLayerHeight, in, true, dummy,
+                                 nullptr) != AIRICE_OK)
+      die("Air2IceRayTracing");
+    return;
+  }
   airice::ScalarCall call;
   if (!call.ok()) die("Air2IceRayTracing");
   airice::ScalarSlot& s = call.slot();
@@ -419,6 +426,23 @@ bool GetHorizontalDistanceToIntersectionPoint(
     double& horizontalDistanceToIntersectionPoint, double& transmissionCoefficientS,
     double& transmissionCoefficientP, double& RecievedAngleInIce) {
   const airice_medium m = medium();
+  if (airice::scalar_on_host()) {  // one query: on the host (airice_scalar_mode)
+    const double in[3] = {SrcHeightASL, HorizontalDistanceToRx, RxDepthBelowIceBoundary};
+    double o[9];
+    uint8_t ok = 0;
+    if (airice::hdtip_query_host(&m, IceLayerHeight, in, o, &ok) != AIRICE_OK)
+      die("GetHorizontalDistanceToIntersectionPoint");
+    opticalPathLengthInIce = o[0];
+    opticalPathLengthInAir = o[1];
+    geometricalPathLengthInIce = o[2];
+    geometricalPathLengthInAir = o[3];
+    launchAngle = o[4];
+    horizontalDistanceToIntersectionPoint = o[5];
+    transmissionCoefficientS = o[6];
+    transmissionCoefficientP = o[7];
+    RecievedAngleInIce = o[8];
+    return ok != 0;
+  }
   airice::ScalarCall call;
   if (!call.ok()) die("GetHorizontalDistanceToIntersectionPoint");
   airice::ScalarSlot& s = call.slot();

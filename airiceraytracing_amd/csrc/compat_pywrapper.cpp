@@ -159,6 +159,13 @@ int layer_of(double zabs) {  // GetB_air / GetC_air layer scan (.cc:180-189)
 // one launch-angle solve through the scalar slot: dummy[0..14] (.cc:1070-1084), status bits
 void solve_one(const airice_medium& m, double H, double D, double ice, double depth,
                const double* straight_angle, double dummy[AIRICE_PYSOLVE_FIELDS]) {
+  if (airice::scalar_on_host()) {  // one query: on the host (airice_scalar_mode)
+    const double in[4] = {H, D, depth, straight_angle != nullptr ? *straight_angle : 0.0};
+    if (airice::solve_query_host(&m, AIRICE_VARIANT_PYWRAPPER, ice, in, straight_angle != nullptr,
+                                 dummy, nullptr) != AIRICE_OK)
+      die("Air2IceRayTracing");
+    return;
+  }
   airice::ScalarCall call;
   if (!call.ok()) die("Air2IceRayTracing");
   airice::ScalarSlot& s = call.slot();
@@ -384,19 +391,24 @@ void TraceIceToAir(double AntennaDepth, double IceLayerHeight, double AirTxHeigh
   }
   // GetRayTracingSolution + the launch/receive swap + ArrayParameters (TraceIceToAir.C:27-68):
   // one launch of the batch trace path with n = 1
-  airice::ScalarCall call;
-  if (!call.ok()) die("TraceIceToAir");
-  airice::ScalarSlot& s = call.slot();
-  s.h[0] = AntennaDepth;
-  s.h[1] = IceLayerHeight;
-  s.h[2] = AirTxHeight;
-  s.h[3] = HorizontalDistance;
-  call.arm(s.h, 4);
-  if (airice_trace_ice_to_air_launch(&m, s.d, s.d + 1, s.d + 2, s.d + 3, 1, s.d + 4, s.st) !=
-          AIRICE_OK ||
-      call.sync() != AIRICE_OK)
-    die("TraceIceToAir");
-  std::memcpy(ArrayParameters, s.h + 4, sizeof(double) * 10);
+  if (airice::scalar_on_host()) {  // one query: on the host (airice_scalar_mode)
+    const double in[4] = {AntennaDepth, IceLayerHeight, AirTxHeight, HorizontalDistance};
+    if (airice::trace_query_host(&m, in, ArrayParameters) != AIRICE_OK) die("TraceIceToAir");
+  } else {
+    airice::ScalarCall call;
+    if (!call.ok()) die("TraceIceToAir");
+    airice::ScalarSlot& s = call.slot();
+    s.h[0] = AntennaDepth;
+    s.h[1] = IceLayerHeight;
+    s.h[2] = AirTxHeight;
+    s.h[3] = HorizontalDistance;
+    call.arm(s.h, 4);
+    if (airice_trace_ice_to_air_launch(&m, s.d, s.d + 1, s.d + 2, s.d + 3, 1, s.d + 4, s.st) !=
+            AIRICE_OK ||
+        call.sync() != AIRICE_OK)
+      die("TraceIceToAir");
+    std::memcpy(ArrayParameters, s.h + 4, sizeof(double) * 10);
+  }
   static const bool verbose = [] {
     const char* v = std::getenv("AIRICE_VERBOSE");
     return v != nullptr && std::strcmp(v, "1") == 0;

@@ -1132,7 +1132,9 @@ def scalar_cpu_per_call(om, og, ot) -> dict:
 def scalar_latencies(args) -> dict | None:
     """Per-call latency of the scalar drop-in entry points (one query per call, host arguments,
     as CoREAS and TraceIceToAir.py call them), measured by tests/cpp/latency_driver (C++, linked
-    against libairice.so) in a child process."""
+    against libairice.so) in a child process: with the one-query calls on the host (the library's
+    default, airice_scalar_mode), and under "device" the same calls as one-wave GPU kernels
+    (AIRICE_SCALAR=device)."""
     import subprocess
     exe = os.path.join(ROOT, "tests", "cpp", "latency_driver")
     if not os.path.exists(exe):
@@ -1145,9 +1147,15 @@ def scalar_latencies(args) -> dict | None:
                 open(os.path.join(td, "Atmosphere.dat"), "wb") as fo:
             fo.write(fz.read())
         r = subprocess.run([exe], cwd=td, capture_output=True, text=True, timeout=300)
+        rd = subprocess.run([exe], cwd=td, capture_output=True, text=True, timeout=300,
+                            env=dict(os.environ, AIRICE_SCALAR="device"))
     if r.returncode != 0:
         return {"error": r.stderr[-500:]}
-    return json.loads(r.stdout.strip().splitlines()[-1])
+    rep = json.loads(r.stdout.strip().splitlines()[-1])
+    rep["where"] = "host (one-query calls on the CPU, airice_scalar_mode default)"
+    rep["device"] = (json.loads(rd.stdout.strip().splitlines()[-1]) if rd.returncode == 0
+                     else {"error": rd.stderr[-500:]})
+    return rep
 
 
 if __name__ == "__main__":

@@ -38,11 +38,14 @@ def test_mangled_namespace_symbols_exported():
 
 
 @pytest.mark.gpu
-def test_cpp_caller_against_oracle(tmp_path, oracle_medium):
+@pytest.mark.parametrize("scalar", ["host", "device"])
+def test_cpp_caller_against_oracle(tmp_path, oracle_medium, scalar):
+    """scalar: the one-query calls on the host (the default) or on the GPU (AIRICE_SCALAR)."""
     assert os.path.exists(DRIVER), "build with __graft_entry__.build()"
     with open(ATMOSPHERE_GZ, "rb") as f:
         (tmp_path / "Atmosphere.dat").write_bytes(gzip.decompress(f.read()))
-    out = subprocess.run([DRIVER], cwd=tmp_path, capture_output=True, text=True, timeout=120)
+    out = subprocess.run([DRIVER], cwd=tmp_path, capture_output=True, text=True, timeout=120,
+                         env=dict(os.environ, AIRICE_SCALAR=scalar))
     assert out.returncode == 0, out.stderr
     txt = re.sub(r"-?\b(nan|inf)\b", lambda mm: {"nan": "NaN", "-nan": "NaN", "inf": "Infinity",
                                                    "-inf": "-Infinity"}[mm.group(0)], out.stdout)

@@ -32,14 +32,15 @@ def _queries():
     return q
 
 
-def _run(tmp_path, q):
+def _run(tmp_path, q, scalar="host"):
+    """scalar: where the one-query calls run (AIRICE_SCALAR: the host by default, or the GPU)."""
     assert os.path.exists(DRIVER), "build with __graft_entry__.build()"
     with open(ATMOSPHERE_GZ, "rb") as f:
         (tmp_path / "Atmosphere.dat").write_bytes(gzip.decompress(f.read()))
     qf = tmp_path / "queries.txt"
     qf.write_text("".join("%.17g %.17g %.17g %.17g\n" % tuple(r) for r in q))
     out = subprocess.run([DRIVER, str(qf)], cwd=tmp_path, capture_output=True, text=True,
-                         timeout=120)
+                         timeout=120, env=dict(os.environ, AIRICE_SCALAR=scalar))
     assert out.returncode == 0, out.stderr
     txt = re.sub(r"-?\b(nan|inf)\b", lambda mm: {"nan": "NaN", "-nan": "NaN", "inf": "Infinity",
                                                    "-inf": "-Infinity"}[mm.group(0)], out.stdout)
@@ -79,9 +80,10 @@ def _check_solves(rows, q, m, mask_unpinned=True, m_trace=None):
 
 
 @pytest.mark.gpu
-def test_pywrapper_cpp_caller_against_oracle(tmp_path, oracle_medium_py):
+@pytest.mark.parametrize("scalar", ["host", "device"])
+def test_pywrapper_cpp_caller_against_oracle(tmp_path, oracle_medium_py, scalar):
     q = _queries()
-    r = _run(tmp_path, q)
+    r = _run(tmp_path, q, scalar)
     m = oracle_medium_py
     ML = m.max_layers
     # namespace data filled by MakeAtmosphere("Atmosphere.dat")

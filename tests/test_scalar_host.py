@@ -1,7 +1,8 @@
 """The one-query calls on the host (airice_rays_host, airice_rtf_eval in AIRICE_SCALAR_HOST mode,
-the library's default): the drop-ins' one-ray GetRayTracingSolutions and the ray layer
-(RayTracingFunctions:: / MultiRayAirIceRefraction:: fDnfR ... MinimizeforLaunchAngle) run on the
-CPU from the same source as the device kernels.  These run here without a GPU: every output
+the library's default): the drop-ins' one-ray GetRayTracingSolutions, the ray layer
+(RayTracingFunctions:: / MultiRayAirIceRefraction:: fDnfR ... MinimizeforLaunchAngle) and the
+one-query solves (Air2IceRayTracing, the CoREAS entry, TraceIceToAir, the lookup fallback) run on
+the CPU from the same source as the device kernels.  These run here without a GPU: every output
 against the oracle at the parity tolerance (1e-9 relative, per-quantity floors, NaN positions
 equal).  Host against device is tests/test_gpu_rtf.py::test_host_matches_device."""
 import numpy as np
@@ -122,3 +123,48 @@ def test_scalar_mode_switch():
     with scalar_mode(_lib.SCALAR_DEVICE):
         assert L.airice_scalar_mode(-1) == _lib.SCALAR_DEVICE
     assert L.airice_scalar_mode(-1) == _lib.SCALAR_HOST
+
+
+@pytest.mark.parametrize("variant", ["multiray", "pywrapper"])
+def test_host_one_query_solves_vs_oracle(oracle_medium, oracle_medium_py, variant):
+    """Air2IceRayTracing one query at a time (airice_solve_host with n = 1: the host root finder,
+    the GSL bisection replay with its guards, and the stage-2 body) against the oracle's solves:
+    status bits equal, outputs within 1e-9 (rows whose GSL state is uninitialised excluded)."""
+    from airiceraytracing_amd import AirIceSolver, VARIANT_MULTIRAY, VARIANT_PYWRAPPER
+    py = variant == "pywrapper"
+    s = AirIceSolver(variant=VARIANT_PYWRAPPER if py else VARIANT_MULTIRAY)
+    txh, dist, dep = parity.cfg3_queries(400, seed=31)
+    outs, sts = [], []
+    for i in range(txh.size):
+        o, st = s.solve_host(txh[i:i + 1], dist[i:i + 1], dep[i:i + 1], 3000.0)
+        outs.append(o[:, 0])
+        sts.append(st[0])
+    got, gst = np.stack(outs, 1), np.array(sts)
+    if py:
+        thr = np.array([oracle.straight_angle_of(oracle_medium_py, a, b, 3000.0, c)
+                        for a, b, c in zip(txh, dist, dep)])
+        rows = [oracle.py_air2ice(oracle_medium_py, a, b, 3000.0, c, t)
+                for a, b, c, t in zip(txh, dist, dep, thr)]
+        ref = np.stack([r[0] for r in rows], 1)
+        rst = np.array([r[1] for r in rows])
+        floors = parity.PYSOLVE_FLOORS
+    else:
+        ref, rst = oracle.solve_batch(oracle_medium, txh, dist, dep, 3000.0)
+        floors = parity.SOLVE_FLOORS
+    mask = (rst & oracle.SOLVE_UNPINNED) == 0
+    assert mask.mean() > 0.95
+    assert np.array_equal(gst[mask], rst[mask])
+    rep = parity.compare_columns(got, ref, floors, mask=mask)
+    assert rep["ok"], rep
+
+
+def test_host_one_query_trace_vs_oracle(oracle_medium_py):
+    """Py_TraceIceToAir one query at a time on the host (airice_trace_ice_to_air_host, n = 1)."""
+    from airiceraytracing_amd import AirIceSolver, VARIANT_PYWRAPPER
+    s = AirIceSolver(variant=VARIANT_PYWRAPPER)
+    d, ice, txh, dist = parity.cfg5_queries(300, seed=17)
+    got = np.stack([s.trace_ice_to_air_host(d[i:i + 1], ice[i:i + 1], txh[i:i + 1],
+                                            dist[i:i + 1])[0] for i in range(d.size)])
+    ref = oracle.py_trace_batch(oracle_medium_py, d, ice, txh, dist)
+    rep = parity.compare_columns(got.T, np.asarray(ref).reshape(-1, 10).T, parity.TRACE_FLOORS)
+    assert rep["ok"], rep
