@@ -219,6 +219,7 @@ def counter_roofline(kernel_key: str, units: int, kernel_ms: float, pmc: dict,
         "fp64_lane_ops_per_unit": ops_per_unit,
         "valu_insts_per_unit": p.get("valu_insts_per_unit"),
         "fp64_pipe_busy_pct": p.get("fp64_pipe_busy_pct"),
+        "valu_busy_pct": p.get("valu_busy_pct"),
         "wave_cycle_shares": p.get("wave_cycle_shares"),
         "units_per_launch": units, "kernel_ms": kernel_ms,
         "hbm_bytes_per_launch_algorithmic": algorithmic_bytes_per_unit * units,

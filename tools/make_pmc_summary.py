@@ -9,6 +9,12 @@ Busy figures, both bounded by construction:
   launch's cycles, GRBM_GUI_ACTIVE / 8 XCDs): a SIMD completes at most one wave64 FP64
   instruction every 4 cycles (16 FP64 lanes per clock, the FP64 vector peak), so this cannot
   exceed 100; it is the roofline fraction at the clock the launch actually ran at.
+* valu_busy_pct = 100 x (4 x FP64 VALU instructions + 2 x the other VALU instructions) / (1024
+  SIMDs x the launch's cycles): every VALU instruction priced at its least issue time on a gfx950
+  SIMD for a wave64 (FP64: 16 lanes per clock, 4 cycles; 32-bit and narrower: 32 lanes per clock, 2
+  cycles -- tools/valu_rates.hip measures these, and the transcendental forms take longer), so the
+  numerator is a lower bound of the SIMDs' VALU-occupied cycles and the figure cannot exceed 100:
+  north_star's "VALU busy", bounded.
 * wave_cycle_shares: SQ_ACTIVE_INST_ANY (issuing), SQ_WAIT_INST_ANY (ready to issue but stalled
   on a dependency or a busy pipe) and SQ_WAIT_ANY (parked on s_waitcnt / barrier) over
   SQ_WAVE_CYCLES -- disjoint parts of every wave's lifetime (MI355X_MICROARCH.md §rocprofv3).
@@ -45,6 +51,8 @@ def derive(name, c, n_units, kernel_ns=None):
         "fp64_valu_insts_per_unit": f64 * 64 / n_units,
         "fp64_fma_share": c.get("SQ_INSTS_VALU_FMA_F64", 0.0) / f64 if f64 else None,
         "fp64_pipe_busy_pct": 100 * f64 * 4 / SIMDS / (grbm / XCDS) if grbm else None,
+        "valu_busy_pct": 100 * (4 * f64 + 2 * (c.get("SQ_INSTS_VALU", 0.0) - f64)) / SIMDS /
+                         (grbm / XCDS) if grbm and "SQ_INSTS_VALU" in c else None,
         "wave_cycle_shares": {
             "issuing": c["SQ_ACTIVE_INST_ANY"] / wc,
             "stalled_ready": c["SQ_WAIT_INST_ANY"] / wc,
