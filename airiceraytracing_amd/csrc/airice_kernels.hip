@@ -36,7 +36,10 @@ constexpr double kSpeedC = 299792458.0;  // .h:30
 constexpr int kBlock = 256;
 // Table launch shape: 256-thread blocks at 8 waves/SIMD (64 VGPRs), measured best of 64 / 128 /
 // 256 / 512 threads, 7 / 8 waves and 1 / 2 rays per lane.
-constexpr int kTableBlock = 256;
+#ifndef AIRICE_TABLE_BLOCK
+#define AIRICE_TABLE_BLOCK 256
+#endif
+constexpr int kTableBlock = AIRICE_TABLE_BLOCK;  // (A/B builds: -DAIRICE_TABLE_BLOCK=...)
 constexpr int kTableWaves = 8;
 // debug builds: shader-clock stamps of the one-query kernels (tools/scalar_stamps.py,
 // tools/ray_stamps.py) and the minimizer's evaluation counts by sorted position (tools/wave_evals.py)
