@@ -73,7 +73,14 @@ def test_batch_matches_oracle_and_scalar(tmp_path, monkeypatch, atmosphere_text,
     assert np.array_equal(out[:, 0] == -1000, ref[:, 0] == -1000)
     rep = parity.compare_columns(out.T, ref.T, parity.TRACE_FLOORS)
     assert rep["ok"], rep
+    # one query per call: on the host by default (the same source, the host's sqrt and quotients:
+    # within an ulp or so of the batch), and bit for bit the batch on the GPU's one-wave kernel
+    from airiceraytracing_amd import _lib
+    from airiceraytracing_amd.solver import scalar_mode
     for i in (0, 17, 4095):
         arr = (ctypes.c_double * 10)()
         m.Py_TraceIceToAir(depth[i], ice[i], txh[i], dist[i], arr)
+        np.testing.assert_allclose(np.array(list(arr)), out[i], rtol=1e-12, atol=1e-12)
+        with scalar_mode(_lib.SCALAR_DEVICE):
+            m.Py_TraceIceToAir(depth[i], ice[i], txh[i], dist[i], arr)
         assert np.array_equal(np.array(list(arr)), out[i])
