@@ -55,6 +55,12 @@ constexpr int kTableWaves = 8;
 #ifndef AIRICE_SORTED_STATS
 #define AIRICE_SORTED_STATS 0
 #endif
+// debug build: roots_kernel writes shader-clock stamps instead of evaluation counts
+// (AIRICE_SOLVE_STATS, 4 ints per query: entry, sorted, inputs at hand, solved; tools/roots_stamps.py)
+#ifndef AIRICE_ROOTS_STAMP
+#define AIRICE_ROOTS_STAMP 0
+#endif
+constexpr int kStatsInts = AIRICE_ROOTS_STAMP ? 4 : 3;
 // evaluation-free bisection steps of the root finder per loop trip (as compare-and-select)
 constexpr int kLeanUnroll = 4;
 // table stores take an SGPR column base and a 32-bit lane byte offset (global_store saddr form):
@@ -344,6 +350,7 @@ __device__ __forceinline__ void table_ray(const DevMedium& M, const IceConsts& I
     char* tb = reinterpret_cast<char*>(table);
     const size_t ldb = ld * sizeof(float);
     const uint32_t off = (uint32_t)k * 4u;
+    // (non-temporal stores: cfg2 28.9 -> 29.9 us, same bits)
     auto st = [&](int c, double v) { *reinterpret_cast<float*>(tb + c * ldb + off) = (float)v; };
     st(0, d[1]);
     st(1, d[2]);
@@ -1770,7 +1777,10 @@ static inline int bisect_exact() {
 // own and written by its index.
 constexpr int kSortBuckets = 16;
 // 1024 queries per block: larger groups sort better, and a 16-wave block runs at 4 waves/SIMD
-// (128 VGPRs, some spilled) -- measured faster than 256 (3 waves, no spills), 512 and 768.
+// (128 VGPRs) -- measured faster than 256 (3 waves, no spills), 512 and 768; and (round 5) than
+// 512- and 256-thread blocks that each sort the whole 1,024-query chunk (a deterministic ballot
+// sort) and solve their half / quarter of it: the same waves at a finer dispatch grain, 0.263 /
+// 0.307 against 0.244 ms per call (the duplicated keying costs more than the block tail saves).
 constexpr int kRootsBlock = 1024;
 constexpr int kRootsWaves = 4;  // 127 VGPRs: 4 waves/SIMD (5 and 6 spill and run slower)
 // batch-wide grouping: trace (IN_TRACE) batches of at least kGroupMin queries are sorted across
@@ -1823,8 +1833,12 @@ template <int IN>
 __global__ __launch_bounds__(kRootsBlock, kRootsWaves) void roots_kernel(DevMedium M, IceConsts I,
                                                                          QueryArgs Q, Park park) {
   static_assert(solves_every_lane(IN), "IN_CM100 lanes are masked: use lookup_fallback_kernel");
+#if AIRICE_ROOTS_STAMP
+  const unsigned long long st0 = __builtin_amdgcn_s_memtime();
+#endif
   __shared__ int s_count[kSortBuckets + 1];
   __shared__ int s_slot[kRootsBlock];
+  __shared__ double s_q[6][kRootsBlock];  // the sorted queries' geometry and straight-line angle
   const long long k0 = (long long)blockIdx.x * kRootsBlock;
   const long long kt = k0 + threadIdx.x;
   // the log table in LDS (one 16-byte entry per thread), as in table_kernel: every evaluation's
@@ -1835,40 +1849,66 @@ __global__ __launch_bounds__(kRootsBlock, kRootsWaves) void roots_kernel(DevMedi
     s_logtab[t][1] = kLogTable[t][1];
   }
   if (threadIdx.x <= kSortBuckets) s_count[threadIdx.x] = 0;
-  __syncthreads();
-  // bucket of this lane's own query (unused lanes last)
+  // bucket of this lane's own query (unused lanes last); its inputs are read while the log table
+  // is staged
   int bucket = kSortBuckets;
+  Geometry g0{};
+  double thR0 = 0.0;
   if (kt < Q.n) {
-    double thR0;
-    (void)load_query<IN>(M, Q, kt, thR0);
+    g0 = load_query<IN>(M, Q, kt, thR0);
     const double b = (thR0 - 90.0) * (kSortBuckets / 90.0);
     bucket = (b >= 0.0 && b < kSortBuckets) ? (int)b : ((b >= kSortBuckets) ? kSortBuckets - 1 : 0);
   }
+  __syncthreads();
   const int rank = atomicAdd(&s_count[bucket], 1);
   __syncthreads();
-  if (threadIdx.x == 0) {  // exclusive prefix sum of the bucket sizes
-    int acc = 0;
-    for (int b = 0; b <= kSortBuckets; ++b) {
-      const int c = s_count[b];
-      s_count[b] = acc;
-      acc += c;
-    }
-  }
-  __syncthreads();
-  s_slot[s_count[bucket] + rank] = threadIdx.x;
+  // the first slot of the lane's bucket: the sizes of the buckets below it (independent LDS reads)
+  int slot = rank;
+#pragma unroll
+  for (int b = 0; b < kSortBuckets; ++b) slot += b < bucket ? s_count[b] : 0;
+  // the query moves to its slot through LDS: index, geometry and angle (no second global read)
+  s_slot[slot] = threadIdx.x;
+  s_q[0][slot] = g0.H;
+  s_q[1][slot] = g0.D;
+  s_q[2][slot] = g0.ice;
+  s_q[3][slot] = g0.depth;
+  s_q[4][slot] = g0.depth_pos;
+  s_q[5][slot] = thR0;
   __syncthreads();
   const long long k = k0 + s_slot[threadIdx.x];
   if (k >= Q.n) return;
-  double thR;
-  const Geometry g = load_query<IN>(M, Q, k, thR);
+#if AIRICE_ROOTS_STAMP
+  const unsigned long long st1 = __builtin_amdgcn_s_memtime() + (unsigned long long)(k & 0);
+#endif
+  Geometry g;
+  g.H = s_q[0][threadIdx.x];
+  g.D = s_q[1][threadIdx.x];
+  g.ice = s_q[2][threadIdx.x];
+  g.depth = s_q[3][threadIdx.x];
+  g.depth_pos = s_q[4][threadIdx.x];
+  const double thR = s_q[5][threadIdx.x];
+#if AIRICE_ROOTS_STAMP
+  const unsigned long long st2 =
+      __builtin_amdgcn_s_memtime() + (unsigned long long)(0.0 * (thR + g.H + g.D + g.depth + g.ice));
+#endif
   const SolveResult r = solve_root(M, I, g, thR, park.exact != 0, &s_logtab[0][0]);
   park.root[k * park.stride] = r.root;
   park.status[k * park.stride] = (double)r.status;
+#if AIRICE_ROOTS_STAMP
+  const unsigned long long st3 = __builtin_amdgcn_s_memtime() + (unsigned long long)(0.0 * r.root);
+  if (park.stats != nullptr) {
+    park.stats[4 * k] = (int)(unsigned)st0;
+    park.stats[4 * k + 1] = (int)(st1 - st0);
+    park.stats[4 * k + 2] = (int)(st2 - st0);
+    park.stats[4 * k + 3] = (int)(st3 - st0);
+  }
+#else
   if (park.stats != nullptr) {
     park.stats[3 * k] = r.n_eval;
     park.stats[3 * k + 1] = r.n_est;
     park.stats[3 * k + 2] = r.n_inside;
   }
+#endif
 }
 
 // ---------------------------------------------------------------------------
@@ -2976,7 +3016,7 @@ int launch_solve(const DevMedium& M, const IceConsts& I, int variant, const doub
   const QueryArgs Q{txh, dist, depth, thr, I.ice_h, (long long)n};
   Park park{out + 10 * ld, out, 1, bisect_exact(), nullptr};
   static const char* stats_path = getenv("AIRICE_SOLVE_STATS");
-  if (stats_path != nullptr && hipMalloc(&park.stats, sizeof(int) * 3 * n) != hipSuccess)
+  if (stats_path != nullptr && hipMalloc(&park.stats, sizeof(int) * kStatsInts * n) != hipSuccess)
     return AIRICE_EHIP;
   const dim3 grid(grid_for((long long)n)), block(kBlock);
   if (n == 1 && park.stats == nullptr) {
@@ -2993,13 +3033,13 @@ int launch_solve(const DevMedium& M, const IceConsts& I, int variant, const doub
   RootsScratch scr(st);
   if (int rc = launch_roots<IN_M>(M, I, Q, park, n, st, sp, scr.ws)) return rc;
   if (park.stats != nullptr) {  // debug: append the per-query counts (synchronous)
-    std::vector<int> h(3 * n);
+    std::vector<int> h(kStatsInts * n);
     if (hipStreamSynchronize(st) != hipSuccess ||
-        hipMemcpy(h.data(), park.stats, sizeof(int) * 3 * n, hipMemcpyDeviceToHost) != hipSuccess)
+        hipMemcpy(h.data(), park.stats, sizeof(int) * kStatsInts * n, hipMemcpyDeviceToHost) != hipSuccess)
       return AIRICE_EHIP;
     (void)hipFree(park.stats);
     if (FILE* f = fopen(stats_path, "ab")) {
-      fwrite(h.data(), sizeof(int), 3 * n, f);
+      fwrite(h.data(), sizeof(int), kStatsInts * n, f);
       fclose(f);
     }
   }

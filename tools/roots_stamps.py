@@ -1,0 +1,78 @@
+"""Where roots_kernel's wave time goes (debug, GPU box): a -DAIRICE_ROOTS_STAMP=1 build records four
+shader-clock stamps per wave (entry, after the block's LDS counting sort, after the sorted query's
+inputs are at hand, after solve_root) through AIRICE_SOLVE_STATS; this prints, over the 1e6 cfg3 solves,
+the share of wave time in each phase and the share of a block's wave slots left idle waiting for
+the block's slowest wave (a CU starts its next 1,024-query block only then).
+
+    tools/build_variant.sh airiceraytracing_amd/csrc /tmp/stamp.so -DAIRICE_ROOTS_STAMP=1 ...
+    python tools/roots_stamps.py /tmp/stamp.so [n]
+"""
+import json
+import os
+import subprocess
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+BLOCK = 1024
+
+
+def main():
+    lib = os.path.abspath(sys.argv[1])
+    n = int(sys.argv[2]) if len(sys.argv) > 2 else 1000000
+    path = "/tmp/roots_stamps.bin"
+    if os.path.exists(path):
+        os.remove(path)
+    env = dict(os.environ, AB_LIB=lib)
+    subprocess.run([sys.executable, os.path.join(ROOT, "tools", "solve_stats.py"), "--child",
+                    "stamp", str(n), path], env=env, check=True, timeout=300)
+    a = np.fromfile(path, dtype=np.int32).reshape(-1, 4).astype(np.int64)
+    a = a[:n]
+    blk = np.arange(len(a)) // BLOCK
+    t0 = a[:, 0] & 0xFFFFFFFF
+    # one row per wave: the 64 lanes of a wave share all four (scalar) stamps
+    key = np.stack([blk, t0, a[:, 1], a[:, 2], a[:, 3]], axis=1)
+    w = np.unique(key, axis=0)
+    wb, w0, s1, s2, s3 = w[:, 0], w[:, 1], w[:, 2], w[:, 3], w[:, 4]
+    sort_c, gather_c, solve_c = s1, s2 - s1, s3 - s2
+    life = s3
+    # per block: entry of its first wave, end of its last (32-bit wrap within a block)
+    order = np.argsort(wb, kind="stable")
+    wb, w0, life = wb[order], w0[order], life[order]
+    starts = np.r_[0, np.flatnonzero(np.diff(wb)) + 1]
+    ends = np.r_[starts[1:], len(wb)]
+    idle = span_sum = 0
+    waves_per_block = []
+    for s, e in zip(starts, ends):
+        rel = (w0[s:e] - w0[s]) % (1 << 32)
+        rel = np.where(rel >= (1 << 31), rel - (1 << 32), rel)
+        b0 = rel.min()
+        fin = rel + life[s:e]
+        span = fin.max() - b0
+        idle += (fin.max() - fin).sum()
+        span_sum += span * (e - s)
+        waves_per_block.append(e - s)
+    tot = life.sum()
+    rep = {
+        "waves": int(len(w)),
+        "waves_per_block_mean": float(np.mean(waves_per_block)),
+        "wave_cycles_mean": float(life.mean()),
+        "share_sort": float(sort_c.sum() / tot),
+        "share_gather": float(gather_c.sum() / tot),
+        "share_solve": float(solve_c.sum() / tot),
+        "block_slot_idle_share": float(idle / span_sum),
+        "sort_cycles_mean": float(sort_c.mean()),
+        "gather_cycles_mean": float(gather_c.mean()),
+        "solve_cycles_mean": float(solve_c.mean()),
+        "solve_cycles_p50_p90_max": [float(np.percentile(solve_c, 50)),
+                                     float(np.percentile(solve_c, 90)), float(solve_c.max())],
+    }
+    print(json.dumps(rep, indent=1))
+    os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
+    with open(os.path.join(ROOT, "gpurun_out", "roots_stamps.json"), "w") as f:
+        json.dump(rep, f, indent=1)
+
+
+if __name__ == "__main__":
+    main()
