@@ -140,6 +140,53 @@ def solve(f, lo, hi, tau, strategy):
     return n + cnt[0], est, 0.5 * (blo + bhi)
 
 
+def model_guess(m, H, D, ice, depth, iters=3):
+    """Launch angle (deg) from a two-medium model without evaluating f: straight in air at n(Tx),
+    straight in the ice at n(|depth| / 2), Snell at the surface; Newton on the launch angle."""
+    h = H - ice
+    d = abs(depth)
+    n_tx = oracle.getnz_air(m, H)
+    n_e = oracle.getnz_ice(m, -d / 2) if d > 0 else oracle.getnz_ice(m, 0.0)
+    a = math.atan2(D, h + d)
+    for _ in range(iters):
+        L = n_tx * math.sin(a)
+        if L >= n_e:
+            break
+        q = math.sqrt(n_e * n_e - L * L)
+        g = h * math.tan(a) + d * L / q - D
+        gp = h / math.cos(a) ** 2 + d * n_tx * math.cos(a) * n_e * n_e / q ** 3
+        a = a - g / gp
+    return 180 - a * R2D
+
+
+def straddle_trips(m, H, D, d, f, lo, hi, tau, b):
+    """Trips (the paired first evaluation counted 1.3) of a search that evaluates f at the model
+    guess -+ b instead of at the bracket ends, takes the ends' signs from monotonicity when the
+    pair straddles the root, then steps by secant / IQI; None when the pair does not straddle."""
+    xm = model_guess(m, H, D, 3000.0, d)
+    xa, xb = max(lo, xm - b), min(hi, xm + b)
+    fa, fb = f(xa), f(xb)
+    if not (math.isfinite(fa) and math.isfinite(fb) and (fa < 0) != (fb < 0) and
+            abs(fa) >= tau and abs(fb) >= tau):
+        return None
+    pts = [(xa, fa), (xb, fb)]
+    steps = 0
+    while steps < 12:
+        (xB, fB), (xC, fC) = pts[-2:]
+        x2 = xC - fC * (xC - xB) / (fC - fB)
+        if len(pts) >= 3:
+            xA, fA = pts[-3]
+            d1 = (xC - xB) / (fC - fB)
+            d0 = (xB - xA) / (fB - fA)
+            x2 += fB * fC * ((d1 - d0) / (fC - fA))
+        f2 = f(x2)
+        steps += 1
+        pts.append((x2, f2))
+        if not math.isfinite(f2) or abs(f2) < tau:
+            break
+    return 1.3 + steps
+
+
 def main():
     n = int(sys.argv[1]) if len(sys.argv) > 1 else 300
     m = oracle.load_atmosphere(os.path.join(ROOT, "airiceraytracing_amd", "data",
@@ -182,6 +229,34 @@ def main():
         print(f"{s}: {np.mean(v):.3f} evaluations per solve over {len(v)} queries; root equal to "
               f"the every-midpoint bisection on {same}/{int(ok.sum())}")
     print(f"search steps (base) {np.mean(ests):.3f}")
+    # the straddling model pair: trips per solve against the kept search's
+    # (paired ends 1.3 + its search steps), a pair that does not straddle re-running the kept search
+    txh, dst, dep = cfg3_queries(4 * n, seed=2024)
+    for b in (0.003, 0.006, 0.012, 0.025):
+        base, new, miss, k = [], [], 0, 0
+        for i in range(len(txh)):
+            H, D, d = txh[i], dst[i], dep[i]
+            thR = oracle.straight_angle_of(m, H, D, 3000.0, d)
+            lo, hi = thR - 16, thR
+            if lo < 90.001:
+                continue
+
+            def f(t):
+                return D - oracle.ray_solution(m, t, H, 3000.0, d)[2]
+
+            tau = 1e-6 + 1e-10 * abs(D)
+            _, e, _ = solve(f, lo, hi, tau, "model")
+            if e is None:
+                continue
+            t = straddle_trips(m, H, D, d, f, lo, hi, tau, b)
+            miss += t is None
+            base.append(1.3 + e)
+            new.append(t if t is not None else 2.6 + e)
+            k += 1
+            if k >= n:
+                break
+        print(f"straddle b={b} deg: {np.mean(new):.3f} trips per solve against {np.mean(base):.3f} "
+              f"(pair not straddling: {miss / k:.3f})")
 
 
 if __name__ == "__main__":
