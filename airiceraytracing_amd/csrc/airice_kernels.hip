@@ -60,7 +60,7 @@ constexpr int kTableWaves = 8;
 #ifndef AIRICE_ROOTS_STAMP
 #define AIRICE_ROOTS_STAMP 0
 #endif
-constexpr int kStatsInts = AIRICE_ROOTS_STAMP ? 4 : 3;
+constexpr int kStatsInts = AIRICE_ROOTS_STAMP == 2 ? 7 : AIRICE_ROOTS_STAMP ? 4 : 3;
 // evaluation-free bisection steps of the root finder per loop trip (as compare-and-select)
 constexpr int kLeanUnroll = 4;
 // table stores take an SGPR column base and a 32-bit lane byte offset (global_store saddr form):
@@ -956,6 +956,11 @@ struct SolveResult {
   int t_setup = 0, t_lean = 0;  // debug: shader clocks of the set-up and of the lean bisection runs
   int t_pre = 0, t_post = 0;    //        loop top -> evaluation, evaluation -> loop top
 #endif
+#if AIRICE_ROOTS_STAMP == 2
+  int t_next = 0, t_eval = 0;  // debug: shader clocks in next_point and in the evaluations
+  int t_upd = 0, t_pre = 0;    //        in update, and before the loop (set-up, paired ends)
+  int t_begin = 0;             //        in the set-up (begin)
+#endif
 };
 
 enum { PH_PROBE = 0, PH_FLO = 1, PH_FHI = 2, PH_EST = 3, PH_G1 = 4, PH_G2 = 5, PH_BISECT = 6,
@@ -978,6 +983,15 @@ __device__ unsigned long long g_dbg_exec[16];
   do {              \
   } while (0)
 #endif
+
+// Shader clock for the debug stamp builds (0 on the host pass of the shared code).
+__host__ __device__ __forceinline__ unsigned long long dbg_clock() {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __builtin_amdgcn_s_memtime();
+#else
+  return 0;
+#endif
+}
 
 // Quotients and the first guess's tangent that only steer the search (the root comes from GSL's
 // bisection replay): v_rcp_f64 (~2^-24 relative) and the fast single-precision tangent on the
@@ -1238,7 +1252,7 @@ struct RootSearch {
       }
       if ((okL || okR) && lo > 0.0) {
 #if AIRICE_SCALAR_STAMP
-        const unsigned long long tl0 = __builtin_amdgcn_s_memtime();
+        const unsigned long long tl0 = dbg_clock();
 #endif
         // lean run (0 < lo < hi here): the root GSL reports after a step is 0.5 (lo + hi) of the
         // new bracket either way; the interval test reduces to hi - lo < tol lo
@@ -1281,7 +1295,7 @@ struct RootSearch {
         if (lo != lo0) f_lower = fL;
         if (hi != hi0) f_upper = fR;
 #if AIRICE_SCALAR_STAMP
-        t_lean += (int)(__builtin_amdgcn_s_memtime() - tl0) + (int)(0.0 * (lo + hi));
+        t_lean += (int)(dbg_clock() - tl0) + (int)(0.0 * (lo + hi));
 #endif
         if (done) {
           phase = PH_DONE;
@@ -1458,21 +1472,31 @@ __host__ __device__ __forceinline__ SolveResult solve_root(const DevMedium& M, c
                                                   const Geometry& g, double thR, bool exact,
                                                   const double* tab) {
 #if AIRICE_SCALAR_STAMP
-  const unsigned long long ts0 = __builtin_amdgcn_s_memtime();
+  const unsigned long long ts0 = dbg_clock();
+#endif
+#if AIRICE_ROOTS_STAMP == 2
+  const unsigned long long ts_entry = dbg_clock();
 #endif
   RootSearch s;
   s.begin(M, I, g, thR, exact);
+#if AIRICE_ROOTS_STAMP == 2
+  const unsigned long long ts_begun = dbg_clock() + (unsigned long long)(0.0 * (s.lo + s.hi + s.q.ratio));
+#endif
   if constexpr (!WAVE) s.ends_paired(M, I, tab);
 #if AIRICE_SCALAR_STAMP
-  const int t_setup = (int)(__builtin_amdgcn_s_memtime() - ts0) + (int)(0.0 * (s.lo + s.hi));
+  const int t_setup = (int)(dbg_clock() - ts0) + (int)(0.0 * (s.lo + s.hi));
   int t_pre = 0, t_post = 0;
-  unsigned long long tq = __builtin_amdgcn_s_memtime();
+  unsigned long long tq = dbg_clock();
 #endif
   // WAVE: f(lo) and f(hi), and the two guards, are independent pairs of points; the wave evaluates
   // each pair at once and keeps the second value for the next trip (the same points, the same
   // bits, two sequential evaluations fewer)
   bool have_next = false;
   double next_air = 0.0, next_ice = 0.0;
+#if AIRICE_ROOTS_STAMP == 2
+  int rs_next = 0, rs_eval = 0, rs_upd = 0;
+  const unsigned long long rs_l0 = dbg_clock() + (unsigned long long)(0.0 * (s.lo + s.hi));
+#endif
   while (s.phase != PH_DONE) {
     DBG_EXEC(0);
     if constexpr (WAVE) {
@@ -1483,7 +1507,15 @@ __host__ __device__ __forceinline__ SolveResult solve_root(const DevMedium& M, c
       s.iter = __builtin_amdgcn_readfirstlane(s.iter);
     }
     double x;
+#if AIRICE_ROOTS_STAMP == 2
+    const unsigned long long tn0 = dbg_clock();
+    const bool more = s.next_point(M, x);
+    const unsigned long long tn1 = dbg_clock() + (unsigned long long)(0.0 * x);
+    rs_next += (int)(tn1 - tn0);
+    if (!more) break;
+#else
     if (!s.next_point(M, x)) break;
+#endif
     // the single evaluation site: MinimizeforLaunchAngle (.cc:873-917)
     DBG_EXEC(4);
     double thd_air, thd_ice;
@@ -1499,26 +1531,38 @@ __host__ __device__ __forceinline__ SolveResult solve_root(const DevMedium& M, c
         const bool pair = ph == PH_FLO || ph == PH_G1;
         const double xb = ph == PH_FLO ? s.hi : s.x2 + s.dlt();
 #if AIRICE_SCALAR_STAMP
-        const unsigned long long e0 = __builtin_amdgcn_s_memtime();
+        const unsigned long long e0 = dbg_clock();
         t_pre += (int)(e0 - tq) + (int)(0.0 * x);
 #endif
         eval_thd_wave(M, I, s.q, x, pair ? xb : x, tab, thd_air, thd_ice, next_air, next_ice);
 #if AIRICE_SCALAR_STAMP
         // debug: evaluation ticks in n_inside (the wave form does not count midpoints)
-        tq = __builtin_amdgcn_s_memtime();
+        tq = dbg_clock();
         s.n_inside += (int)(tq - e0) + (int)(0.0 * (thd_air + thd_ice));
 #endif
         have_next = pair;
       }
     } else {
+#if AIRICE_ROOTS_STAMP == 2
+      const unsigned long long te0 = dbg_clock() + (unsigned long long)(0.0 * x);
       eval_thd(M, I, s.q, x, tab, thd_air, thd_ice);
+      rs_eval += (int)(dbg_clock() + (unsigned long long)(0.0 * (thd_air + thd_ice)) - te0);
+#else
+      eval_thd(M, I, s.q, x, tab, thd_air, thd_ice);
+#endif
     }
+#if AIRICE_ROOTS_STAMP == 2
+    const unsigned long long tu0 = dbg_clock() + (unsigned long long)(0.0 * (thd_air + thd_ice));
     s.template update<!WAVE>(M, x, thd_air, thd_ice);
+    rs_upd += (int)(dbg_clock() + (unsigned long long)(0.0 * (s.lo + s.hi + s.x2)) - tu0);
+#else
+    s.template update<!WAVE>(M, x, thd_air, thd_ice);
+#endif
     // f(hi) is not wanted after all when f(lo) was not finite
     if (WAVE && ph == PH_FLO && s.phase != PH_FHI) have_next = false;
 #if AIRICE_SCALAR_STAMP
     if constexpr (WAVE) {
-      const unsigned long long te = __builtin_amdgcn_s_memtime();
+      const unsigned long long te = dbg_clock();
       t_post += (int)(te - tq) + (int)(0.0 * (s.lo + s.hi + s.x2));
       tq = te;
     }
@@ -1532,7 +1576,15 @@ __host__ __device__ __forceinline__ SolveResult solve_root(const DevMedium& M, c
   sr.t_post = t_post;
   return sr;
 #else
-  return SolveResult{s.root(), s.status, s.n_eval, s.est, s.n_inside};
+  SolveResult sr{s.root(), s.status, s.n_eval, s.est, s.n_inside};
+#if AIRICE_ROOTS_STAMP == 2
+  sr.t_next = rs_next;
+  sr.t_eval = rs_eval;
+  sr.t_upd = rs_upd;
+  sr.t_pre = (int)(rs_l0 - ts_entry);
+  sr.t_begin = (int)(ts_begun - ts_entry);
+#endif
+  return sr;
 #endif
 }
 
@@ -1897,10 +1949,21 @@ __global__ __launch_bounds__(kRootsBlock, kRootsWaves) void roots_kernel(DevMedi
 #if AIRICE_ROOTS_STAMP
   const unsigned long long st3 = __builtin_amdgcn_s_memtime() + (unsigned long long)(0.0 * r.root);
   if (park.stats != nullptr) {
+#if AIRICE_ROOTS_STAMP == 2
+    // the search split: next_point, the evaluations and the rest (update, loop control)
+    park.stats[7 * k] = (int)(unsigned)st0 + 0 * (int)(st1 - st0);
+    park.stats[7 * k + 1] = (int)(st3 - st2);
+    park.stats[7 * k + 2] = r.t_eval;
+    park.stats[7 * k + 3] = r.t_next;
+    park.stats[7 * k + 4] = r.t_upd;
+    park.stats[7 * k + 5] = r.t_pre;
+    park.stats[7 * k + 6] = r.t_begin;
+#else
     park.stats[4 * k] = (int)(unsigned)st0;
     park.stats[4 * k + 1] = (int)(st1 - st0);
     park.stats[4 * k + 2] = (int)(st2 - st0);
     park.stats[4 * k + 3] = (int)(st3 - st0);
+#endif
   }
 #else
   if (park.stats != nullptr) {

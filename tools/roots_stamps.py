@@ -6,6 +6,8 @@ the block's slowest wave (a CU starts its next 1,024-query block only then).
 
     tools/build_variant.sh airiceraytracing_amd/csrc /tmp/stamp.so -DAIRICE_ROOTS_STAMP=1 ...
     python tools/roots_stamps.py /tmp/stamp.so [n]
+    (a -DAIRICE_ROOTS_STAMP=2 build with --loop: the search's time in next_point, in the
+    evaluations and in the rest of the loop, per wave)
 """
 import json
 import os
@@ -27,8 +29,43 @@ def main():
     env = dict(os.environ, AB_LIB=lib)
     subprocess.run([sys.executable, os.path.join(ROOT, "tools", "solve_stats.py"), "--child",
                     "stamp", str(n), path], env=env, check=True, timeout=300)
-    a = np.fromfile(path, dtype=np.int32).reshape(-1, 4).astype(np.int64)
-    a = a[:n]
+    if "--loop" in sys.argv:
+        a = np.fromfile(path, dtype=np.int32).reshape(-1, 7).astype(np.int64)[:n]
+        # a wave: the (scalar) entry stamp and search total; its longest-running lane saw every
+        # trip, so the wave's eval / next_point time is the maximum over its lanes, and the mean
+        # over its lanes is the time a lane spends in them (the rest: waiting for other lanes)
+        key = np.stack([np.arange(len(a)) // BLOCK, a[:, 0], a[:, 1]], axis=1)
+        _, inv = np.unique(key, axis=0, return_inverse=True)
+        inv = inv.ravel()
+        nw = inv.max() + 1
+        tot = np.zeros(nw)
+        ev_max = np.zeros(nw)
+        nx_max = np.zeros(nw)
+        up_max = np.zeros(nw)
+        pre_max = np.zeros(nw)
+        beg_max = np.zeros(nw)
+        np.maximum.at(beg_max, inv, a[:, 6])
+        np.maximum.at(tot, inv, a[:, 1])
+        np.maximum.at(ev_max, inv, a[:, 2])
+        np.maximum.at(nx_max, inv, a[:, 3])
+        np.maximum.at(up_max, inv, a[:, 4])
+        np.maximum.at(pre_max, inv, a[:, 5])
+        T = tot.sum()
+        rep = {"waves": int(nw), "search_cycles_mean": float(tot.mean()),
+               "share_eval_wave": float(ev_max.sum() / T),
+               "share_next_point_wave": float(nx_max.sum() / T),
+               "share_update_wave": float(up_max.sum() / T),
+               "share_before_loop_wave": float(pre_max.sum() / T),
+               "share_begin_wave": float(beg_max.sum() / T),
+               "share_rest_wave": float(1 - (ev_max.sum() + nx_max.sum() + up_max.sum() +
+                                             pre_max.sum()) / T),
+               "lane_active_eval_share": float(a[:, 2].sum() / (nw and a[:, 1].sum())),
+               "lane_eval_over_wave_eval": float(a[:, 2].mean() / (ev_max[inv].mean()))}
+        print(json.dumps(rep, indent=1))
+        with open(os.path.join(ROOT, "gpurun_out", "roots_stamps_loop.json"), "w") as f:
+            json.dump(rep, f, indent=1)
+        return
+    a = np.fromfile(path, dtype=np.int32).reshape(-1, 4).astype(np.int64)[:n]
     blk = np.arange(len(a)) // BLOCK
     t0 = a[:, 0] & 0xFFFFFFFF
     # one row per wave: the 64 lanes of a wave share all four (scalar) stamps
