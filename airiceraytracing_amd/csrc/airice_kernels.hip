@@ -60,7 +60,7 @@ constexpr int kTableWaves = 8;
 #ifndef AIRICE_ROOTS_STAMP
 #define AIRICE_ROOTS_STAMP 0
 #endif
-constexpr int kStatsInts = AIRICE_ROOTS_STAMP == 2 ? 7 : AIRICE_ROOTS_STAMP ? 4 : 3;
+constexpr int kStatsInts = AIRICE_ROOTS_STAMP == 3 ? 8 : AIRICE_ROOTS_STAMP == 2 ? 7 : AIRICE_ROOTS_STAMP ? 4 : 3;
 // evaluation-free bisection steps of the root finder per loop trip (as compare-and-select)
 constexpr int kLeanUnroll = 4;
 // table stores take an SGPR column base and a 32-bit lane byte offset (global_store saddr form):
@@ -956,6 +956,9 @@ struct SolveResult {
   int t_setup = 0, t_lean = 0;  // debug: shader clocks of the set-up and of the lean bisection runs
   int t_pre = 0, t_post = 0;    //        loop top -> evaluation, evaluation -> loop top
 #endif
+#if AIRICE_ROOTS_STAMP == 3
+  int tb[6] = {0, 0, 0, 0, 0, 0};
+#endif
 #if AIRICE_ROOTS_STAMP == 2
   int t_next = 0, t_eval = 0;  // debug: shader clocks in next_point and in the evaluations
   int t_upd = 0, t_pre = 0;    //        in update, and before the loop (set-up, paired ends)
@@ -1026,6 +1029,14 @@ __host__ __device__ __forceinline__ float tanf_steer(float x) {
 #endif
 }
 
+// The air model at the ice height of a batch whose queries share it (the ice end of every air
+// path), formed once per block by the kernel: x the ice height it is for, bot its layer.
+struct IceAirPre {
+  Slim s;
+  double n, x;
+  int bot;
+};
+
 // The root finder of one query as a state machine with a single evaluation site (RootSearch):
 // begin() sets up the bracket and the probe, next_point() runs the evaluation-free bisection
 // steps and returns the point to evaluate next, update() takes f there.  solve_root() below drives
@@ -1057,6 +1068,9 @@ struct RootSearch {
 #if AIRICE_SCALAR_STAMP
   int t_lean;
 #endif
+#if AIRICE_ROOTS_STAMP == 3
+  int tb[6];  // debug: set-up stamps (tx endpoint, ice endpoint + rtop, ratio, rx, probe, total)
+#endif
 
   __host__ __device__ __forceinline__ double& dlt() { return x1; }
 
@@ -1064,7 +1078,11 @@ struct RootSearch {
   // and the 0.05-degree probe.  An uninitialised solver state (non-finite bracket end) is modelled
   // as zeros.
   __host__ __device__ __forceinline__ void begin(const DevMedium& M, const IceConsts& I, const Geometry& g,
-                                        double thR, bool exact_) {
+                                        double thR, bool exact_,
+                                        const IceAirPre* pre = nullptr) {
+#if AIRICE_ROOTS_STAMP == 3
+    const unsigned long long tb0 = dbg_clock();
+#endif
     status = 0;
     exact = exact_;
 #if AIRICE_SCALAR_STAMP
@@ -1073,10 +1091,28 @@ struct RootSearch {
     q.depth_pos = g.depth_pos;
     q.dist = g.D;
     q.top = top_layer(M, g.H);
-    q.bot = bottom_layer(M, g.ice);
-    q.tx = air_slim(M, g.H, q.n_tx);
+    // the ice end: the block's copy when every lane of the wave has the batch's ice height
+    bool have_pre = false;
+    if (pre != nullptr) {
+#if defined(__HIP_DEVICE_COMPILE__)
+      have_pre = __ballot(g.ice != pre->x) == 0;
+#else
+      have_pre = g.ice == pre->x;
+#endif
+    }
     double n_ice;
-    q.iceair = air_slim(M, g.ice, n_ice);
+    if (have_pre) {
+      q.bot = pre->bot;
+      q.iceair = pre->s;
+      n_ice = pre->n;
+    } else {
+      q.bot = bottom_layer(M, g.ice);
+      q.iceair = air_slim(M, g.ice, n_ice);
+    }
+    q.tx = air_slim(M, g.H, q.n_tx);
+#if AIRICE_ROOTS_STAMP == 3
+    tb[0] = (int)(dbg_clock() + (unsigned long long)(0.0 * (q.tx.y2 + q.n_tx)) - tb0);
+#endif
     // Rx end of the top layer: the ice, or the layer's lower boundary (stop endpoint)
     const bool to_ice = q.top == q.bot;
     q.rtop = pick(to_ice, q.iceair, stop_slim(M, q.top));
@@ -1086,7 +1122,13 @@ struct RootSearch {
       q.rtop = q.tx;
       q.n_rtop = q.n_tx;
     }
+#if AIRICE_ROOTS_STAMP == 3
+    tb[1] = (int)(dbg_clock() + (unsigned long long)(0.0 * (q.rtop.y2 + q.n_rtop)) - tb0);
+#endif
     q.ratio = q.n_tx / q.n_rtop;
+#if AIRICE_ROOTS_STAMP == 3
+    tb[2] = (int)(dbg_clock() + (unsigned long long)(0.0 * q.ratio) - tb0);
+#endif
     {
       const double e = exp(M.negC_ice * g.depth_pos);
       const double y = M.A_ice + M.B_ice * e;
@@ -1094,6 +1136,9 @@ struct RootSearch {
       // argument, so it occupies no VGPRs across the loop
       q.rx = Slim{y * y, M.A_ice * y, M.negC_ice * g.depth_pos, I.ice0.invC};
     }
+#if AIRICE_ROOTS_STAMP == 3
+    tb[3] = (int)(dbg_clock() + (unsigned long long)(0.0 * q.rx.y2) - tb0);
+#endif
     lo = thR - 16;
     hi = thR;
     phase = PH_FLO;
@@ -1136,6 +1181,10 @@ struct RootSearch {
     // GSL's reported root is 0.5 (lo + hi) of the final bracket on every path (each iterate sets
     // it so, and the exact-zero exits make lo == hi), except the failed probe, which reports 0:
     // the root is formed once at the end instead of being carried through the loop
+#if AIRICE_ROOTS_STAMP == 3
+    tb[4] = (int)(dbg_clock() + (unsigned long long)(0.0 * (lo + hi)) - tb0);
+    tb[5] = phase == PH_PROBE || (status & AIRICE_SOLVE_PROBED) ? 1 : 0;
+#endif
     root_zero = probe_bad;
     f_lower = 0.0;
     f_upper = 0.0;
@@ -1470,7 +1519,8 @@ __host__ __device__ __forceinline__ void eval_thd(const DevMedium& M, const IceC
 template <bool WAVE = false>
 __host__ __device__ __forceinline__ SolveResult solve_root(const DevMedium& M, const IceConsts& I,
                                                   const Geometry& g, double thR, bool exact,
-                                                  const double* tab) {
+                                                  const double* tab,
+                                                  const IceAirPre* pre = nullptr) {
 #if AIRICE_SCALAR_STAMP
   const unsigned long long ts0 = dbg_clock();
 #endif
@@ -1478,7 +1528,7 @@ __host__ __device__ __forceinline__ SolveResult solve_root(const DevMedium& M, c
   const unsigned long long ts_entry = dbg_clock();
 #endif
   RootSearch s;
-  s.begin(M, I, g, thR, exact);
+  s.begin(M, I, g, thR, exact, pre);
 #if AIRICE_ROOTS_STAMP == 2
   const unsigned long long ts_begun = dbg_clock() + (unsigned long long)(0.0 * (s.lo + s.hi + s.q.ratio));
 #endif
@@ -1577,6 +1627,9 @@ __host__ __device__ __forceinline__ SolveResult solve_root(const DevMedium& M, c
   return sr;
 #else
   SolveResult sr{s.root(), s.status, s.n_eval, s.est, s.n_inside};
+#if AIRICE_ROOTS_STAMP == 3
+  for (int i = 0; i < 6; ++i) sr.tb[i] = s.tb[i];
+#endif
 #if AIRICE_ROOTS_STAMP == 2
   sr.t_next = rs_next;
   sr.t_eval = rs_eval;
@@ -1901,6 +1954,15 @@ __global__ __launch_bounds__(kRootsBlock, kRootsWaves) void roots_kernel(DevMedi
     s_logtab[t][1] = kLogTable[t][1];
   }
   if (threadIdx.x <= kSortBuckets) s_count[threadIdx.x] = 0;
+  // the batch's ice end, once per block (IN_TRACE queries carry their own ice height)
+  __shared__ IceAirPre s_ice;
+  constexpr bool kIcePre = IN != IN_TRACE;
+  if (kIcePre && threadIdx.x == 0) {
+    const double ice = IN == IN_M ? Q.ice : Q.ice / 100;  // load_query's ice before the shift
+    s_ice.x = ice;
+    s_ice.bot = bottom_layer(M, ice);
+    s_ice.s = air_slim(M, ice, s_ice.n);
+  }
   // bucket of this lane's own query (unused lanes last); its inputs are read while the log table
   // is staged
   int bucket = kSortBuckets;
@@ -1943,13 +2005,18 @@ __global__ __launch_bounds__(kRootsBlock, kRootsWaves) void roots_kernel(DevMedi
   const unsigned long long st2 =
       __builtin_amdgcn_s_memtime() + (unsigned long long)(0.0 * (thR + g.H + g.D + g.depth + g.ice));
 #endif
-  const SolveResult r = solve_root(M, I, g, thR, park.exact != 0, &s_logtab[0][0]);
+  const SolveResult r = solve_root(M, I, g, thR, park.exact != 0, &s_logtab[0][0],
+                                   kIcePre ? &s_ice : nullptr);
   park.root[k * park.stride] = r.root;
   park.status[k * park.stride] = (double)r.status;
 #if AIRICE_ROOTS_STAMP
   const unsigned long long st3 = __builtin_amdgcn_s_memtime() + (unsigned long long)(0.0 * r.root);
   if (park.stats != nullptr) {
-#if AIRICE_ROOTS_STAMP == 2
+#if AIRICE_ROOTS_STAMP == 3
+    park.stats[8 * k] = (int)(unsigned)st0 + 0 * (int)(st1 - st0);
+    park.stats[8 * k + 1] = (int)(st3 - st2);
+    for (int i = 0; i < 6; ++i) park.stats[8 * k + 2 + i] = r.tb[i];
+#elif AIRICE_ROOTS_STAMP == 2
     // the search split: next_point, the evaluations and the rest (update, loop control)
     park.stats[7 * k] = (int)(unsigned)st0 + 0 * (int)(st1 - st0);
     park.stats[7 * k + 1] = (int)(st3 - st2);

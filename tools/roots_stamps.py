@@ -29,6 +29,30 @@ def main():
     env = dict(os.environ, AB_LIB=lib)
     subprocess.run([sys.executable, os.path.join(ROOT, "tools", "solve_stats.py"), "--child",
                     "stamp", str(n), path], env=env, check=True, timeout=300)
+    if "--begin" in sys.argv:
+        # a -DAIRICE_ROOTS_STAMP=3 build: the set-up's cumulative stamps per wave (longest lane)
+        a = np.fromfile(path, dtype=np.int32).reshape(-1, 8).astype(np.int64)[:n]
+        key = np.stack([np.arange(len(a)) // BLOCK, a[:, 0], a[:, 1]], axis=1)
+        _, inv = np.unique(key, axis=0, return_inverse=True)
+        inv = inv.ravel()
+        nw = inv.max() + 1
+        cols = {}
+        for j, name in enumerate(["tx_endpoint", "ice_endpoint_rtop", "ratio", "rx_endpoint",
+                                  "probe_and_bracket", "probing_lanes"]):
+            v = np.zeros(nw)
+            np.maximum.at(v, inv, a[:, 2 + j])
+            cols[name] = v
+        tot = np.zeros(nw)
+        np.maximum.at(tot, inv, a[:, 1])
+        rep = {"waves": int(nw), "search_cycles_mean": float(tot.mean()),
+               "waves_with_a_probing_lane": float(cols["probing_lanes"].mean())}
+        for name in ["tx_endpoint", "ice_endpoint_rtop", "ratio", "rx_endpoint", "probe_and_bracket"]:
+            rep[name + "_cum_cycles_mean"] = float(cols[name].mean())
+        pw = cols["probing_lanes"] > 0
+        rep["probe_and_bracket_cycles_probing_waves"] = float(cols["probe_and_bracket"][pw].mean()) if pw.any() else 0.0
+        rep["probe_and_bracket_cycles_other_waves"] = float(cols["probe_and_bracket"][~pw].mean()) if (~pw).any() else 0.0
+        print(json.dumps(rep, indent=1))
+        return
     if "--loop" in sys.argv:
         a = np.fromfile(path, dtype=np.int32).reshape(-1, 7).astype(np.int64)[:n]
         # a wave: the (scalar) entry stamp and search total; its longest-running lane saw every
