@@ -129,3 +129,28 @@ def test_replay_grazing_and_layer_bounds(solvers):
     (out_f, st_f), (out_e, st_e) = _both(lambda: s.solve_host(txh, dist, depth, 3000.0))
     _same(st_f, st_e)
     _same(out_f, out_e)
+
+
+def test_block_ice_endpoint_matches_per_lane_form(solvers, oracle_medium):
+    """roots_kernel forms the batch's ice endpoint once per block and a wave takes it only when
+    every lane has that ice height; antennas above the ice shift the height and keep the per-lane
+    form.  The in-ice queries must come out bit-identical whether their waves are uniform (alone)
+    or mixed with shifted queries (interleaved), and the mixed batch must match the oracle."""
+    import oracle
+    s, _ = solvers
+    rng = np.random.default_rng(33)
+    n = 40000
+    txh = rng.uniform(3100, 60000, n)
+    dist = (txh - 3000) * rng.uniform(0.05, 5, n)
+    depth = np.where(np.arange(n) % 3 == 0, rng.uniform(0, 80, n), -rng.uniform(1, 200, n))
+    inice = depth < 0
+    out_mix, st_mix = s.solve_host(txh, dist, depth, 3000.0)
+    out_ice, st_ice = s.solve_host(txh[inice], dist[inice], depth[inice], 3000.0)
+    _same(st_mix[inice], st_ice)
+    _same(out_mix[:, inice], out_ice)
+    sub = np.arange(0, n, 7)
+    ref, rst = oracle.solve_batch(oracle_medium, txh[sub], dist[sub], depth[sub], 3000.0)
+    mask = (rst & oracle.SOLVE_UNPINNED) == 0
+    np.testing.assert_array_equal(st_mix[sub][mask] & 0x1F, rst[mask] & 0x1F)
+    rep = parity.compare_columns(out_mix[:, sub], ref, parity.SOLVE_FLOORS, mask=mask)
+    assert rep["ok"], rep
