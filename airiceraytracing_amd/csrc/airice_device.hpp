@@ -184,6 +184,17 @@ __host__ __device__ __forceinline__ Endpoint pick(bool c, const Endpoint& a, con
   return r;
 }
 
+// A result store at agent scope (device: a relaxed atomic store, i.e. global_store ... sc1, a
+// vector store); the host pass stores plainly.  Used for the kernels' streamed output columns.
+template <typename T>
+__host__ __device__ __forceinline__ void st_agent(T* p, T v) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#else
+  *p = v;
+#endif
+}
+
 // sin(asin(u)): u on the domain of asin, NaN outside it (identity (2)).
 __host__ __device__ __forceinline__ double sin_asin(double u) { return (fabs(u) <= 1.0) ? u : __builtin_nan(""); }
 

@@ -39,7 +39,10 @@ constexpr int kBlock = 256;
 #ifndef AIRICE_TABLE_BLOCK
 #define AIRICE_TABLE_BLOCK 256
 #endif
-constexpr int kTableBlock = AIRICE_TABLE_BLOCK;  // (A/B builds: -DAIRICE_TABLE_BLOCK=...)
+constexpr int kTableBlock = AIRICE_TABLE_BLOCK;
+#ifndef AIRICE_TABLE_ST
+#define AIRICE_TABLE_ST 0
+#endif  // (A/B builds: -DAIRICE_TABLE_BLOCK=...)
 constexpr int kTableWaves = 8;
 // debug builds: shader-clock stamps of the one-query kernels (tools/scalar_stamps.py,
 // tools/ray_stamps.py) and the minimizer's evaluation counts by sorted position (tools/wave_evals.py)
@@ -351,7 +354,9 @@ __device__ __forceinline__ void table_ray(const DevMedium& M, const IceConsts& I
     const size_t ldb = ld * sizeof(float);
     const uint32_t off = (uint32_t)k * 4u;
     // (non-temporal stores: cfg2 28.9 -> 29.9 us, same bits)
-    auto st = [&](int c, double v) { *reinterpret_cast<float*>(tb + c * ldb + off) = (float)v; };
+    // the column stores at agent scope (global_store ... sc1): cfg2 28.9-29.2 -> 27.8-28.2 us,
+    // the same table (without any table store the kernel takes 25.6 us: the stores' share)
+    auto st = [&](int c, double v) { st_agent(reinterpret_cast<float*>(tb + c * ldb + off), (float)v); };
     st(0, d[1]);
     st(1, d[2]);
     st(2, d[7]);
@@ -643,7 +648,7 @@ __global__ __launch_bounds__(kBlock) void rays_kernel(DevMedium M, IceConsts I,
   const bool inl = sig.n_in >= 2;  // one-ray call: its inputs in the kernel arguments
   ray_solution(M, I, inl ? sig.in[0] : launch[k], inl ? sig.in[1] : txh[k], in_ice != 0, d);
 #pragma unroll
-  for (int c = 0; c < 18; ++c) out[c * ld + k] = d[c];
+  for (int c = 0; c < 18; ++c) st_agent(out + c * ld + k, d[c]);
   if (k == 0) signal_done(sig);  // armed for one-ray calls only
 }
 
@@ -2007,8 +2012,8 @@ __global__ __launch_bounds__(kRootsBlock, kRootsWaves) void roots_kernel(DevMedi
 #endif
   const SolveResult r = solve_root(M, I, g, thR, park.exact != 0, &s_logtab[0][0],
                                    kIcePre ? &s_ice : nullptr);
-  park.root[k * park.stride] = r.root;
-  park.status[k * park.stride] = (double)r.status;
+  st_agent(park.root + k * park.stride, r.root);
+  st_agent(park.status + k * park.stride, (double)r.status);
 #if AIRICE_ROOTS_STAMP
   const unsigned long long st3 = __builtin_amdgcn_s_memtime() + (unsigned long long)(0.0 * r.root);
   if (park.stats != nullptr) {
@@ -2219,7 +2224,9 @@ __device__ __forceinline__ void stage_log_table(double (*s)[2]) {
 // WAVE (one-query kernel): every lane runs the body with the root in wr; evaluate_root_wave
 // spreads the evaluation over the wave and lane 0 writes the outputs.
 // Stage-2 output stores (non-temporal stores measured no faster)
-__host__ __device__ __forceinline__ void put_out(double* p, double v) { *p = v; }
+// (agent-scope stores: cfg3 solve call 0.2359-0.2370 -> 0.2352-0.2358 ms with the parked roots
+// stored the same way, same outputs; the lookup's non-temporal stores stay: 101.7 against 102.4 us)
+__host__ __device__ __forceinline__ void put_out(double* p, double v) { st_agent(p, v); }
 
 template <int VARIANT, bool WAVE = false>
 __host__ __device__ __forceinline__ void solve_out_body(const DevMedium& M, const IceConsts& I,

@@ -61,7 +61,8 @@ __global__ __launch_bounds__(kLkBlock) void lookup_kernel(LkTable T, const doubl
   bool good = false;
   if (!lk_query(T, src[k] / 100, dist[k] / 100, d2r, o, &good, fl, &s_win[0][threadIdx.x])) {
     // streaming result stores (non-temporal: 1e6 random queries 103.2 -> 101.6 us, L2 misses
-    // 4.05 -> 3.88 per query, same hash; non-temporal pair-record loads were 165 us)
+    // 4.05 -> 3.88 per query, same hash; non-temporal pair-record loads were 165 us, agent-scope
+    // stores 102.4 us)
 #pragma unroll
     for (int c = 0; c < 9; ++c) __builtin_nontemporal_store(o[c], out + c * ld + k);
   }
