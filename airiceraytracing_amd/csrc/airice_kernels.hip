@@ -39,10 +39,7 @@ constexpr int kBlock = 256;
 #ifndef AIRICE_TABLE_BLOCK
 #define AIRICE_TABLE_BLOCK 256
 #endif
-constexpr int kTableBlock = AIRICE_TABLE_BLOCK;
-#ifndef AIRICE_TABLE_ST
-#define AIRICE_TABLE_ST 0
-#endif  // (A/B builds: -DAIRICE_TABLE_BLOCK=...)
+constexpr int kTableBlock = AIRICE_TABLE_BLOCK;  // (A/B builds: -DAIRICE_TABLE_BLOCK=...)
 constexpr int kTableWaves = 8;
 // debug builds: shader-clock stamps of the one-query kernels (tools/scalar_stamps.py,
 // tools/ray_stamps.py) and the minimizer's evaluation counts by sorted position (tools/wave_evals.py)
