@@ -66,6 +66,8 @@ constexpr int kLeanUnroll = 4;
 // table stores take an SGPR column base and a 32-bit lane byte offset (global_store saddr form):
 // launches are split at 2^30 rays so that 4 k < 2^32
 constexpr long long kMaxLaunchRays = 1LL << 30;
+// table launches of fewer rays store their columns at agent scope (table_ray's SC1)
+constexpr long long kAgentStoreRays = 1LL << 24;
 
 // ---------------------------------------------------------------------------
 // Forward ray: GetRayTracingSolutions (.cc:1796-2017).  d[] = dummy[0..17].
@@ -327,7 +329,7 @@ __device__ __forceinline__ double table_angle(const TableArgs& G, int iang) {
   return th;
 }
 
-template <bool A1>
+template <bool A1, bool SC1>
 __device__ __forceinline__ void table_ray(const DevMedium& M, const IceConsts& I,
                                           const TableArgs& G, const RowConst& rc, int r, int k,
                                           float* __restrict__ table, double* __restrict__ full,
@@ -351,9 +353,17 @@ __device__ __forceinline__ void table_ray(const DevMedium& M, const IceConsts& I
     const size_t ldb = ld * sizeof(float);
     const uint32_t off = (uint32_t)k * 4u;
     // (non-temporal stores: cfg2 28.9 -> 29.9 us, same bits)
-    // the column stores at agent scope (global_store ... sc1): cfg2 28.9-29.2 -> 27.8-28.2 us,
-    // the same table (without any table store the kernel takes 25.6 us: the stores' share)
-    auto st = [&](int c, double v) { st_agent(reinterpret_cast<float*>(tb + c * ldb + off), (float)v); };
+    // SC1: the column stores at agent scope (global_store ... sc1), for launches short enough that
+    // the lines they leave dirty in the XCDs' L2s are a visible part of the launch: cfg2 28.9-29.2
+    // -> 27.8-28.2 us, the same table (without any table store the kernel takes 25.6 us); at cfg4
+    // size plain stores are faster (20.8 against 21.9 ms per build)
+    auto st = [&](int c, double v) {
+      float* p = reinterpret_cast<float*>(tb + c * ldb + off);
+      if constexpr (SC1)
+        st_agent(p, (float)v);
+      else
+        *p = (float)v;
+    };
     st(0, d[1]);
     st(1, d[2]);
     st(2, d[7]);
@@ -382,7 +392,7 @@ __device__ __forceinline__ void table_ray(const DevMedium& M, const IceConsts& I
 // when capped at 64, and runs 2.7x / 7x slower -- and two rays per lane.)
 // The work of one table block (kTableBlock rays of one antenna's grid), shared by the single- and
 // the multi-antenna kernels.
-template <bool TRACE, bool A1>
+template <bool TRACE, bool A1, bool SC1>
 __device__ __forceinline__ void table_block(const DevMedium& M, const IceConsts& I,
                                             const TableArgs& G, float* __restrict__ table,
                                             double* __restrict__ full,
@@ -421,7 +431,7 @@ __device__ __forceinline__ void table_block(const DevMedium& M, const IceConsts&
     __builtin_assume(top_hi >= 0);
     if (k < G.n) {
       const int r = ray_row(G, k);
-      table_ray<A1>(M, I, G, rows[r - r0], r, k, table, full, &s_logtab[0][0], top_hi);
+      table_ray<A1, SC1>(M, I, G, rows[r - r0], r, k, table, full, &s_logtab[0][0], top_hi);
     }
   }
   if (TRACE && lane == 0) {
@@ -433,13 +443,13 @@ __device__ __forceinline__ void table_block(const DevMedium& M, const IceConsts&
 }
 
 // waves_per_eu(8): 64 VGPRs at 8 waves/SIMD, measured on par or slightly ahead of 67 VGPRs at 7.
-template <bool TRACE, bool A1>
+template <bool TRACE, bool A1, bool SC1>
 __global__ __launch_bounds__(kTableBlock) __attribute__((amdgpu_waves_per_eu(kTableWaves, kTableWaves))) void table_kernel(
                                                    DevMedium M, IceConsts I, TableArgs G,
                                                    float* __restrict__ table,
                                                    double* __restrict__ full,
                                                    WaveTrace* __restrict__ trace) {
-  table_block<TRACE, A1>(M, I, G, table, full, trace, blockIdx.x);
+  table_block<TRACE, A1, SC1>(M, I, G, table, full, trace, blockIdx.x);
 }
 
 // Several antennas' tables in one grid (airice_table_launch_multi): the blocks of antenna a are
@@ -453,13 +463,13 @@ struct MultiMap {
   float* table[kMaxAntennas];
 };
 
-template <bool A1>
+template <bool A1, bool SC1>
 __global__ __launch_bounds__(kTableBlock) __attribute__((amdgpu_waves_per_eu(kTableWaves, kTableWaves))) void table_multi_kernel(
     DevMedium M, const IceConsts* __restrict__ Iv, const TableArgs* __restrict__ Gv, MultiMap map) {
   int a = 0;
   for (int j = 1; j < map.n_ant; ++j) a += (int)blockIdx.x >= map.begin[j];
   a = __builtin_amdgcn_readfirstlane(a);
-  table_block<false, A1>(M, Iv[a], Gv[a], map.table[a], nullptr, nullptr,
+  table_block<false, A1, SC1>(M, Iv[a], Gv[a], map.table[a], nullptr, nullptr,
                          blockIdx.x - (unsigned)map.begin[a]);
 }
 
@@ -2956,12 +2966,19 @@ int launch_table(const DevMedium& M, const IceConsts& I, const airice_grid* g, i
     const unsigned blocks = (unsigned)((A.n + kTableBlock - 1) / kTableBlock);
     if (trace_path == nullptr) {
       ktimer_begin(KT_TABLE, st);
-      if (M.A_air == 1.0)
-        hipLaunchKernelGGL((table_kernel<false, true>), dim3(blocks), dim3(kTableBlock), lds, st,
-                           M, I, A, tab, full, nullptr);
+      const bool sc1 = A.n < kAgentStoreRays;
+      if (M.A_air == 1.0 && sc1)
+        hipLaunchKernelGGL((table_kernel<false, true, true>), dim3(blocks), dim3(kTableBlock), lds,
+                           st, M, I, A, tab, full, nullptr);
+      else if (M.A_air == 1.0)
+        hipLaunchKernelGGL((table_kernel<false, true, false>), dim3(blocks), dim3(kTableBlock), lds,
+                           st, M, I, A, tab, full, nullptr);
+      else if (sc1)
+        hipLaunchKernelGGL((table_kernel<false, false, true>), dim3(blocks), dim3(kTableBlock), lds,
+                           st, M, I, A, tab, full, nullptr);
       else
-        hipLaunchKernelGGL((table_kernel<false, false>), dim3(blocks), dim3(kTableBlock), lds, st,
-                           M, I, A, tab, full, nullptr);
+        hipLaunchKernelGGL((table_kernel<false, false, false>), dim3(blocks), dim3(kTableBlock), lds,
+                           st, M, I, A, tab, full, nullptr);
       ktimer_end(KT_TABLE, st);
       if (hipGetLastError() != hipSuccess) return AIRICE_EHIP;
       continue;
@@ -2970,7 +2987,7 @@ int launch_table(const DevMedium& M, const IceConsts& I, const airice_grid* g, i
     const long long nw = (long long)blocks * (kTableBlock / 64);
     WaveTrace* dtr = nullptr;
     if (hipMalloc(&dtr, sizeof(WaveTrace) * nw) != hipSuccess) return AIRICE_EHIP;
-    hipLaunchKernelGGL((table_kernel<true, false>), dim3(blocks), dim3(kTableBlock), lds, st, M, I,
+    hipLaunchKernelGGL((table_kernel<true, false, true>), dim3(blocks), dim3(kTableBlock), lds, st, M, I,
                        A, tab, full, dtr);
     std::vector<WaveTrace> h(nw);
     if (hipStreamSynchronize(st) != hipSuccess ||
@@ -3106,7 +3123,9 @@ int launch_table_multi(const DevMedium& M, const IceConsts* Ih, const airice_gri
   void* dconst = c->dev;
   const size_t lds_bytes = sizeof(RowConst) * (size_t)rpb;
   ktimer_begin(KT_TABLE, st);
-  auto multi = M.A_air == 1.0 ? table_multi_kernel<true> : table_multi_kernel<false>;
+  const bool sc1 = (long long)blocks * kTableBlock < kAgentStoreRays;
+  auto multi = M.A_air == 1.0 ? (sc1 ? table_multi_kernel<true, true> : table_multi_kernel<true, false>)
+                              : (sc1 ? table_multi_kernel<false, true> : table_multi_kernel<false, false>);
   hipLaunchKernelGGL(multi, dim3((unsigned)blocks), dim3(kTableBlock),
                      lds_bytes, st, M, static_cast<const IceConsts*>(dconst),
                      reinterpret_cast<const TableArgs*>(static_cast<unsigned char*>(dconst) +
