@@ -655,7 +655,7 @@ __global__ __launch_bounds__(kBlock) void rays_kernel(DevMedium M, IceConsts I,
   const bool inl = sig.n_in >= 2;  // one-ray call: its inputs in the kernel arguments
   ray_solution(M, I, inl ? sig.in[0] : launch[k], inl ? sig.in[1] : txh[k], in_ice != 0, d);
 #pragma unroll
-  for (int c = 0; c < 18; ++c) st_agent(out + c * ld + k, d[c]);
+  for (int c = 0; c < 18; ++c) out[c * ld + k] = d[c];
   if (k == 0) signal_done(sig);  // armed for one-ray calls only
 }
 
