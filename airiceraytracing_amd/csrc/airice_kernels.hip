@@ -1888,11 +1888,13 @@ static inline int bisect_exact() {
 
 // Lanes of a wave run until its slowest query is solved, and the number of f-evaluations
 // follows the geometry (near-horizontal queries probe and need more secant steps).  So the block
-// first groups its queries by straight-line angle (a 16-bucket counting sort in LDS) and each
+// first groups its queries by straight-line angle (a 24-bucket counting sort in LDS) and each
 // lane then solves the query of its slot: waves hold similar queries (per-wave maximum 10.3 ->
 // ~8.2 evaluations on cfg3, 0.52 -> 0.45 ms per 1e6 solves).  Every query is still solved on its
 // own and written by its index.
-constexpr int kSortBuckets = 16;
+// (round 5, six alternating A/B rounds of the cfg3 solve call, same outputs: 16 buckets median
+// 0.2377 ms, 24 buckets 0.2351, 64 buckets 0.2362; 8 angle classes x the layers spanned 0.241)
+constexpr int kSortBuckets = 24;
 // 1024 queries per block: larger groups sort better, and a 16-wave block runs at 4 waves/SIMD
 // (128 VGPRs) -- measured faster than 256 (3 waves, no spills), 512 and 768; and (round 5) than
 // 512- and 256-thread blocks that each sort the whole 1,024-query chunk (a deterministic ballot
