@@ -35,11 +35,11 @@ namespace airice {
 
 namespace {
 
-static_assert(kLkBlock == 256, "lookup_kernel's LDS window (airice_lookup.hpp) and grids");
+static_assert(kLkBlock % 64 == 0, "lookup_kernel's LDS window (airice_lookup.hpp) and grids");
 
-// Occupancy: the compiler's choice (87 VGPRs = 5 waves/SIMD).  Measured (1e6 cfg3 queries,
-// tools/gpu_ab_lookup.sh, identical outputs): 6 waves (80 VGPRs, 36 B/lane spilled) 138 against
-// 124 us.  (Round 3, before the row records' trees: 7 and 8 waves with spills 166 / 175 against
+// Occupancy: the compiler's choice (97 VGPRs = 4 waves/SIMD; held to 5 waves it spills, 106 against
+// 103 us).  Round 4 (1e6 cfg3 queries, tools/gpu_ab_lookup.sh, identical outputs): 6 waves
+// (80 VGPRs, 36 B/lane spilled) 138 against 124 us.  (Round 3, before the row records' trees: 7 and 8 waves with spills 166 / 175 against
 // 152 us at 6; the two rows of GetParValues searched side by side 163 against 161 us.)
 __global__ __launch_bounds__(kLkBlock) void lookup_kernel(LkTable T, const double* __restrict__ src,
                                                           const double* __restrict__ dist,

@@ -190,7 +190,9 @@ __host__ __device__ __forceinline__ LkTxhBins lk_closest_txh(const LkTable& T, d
 // interpolation height searches (s2, e2): a query then takes its first four steps from two 128-byte
 // lines it reads anyway instead of four dependent gathers into the THD column, and the rest of
 // the search and the linear scan from one short window of that column (lk_closest_thd_tree).
-constexpr int kLkBlock = 256;      // threads per block of the batch lookup_kernel (its LDS window
+// threads per block of the batch lookup_kernel (round 5, 1e6 random queries incl. the fallback
+// pass, same outputs: 64 100.3-100.9, 128 100.6-100.9, 256 101.5-102.3, 512 104.0-104.6 us)
+constexpr int kLkBlock = 128;      // (its LDS window
                                    // has one column per thread: lk_closest_thd_tree)
 constexpr int kLkTreeNodes = 15;  // bisection steps 0-3
 constexpr int kLkWindow = 12;     // THD entries the steps 4-7 and the scan may read
