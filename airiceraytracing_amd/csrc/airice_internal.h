@@ -49,8 +49,8 @@ hipError_t scratch_alloc(void** p, size_t bytes, hipStream_t st);
 // Batch size from which the minimizer groups the queries of source `in` batch-wide
 // (AIRICE_GROUP_MIN overrides it; 0 when a source never groups by default).
 size_t group_min_batch(int in);
-// Table lookup: lookup_kernel, then the masked minimizer fallback for AIRICE_LOOKUP_FALLBACK
-// lanes (airice_lookup.hip / airice_kernels.hip).
+// Table lookup: lookup_kernel, each AIRICE_LOOKUP_FALLBACK lane solving its minimizer fallback
+// in place (airice_kernels.hip; the pack kernels: airice_lookup.hip).
 int launch_lookup(const DevMedium& M, const IceConsts& I, const airice_lookup_table* t,
                   const double* src, const double* dist, const double* depth, double ice_cm,
                   size_t n, double* out, size_t ld, uint8_t* ok, uint8_t* flags, hipStream_t st);

@@ -26,6 +26,7 @@
 #include <vector>
 
 #include "airice.h"
+#include "airice_lookup.hpp"
 #include "airice_device.hpp"
 #include "airice_internal.h"
 #include "airice_lean.hpp"
@@ -1907,7 +1908,7 @@ constexpr int kRootsWaves = 4;  // 127 VGPRs: 4 waves/SIMD (5 and 6 spill and ru
 // the other sources stay block-local, AIRICE_GROUP_MIN in the environment overrides it)
 constexpr long long kGroupMin = 65536;
 
-// Stage 2 of the lookup fallback with the root handed over in registers (lookup_fallback_kernel):
+// Stage 2 of the lookup fallback with the root handed over in registers (lookup_kernel):
 // defined below.
 __host__ __device__ __forceinline__ void fallback_out_direct(const DevMedium& M, const IceConsts& I,
                                                     const QueryArgs& Q, double* __restrict__ out,
@@ -1945,13 +1946,13 @@ __device__ __forceinline__ int query_bucket(const DevMedium& M, const QueryArgs&
   return b * kGroupHeights + (span < 0 ? 0 : (span > 3 ? 3 : span));
 }
 
-// (the table lookup's fallback solves only its flagged lanes: lookup_fallback_kernel, not this)
+// (the table lookup's fallback solves only its flagged lanes: lookup_kernel, not this)
 constexpr bool solves_every_lane(int in) { return in != IN_CM100; }
 
 template <int IN>
 __global__ __launch_bounds__(kRootsBlock, kRootsWaves) void roots_kernel(DevMedium M, IceConsts I,
                                                                          QueryArgs Q, Park park) {
-  static_assert(solves_every_lane(IN), "IN_CM100 lanes are masked: use lookup_fallback_kernel");
+  static_assert(solves_every_lane(IN), "IN_CM100 lanes are masked: use lookup_kernel");
 #if AIRICE_ROOTS_STAMP
   const unsigned long long st0 = __builtin_amdgcn_s_memtime();
 #endif
@@ -2179,7 +2180,7 @@ __global__ __launch_bounds__(kSortedBlock, kRootsWaves) void roots_sorted_kernel
   }
   __syncthreads();
   const long long ks = (long long)blockIdx.x * kSortedBlock + threadIdx.x;
-  static_assert(solves_every_lane(IN), "IN_CM100 lanes are masked: use lookup_fallback_kernel");
+  static_assert(solves_every_lane(IN), "IN_CM100 lanes are masked: use lookup_kernel");
   if (ks >= *grouped) return;  // past the queries with a bucket
   DBG_EXEC(12);
   double thR;
@@ -3234,60 +3235,8 @@ int launch_hdtip(const DevMedium& M, const IceConsts& I, const double* src, cons
   return rc;
 }
 
-// The table lookup's fallback pass: a few hundred of a batch's million queries take it, so a grid
-// over every query would be mostly waves that only read their flag and leave (the dispatch of
-// ~4k empty blocks cost ~10 us).  Each block instead scans a chunk of kFbChunk flags (coalesced
-// byte loads), lists its fallback queries in LDS and solves them, one per lane (stage 2 with the
-// root in registers, as roots_kernel<IN_CM100, 256, true>).
-constexpr int kFbBlock = 256;
-constexpr int kFbChunk = 4096;
-__global__ __launch_bounds__(kFbBlock, kRootsWaves) void lookup_fallback_kernel(
-    DevMedium M, IceConsts I, QueryArgs Q, double* __restrict__ out, size_t ld,
-    uint8_t* __restrict__ ok, int exact) {
-  __shared__ int s_list[kFbChunk];
-  __shared__ int s_n;
-  __shared__ __align__(16) double s_logtab[1 << kLogTableBits][2];
-  if (threadIdx.x == 0) s_n = 0;
-  __syncthreads();
-  const long long c0 = (long long)blockIdx.x * kFbChunk;
-  static_assert(kFbChunk == 16 * kFbBlock, "16 flags per thread");
-  const int j0 = 16 * (int)threadIdx.x;  // this thread's 16 consecutive flags
-  if (c0 + kFbChunk <= Q.n && (reinterpret_cast<uintptr_t>(Q.mask + c0) & 15) == 0) {
-    // one 16-byte load per thread (a full, aligned chunk): the scan is one round trip
-    const uint4 v = *reinterpret_cast<const uint4*>(Q.mask + c0 + j0);
-    const unsigned w[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      if (w[q] & (AIRICE_LOOKUP_FALLBACK * 0x01010101u)) {
-#pragma unroll
-        for (int b = 0; b < 4; ++b)
-          if ((w[q] >> (8 * b)) & AIRICE_LOOKUP_FALLBACK) s_list[atomicAdd(&s_n, 1)] = j0 + 4 * q + b;
-      }
-    }
-  } else {
-#pragma unroll 4
-    for (int j = j0; j < j0 + 16; ++j) {
-      const long long k = c0 + j;
-      if (k < Q.n && (Q.mask[k] & AIRICE_LOOKUP_FALLBACK)) s_list[atomicAdd(&s_n, 1)] = j;
-    }
-  }
-  __syncthreads();
-  const int cnt = s_n;
-  if (cnt == 0) return;  // block-uniform
-  for (unsigned t = threadIdx.x; t < (1u << kLogTableBits); t += kFbBlock) {
-    s_logtab[t][0] = kLogTable[t][0];
-    s_logtab[t][1] = kLogTable[t][1];
-  }
-  __syncthreads();
-  for (int i = threadIdx.x; i < cnt; i += kFbBlock) {
-    const long long k = c0 + s_list[i];
-    double thR;
-    const Geometry g = load_query<IN_CM100>(M, Q, k, thR);
-    const SolveResult r = solve_root(M, I, g, thR, exact != 0, &s_logtab[0][0]);
-    fallback_out_direct(M, I, Q, out, ld, ok, k, &s_logtab[0][0], g, r.root, r.status);
-  }
-}
-
+// The table lookup's minimizer fallback for one query (the one-query device call; a batch solves
+// its fallback lanes inside lookup_kernel).
 int launch_lookup_fallback(const DevMedium& M, const IceConsts& I, const double* src,
                            const double* dist, const double* depth, double ice_cm, size_t n,
                            double* out, size_t ld, uint8_t* ok, const uint8_t* flags,
@@ -3297,13 +3246,62 @@ int launch_lookup_fallback(const DevMedium& M, const IceConsts& I, const double*
   const double ice_arg = (ice_cm / 100) * 100;
   const QueryArgs Q{src, dist, depth, nullptr, ice_arg, (long long)n, flags};
   const Park park{out + 4 * ld, out, 1, bisect_exact(), nullptr};
-  if (n == 1) {
-    hipLaunchKernelGGL((scalar_solve_kernel<IN_CM100, OUT_FALLBACK>), dim3(1), dim3(64), 0, st, M,
-                       I, Q, park, out, ld, ok, take_scalar_signal());
-    return launch_ok();
+  if (n != 1) {
+    set_error("launch_lookup_fallback: one query (batches solve their fallback in lookup_kernel)");
+    return AIRICE_EINVAL;
   }
-  hipLaunchKernelGGL(lookup_fallback_kernel, dim3((unsigned)((n + kFbChunk - 1) / kFbChunk)),
-                     dim3(kFbBlock), 0, st, M, I, Q, out, ld, ok, park.exact);
+  hipLaunchKernelGGL((scalar_solve_kernel<IN_CM100, OUT_FALLBACK>), dim3(1), dim3(64), 0, st, M,
+                     I, Q, park, out, ld, ok, take_scalar_signal());
+  return launch_ok();
+}
+
+// GetHorizontalDistanceToIntersectionPoint_Table (.cc:1305-1462) for a batch, one query per lane:
+// lk_query (airice_lookup.hpp: row records, the THD window in LDS, pair records), and a lane whose
+// query hits the one-sided case runs the reference's minimizer fallback (.cc:1418-1420: the root
+// finder and its stage 2 with the root in registers) in place while the other waves go on with
+// their lookups.  (Round 5: a separate fallback pass after the lookup launch -- 4,096-query
+// chunks, flagged lanes listed in LDS -- waited for the whole launch and then for one solve's
+// latency: 100.8-101.8 against 93.1-93.5 us per 1e6 random queries, same outputs.)
+// 128 VGPRs (the root finder's cap, 4 waves/SIMD as the lookup alone at 97).
+__global__ __launch_bounds__(kLkBlock, kRootsWaves) void lookup_kernel(
+    LkTable T, DevMedium M, IceConsts I, QueryArgs Q, double* __restrict__ out, size_t ld,
+    uint8_t* __restrict__ ok, uint8_t* __restrict__ flags, int exact) {
+  const long long k = (long long)blockIdx.x * kLkBlock + threadIdx.x;
+  if (k >= Q.n) return;
+  if (T.ang != nullptr && *reinterpret_cast<const int*>(T.ang + (lk_angles_ok_offset(T.n, T.asteps) -
+                                                                  lk_angles_offset(T.n, T.asteps))) == 0)
+    T.ang = nullptr;
+  __shared__ float s_win[kLkWindow][kLkBlock];
+  int fl = 0;
+  double o[9];
+  bool good = false;
+  const bool fb = lk_query(T, Q.a[k] / 100, Q.b[k] / 100, M.d2r, o, &good, fl, &s_win[0][threadIdx.x]);
+  if (!fb) {
+#pragma unroll
+    for (int c = 0; c < 9; ++c) __builtin_nontemporal_store(o[c], out + c * ld + k);
+  }
+  ok[k] = good ? 1 : 0;
+  flags[k] = (uint8_t)fl;
+  if (fb) {
+    double thR;
+    const Geometry g = load_query<IN_CM100>(M, Q, k, thR);
+    const SolveResult r = solve_root(M, I, g, thR, exact != 0, &kLogTable[0][0]);
+    fallback_out_direct(M, I, Q, out, ld, ok, k, &kLogTable[0][0], g, r.root, r.status);
+  }
+}
+
+int launch_lookup(const DevMedium& M, const IceConsts& I, const airice_lookup_table* t,
+                  const double* src, const double* dist, const double* depth, double ice_cm,
+                  size_t n, double* out, size_t ld, uint8_t* ok, uint8_t* flags, hipStream_t st) {
+  if (n == 0) return AIRICE_OK;
+  const LkTable T = lk_table(t);
+  const double ice_arg = (ice_cm / 100) * 100;  // .cc:1309 in metres, .cc:1419 passes it x100
+  const QueryArgs Q{src, dist, depth, nullptr, ice_arg, (long long)n, flags};
+  const unsigned grid = (unsigned)((n + kLkBlock - 1) / kLkBlock);
+  ktimer_begin(KT_LOOKUP, st);
+  hipLaunchKernelGGL(lookup_kernel, dim3(grid), dim3(kLkBlock), 0, st, T, M, I, Q, out, ld, ok,
+                     flags, bisect_exact());
+  ktimer_end(KT_LOOKUP, st);
   return launch_ok();
 }
 

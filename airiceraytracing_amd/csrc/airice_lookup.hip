@@ -26,6 +26,7 @@
 
 #include <cmath>
 #include <cstdint>
+#include <cstdlib>
 
 #include "airice.h"
 #include "airice_internal.h"
@@ -35,43 +36,8 @@ namespace airice {
 
 namespace {
 
-static_assert(kLkBlock % 64 == 0, "lookup_kernel's LDS window (airice_lookup.hpp) and grids");
+static_assert(kLkBlock % 64 == 0, "the pack kernels' grids (airice_lookup.hpp)");
 
-// Occupancy: the compiler's choice (97 VGPRs = 4 waves/SIMD; held to 5 waves it spills, 106 against
-// 103 us).  Round 4 (1e6 cfg3 queries, tools/gpu_ab_lookup.sh, identical outputs): 6 waves
-// (80 VGPRs, 36 B/lane spilled) 138 against 124 us.  (Round 3, before the row records' trees: 7 and 8 waves with spills 166 / 175 against
-// 152 us at 6; the two rows of GetParValues searched side by side 163 against 161 us.)
-__global__ __launch_bounds__(kLkBlock) void lookup_kernel(LkTable T, const double* __restrict__ src,
-                                                          const double* __restrict__ dist,
-                                                          double ice_cm, long long n, double d2r,
-                                                          double* __restrict__ out, size_t ld,
-                                                          uint8_t* __restrict__ ok,
-                                                          uint8_t* __restrict__ flags) {
-  const long long k = (long long)blockIdx.x * kLkBlock + threadIdx.x;
-  if (k >= n) return;
-  (void)ice_cm;  // the table path never reads the ice height (.cc:1309 converts it, unused)
-  // a table whose rows have different launch angles (the pack cleared the word) reads column 4
-  if (T.ang != nullptr && *reinterpret_cast<const int*>(T.ang + (lk_angles_ok_offset(T.n, T.asteps) -
-                                                                  lk_angles_offset(T.n, T.asteps))) == 0)
-    T.ang = nullptr;
-  // the THD windows of lk_closest_thd_tree: one 4-byte column per thread
-  __shared__ float s_win[kLkWindow][kLkBlock];
-  int fl = 0;
-  double o[9];
-  bool good = false;
-  if (!lk_query(T, src[k] / 100, dist[k] / 100, d2r, o, &good, fl, &s_win[0][threadIdx.x])) {
-    // streaming result stores (non-temporal: 1e6 random queries 103.2 -> 101.6 us, L2 misses
-    // 4.05 -> 3.88 per query, same hash; non-temporal pair-record loads were 165 us, agent-scope
-    // stores 102.4 us)
-#pragma unroll
-    for (int c = 0; c < 9; ++c) __builtin_nontemporal_store(o[c], out + c * ld + k);
-  }
-  ok[k] = good ? 1 : 0;
-  flags[k] = (uint8_t)fl;
-}
-
-// airice_lookup_pack, first the angle vector: column 4 of the table's first row, and its
-// verification word set to 1 (lookup_pack_kernel clears it when another row differs).
 __global__ __launch_bounds__(kLkBlock) void lookup_angles_kernel(LkTable T, float* __restrict__ e) {
   const long long j = (long long)blockIdx.x * kLkBlock + threadIdx.x;
   float* ang = e + lk_angles_offset(T.n, T.asteps);
@@ -108,20 +74,6 @@ __global__ __launch_bounds__(kLkBlock) void lookup_rows_kernel(LkTable T, float*
     p[q] = make_float4(rec[4 * q], rec[4 * q + 1], rec[4 * q + 2], rec[4 * q + 3]);
 }
 
-LkTable lk_table(const airice_lookup_table* t) {
-  LkTable T;
-  for (int c = 0; c < AIRICE_TABLE_COLUMNS; ++c) T.col[c] = t->table + (size_t)c * t->ld;
-  T.e = t->entries;
-  T.n = (long long)t->n_entries;
-  T.stop_h = t->loop_stop_height;
-  T.step_h = t->height_step;
-  T.hsteps = t->total_height_steps;
-  T.asteps = t->total_angle_steps;
-  T.rows = T.e != nullptr ? T.n / T.asteps : 0;
-  // the angle vector; lookup_kernel drops it when the pack found a row with other angles
-  T.ang = T.e != nullptr ? T.e + lk_angles_offset(T.n, T.asteps) : nullptr;
-  return T;
-}
 
 }  // namespace
 
@@ -139,20 +91,6 @@ int launch_lookup_pack(const airice_lookup_table* t, float* e, hipStream_t st) {
     hipLaunchKernelGGL(lookup_rows_kernel, dim3((unsigned)((T.rows + kLkBlock - 1) / kLkBlock)),
                        dim3(kLkBlock), 0, st, T, e);
   return hipGetLastError() == hipSuccess ? AIRICE_OK : AIRICE_EHIP;
-}
-
-int launch_lookup(const DevMedium& M, const IceConsts& I, const airice_lookup_table* t,
-                  const double* src, const double* dist, const double* depth, double ice_cm,
-                  size_t n, double* out, size_t ld, uint8_t* ok, uint8_t* flags, hipStream_t st) {
-  if (n == 0) return AIRICE_OK;
-  const LkTable T = lk_table(t);
-  const unsigned grid = (unsigned)((n + kLkBlock - 1) / kLkBlock);
-  ktimer_begin(KT_LOOKUP, st);
-  hipLaunchKernelGGL(lookup_kernel, dim3(grid), dim3(kLkBlock), 0, st, T, src, dist, ice_cm,
-                     (long long)n, M.d2r, out, ld, ok, flags);
-  ktimer_end(KT_LOOKUP, st);
-  if (hipGetLastError() != hipSuccess) return AIRICE_EHIP;
-  return launch_lookup_fallback(M, I, src, dist, depth, ice_cm, n, out, ld, ok, flags, st);
 }
 
 }  // namespace airice

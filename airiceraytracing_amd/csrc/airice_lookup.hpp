@@ -651,4 +651,20 @@ __host__ __device__ __forceinline__ bool lk_query(const LkTable& T, double H, do
   return false;
 }
 
+// The lookup's view of a table (host: the launchers build it per call).
+inline LkTable lk_table(const airice_lookup_table* t) {
+  LkTable T;
+  for (int c = 0; c < AIRICE_TABLE_COLUMNS; ++c) T.col[c] = t->table + (size_t)c * t->ld;
+  T.e = t->entries;
+  T.n = (long long)t->n_entries;
+  T.stop_h = t->loop_stop_height;
+  T.step_h = t->height_step;
+  T.hsteps = t->total_height_steps;
+  T.asteps = t->total_angle_steps;
+  T.rows = T.e != nullptr ? T.n / T.asteps : 0;
+  // the angle vector; lookup_kernel drops it when the pack found a row with other angles
+  T.ang = T.e != nullptr ? T.e + lk_angles_offset(T.n, T.asteps) : nullptr;
+  return T;
+}
+
 }  // namespace airice

@@ -25,7 +25,7 @@ CHECKS = {
     "table": [("airice::table_kernel<false", ("roofline", "kernel_ms"))],
     "solve": [("airice::roots_kernel<0>", ("minimizer", "roots_kernel_ms")),
               ("airice::solve_out_kernel<0>", ("minimizer", "out_kernel_ms"))],
-    "lookup": [("airice::(anonymous namespace)::lookup_kernel", ("table_lookup", "lookup_kernel_ms"))],
+    "lookup": [("airice::lookup_kernel", ("table_lookup", "lookup_kernel_ms"))],
     "cfg4": [("airice::table_kernel<false", ("table_cfg4", "kernel_ms"))],
 }
 
