@@ -561,7 +561,7 @@ def main(argv=None, make_backend=None, json_path=None):
         lk_ms, lk_n = _lib.kernel_time("lookup_kernel")
         extra["table_lookup"] = {
             "metric": "GetHorizontalDistanceToIntersectionPoint_Table lookups/s (1e6 cfg3 "
-                      "queries on the cfg2 table, incl. the minimizer fallback pass)",
+                      "queries on the cfg2 table, incl. the minimizer fallback, solved in place)",
             "value": args.lookup_n / (lms * 1e-3), "unit": "lookups/s", "ms": lms,
             "lookup_kernel_ms": lk_ms / lk_n if lk_n else None,
             "ok_fraction": float(lok.cpu().numpy().mean()),
