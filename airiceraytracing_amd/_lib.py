@@ -146,6 +146,7 @@ LOOKUP_UNPINNED = 2  # AIRICE_LOOKUP_UNPINNED
 # RayTracingFunctions:: scalar ops (include/airice.h AIRICE_RTF_*)
 RTF_HIT_POINT, RTF_OPTICAL_PATH, RTF_PROPAGATION_TIME, RTF_AIR_PROPAGATION = 0, 1, 2, 3
 RTF_ICE_PROPAGATION, RTF_FDNFR, RTF_FTIMED, RTF_MIN_LAUNCH = 4, 5, 6, 7
+RTF_AIR2ICE = 8  # the Air2IceRayTracing CLI's Brent search (AIRICE_RTF_AIR2ICE_FIELDS outputs)
 # MultiRayAirIceRefraction:: forms of the ray layer (AIRICE_MR_*)
 MR_FPATHD, MR_GEOMETRIC_PATH, MR_HIT_POINT, MR_AIR_PROPAGATION = 9, 10, 11, 12
 MR_ICE_PROPAGATION, MR_MIN_LAUNCH = 13, 14
@@ -160,7 +161,8 @@ EXPORTED_SYMBOLS = (
     "airice_trace_ice_to_air_host", "airice_rtf_outputs", "airice_rtf_eval",
     "airice_rtf_eval_variant", "Py_TraceIceToAir", "airice_device_count", "airice_set_device", "airice_malloc",
     "airice_free", "airice_memcpy_h2d", "airice_memcpy_d2h", "airice_synchronize",
-    "airice_kernel_timing", "airice_kernel_time", "airice_table_cache_stats", "airice_table_to_host",
+    "airice_kernel_timing", "airice_kernel_time", "airice_launch_count",
+    "airice_table_cache_stats", "airice_table_to_host",
     "airice_host_register", "airice_host_unregister", "airice_table_checksum",
     "airice_table_save", "airice_table_file_read_info", "airice_table_load",
 )
@@ -247,6 +249,7 @@ def lib() -> ctypes.CDLL:
         "airice_kernel_timing": ([I], I),
         "airice_kernel_time": ([ctypes.c_char_p, ctypes.POINTER(D), ctypes.POINTER(ctypes.c_int64),
                                 I], I),
+        "airice_launch_count": ([ctypes.c_char_p, ctypes.POINTER(ctypes.c_int64), I], I),
     }
     for name, (args, res) in sig.items():
         fn = getattr(L, name)
@@ -315,6 +318,32 @@ def kernel_time(name: str, reset: bool = True) -> tuple[float, int]:
     check(lib().airice_kernel_time(name.encode(), ctypes.byref(ms), ctypes.byref(cnt),
                                    1 if reset else 0), "airice_kernel_time")
     return ms.value, cnt.value
+
+
+def launch_count(name: str, reset: bool = False) -> int:
+    """Launches of one kernel in this process since the last reset (airice_launch_count)."""
+    cnt = ctypes.c_int64(0)
+    check(lib().airice_launch_count(name.encode(), ctypes.byref(cnt), 1 if reset else 0),
+          "airice_launch_count")
+    return cnt.value
+
+
+class launched:
+    """``with launched("rtf_kernel") as n: ...`` -- n.count is how many launches of that kernel
+    the block made (airice_launch_count; a device test asserts it is > 0)."""
+
+    def __init__(self, name: str):
+        self.name = name
+        self.count = 0
+        self._start = 0
+
+    def __enter__(self):
+        self._start = launch_count(self.name)
+        return self
+
+    def __exit__(self, *exc):
+        self.count = launch_count(self.name) - self._start
+        return False
 
 
 def table_cache_stats() -> dict:

@@ -141,4 +141,22 @@ inline void ktimer_end(int id, hipStream_t st) {
   if (g_ktimer_on.load(std::memory_order_relaxed)) ktimer_record(id, false, st);
 }
 
+// Launch counters (airice_launch_count), always on: one relaxed increment per launch, so a test
+// can assert that the kernel it means to check ran (a host route cannot pass for a device test).
+enum LaunchId {
+  LC_TABLE = 0,     // table_kernel (single- and multi-antenna)
+  LC_RAYS,          // rays_kernel
+  LC_SCALAR_RAY,    // scalar_ray_kernel (one-query GetRayTracingSolutions)
+  LC_ROOTS,         // roots_kernel / roots_sorted_kernel (batched root finder)
+  LC_SCALAR_SOLVE,  // scalar_solve_kernel (one-query minimizer entry points)
+  LC_OUT,           // solve_out / hdtip_out / trace_out
+  LC_LOOKUP,        // lookup_kernel
+  LC_RTF,           // rtf_kernel (ray layer, GSL-Brent search)
+  LC_SINGLE_RAY,    // single_ray_kernel
+  LC_PATH,          // path_kernel
+  LC_COUNT
+};
+extern std::atomic<long long> g_launches[LC_COUNT];
+inline void count_launch(int id) { g_launches[id].fetch_add(1, std::memory_order_relaxed); }
+
 }  // namespace airice

@@ -2649,6 +2649,7 @@ static int launch_roots(const DevMedium& M, const IceConsts& I, const QueryArgs&
   if (group_min == 0 || n < group_min ||
       (park.stats != nullptr && !AIRICE_SORTED_STATS) || n >= (1ull << 31)) {
     ktimer_begin(KT_ROOTS, st);
+    count_launch(LC_ROOTS);
     hipLaunchKernelGGL((roots_kernel<IN>), roots_grid(n), dim3(kRootsBlock), 0, st, M, I, Q, park);
     ktimer_end(KT_ROOTS, st);
     return launch_ok();
@@ -2679,6 +2680,7 @@ static int launch_roots(const DevMedium& M, const IceConsts& I, const QueryArgs&
   ktimer_end(KT_GROUP, st);
   const unsigned sorted_blocks = (unsigned)((n + kSortedBlock - 1) / kSortedBlock);
   ktimer_begin(KT_ROOTS, st);
+  count_launch(LC_ROOTS);
   hipLaunchKernelGGL(roots_sorted_kernel<IN>, dim3(sorted_blocks), dim3(kSortedBlock), 0, st, M, I,
                      Q, park, recs, sorted, grouped);
   ktimer_end(KT_ROOTS, st);
@@ -2969,6 +2971,7 @@ int launch_table(const DevMedium& M, const IceConsts& I, const airice_grid* g, i
     const unsigned blocks = (unsigned)((A.n + kTableBlock - 1) / kTableBlock);
     if (trace_path == nullptr) {
       ktimer_begin(KT_TABLE, st);
+      count_launch(LC_TABLE);
       const bool sc1 = A.n < kAgentStoreRays;
       if (M.A_air == 1.0 && sc1)
         hipLaunchKernelGGL((table_kernel<false, true, true>), dim3(blocks), dim3(kTableBlock), lds,
@@ -3129,6 +3132,7 @@ int launch_table_multi(const DevMedium& M, const IceConsts* Ih, const airice_gri
   const bool sc1 = (long long)blocks * kTableBlock < kAgentStoreRays;
   auto multi = M.A_air == 1.0 ? (sc1 ? table_multi_kernel<true, true> : table_multi_kernel<true, false>)
                               : (sc1 ? table_multi_kernel<false, true> : table_multi_kernel<false, false>);
+  count_launch(LC_TABLE);
   hipLaunchKernelGGL(multi, dim3((unsigned)blocks), dim3(kTableBlock),
                      lds_bytes, st, M, static_cast<const IceConsts*>(dconst),
                      reinterpret_cast<const TableArgs*>(static_cast<unsigned char*>(dconst) +
@@ -3142,10 +3146,12 @@ int launch_rays(const DevMedium& M, const IceConsts& I, const double* launch, co
                 int in_ice, size_t n, double* out, size_t ld, hipStream_t st) {
   if (n == 0) return AIRICE_OK;
   if (n == 1) {  // one ray: spread over a wave (ray_solution_wave)
+    count_launch(LC_SCALAR_RAY);
     hipLaunchKernelGGL(scalar_ray_kernel, dim3(1), dim3(64), 0, st, M, I, launch, txh, in_ice, out,
                        ld, take_scalar_signal());
     return launch_ok();
   }
+  count_launch(LC_RAYS);
   hipLaunchKernelGGL(rays_kernel, dim3(grid_for((long long)n)), dim3(kBlock), 0, st, M, I, launch,
                      txh, in_ice, (long long)n, out, ld, Signal{});
   return launch_ok();
@@ -3177,6 +3183,7 @@ int launch_solve(const DevMedium& M, const IceConsts& I, int variant, const doub
   const dim3 grid(grid_for((long long)n)), block(kBlock);
   if (n == 1 && park.stats == nullptr) {
     const Signal sig = take_scalar_signal();
+    count_launch(LC_SCALAR_SOLVE);
     if (variant == AIRICE_VARIANT_MULTIRAY)
       hipLaunchKernelGGL((scalar_solve_kernel<IN_M, OUT_SOLVE_MR>), dim3(1), dim3(64), 0, st, M, I,
                          Q, park, out, ld, status, sig);
@@ -3200,6 +3207,7 @@ int launch_solve(const DevMedium& M, const IceConsts& I, int variant, const doub
     }
   }
   ktimer_begin(KT_OUT, st);
+  count_launch(LC_OUT);
   if (variant == AIRICE_VARIANT_MULTIRAY)
     hipLaunchKernelGGL(solve_out_kernel<AIRICE_VARIANT_MULTIRAY>, grid, block, 0, st, M, I, Q, out,
                        ld, status, sp);
@@ -3220,6 +3228,7 @@ int launch_hdtip(const DevMedium& M, const IceConsts& I, const double* src, cons
   const Park park{out + 4 * ld, out, 1, bisect_exact(), nullptr};
   const dim3 grid(grid_for((long long)n)), block(kBlock);
   if (n == 1) {
+    count_launch(LC_SCALAR_SOLVE);
     hipLaunchKernelGGL((scalar_solve_kernel<IN_CM, OUT_HDTIP>), dim3(1), dim3(64), 0, st, M, I, Q,
                        park, out, ld, ok, take_scalar_signal());
     return launch_ok();
@@ -3228,6 +3237,7 @@ int launch_hdtip(const DevMedium& M, const IceConsts& I, const double* src, cons
   RootsScratch scr(st);
   if (int rc = launch_roots<IN_CM>(M, I, Q, park, n, st, sp, scr.ws)) return rc;
   ktimer_begin(KT_OUT, st);
+  count_launch(LC_OUT);
   hipLaunchKernelGGL(hdtip_out_kernel, grid, block, 0, st, M, I, Q, out, ld, ok, sp);
   ktimer_end(KT_OUT, st);
   const int rc = launch_ok();
@@ -3250,6 +3260,7 @@ int launch_lookup_fallback(const DevMedium& M, const IceConsts& I, const double*
     set_error("launch_lookup_fallback: one query (batches solve their fallback in lookup_kernel)");
     return AIRICE_EINVAL;
   }
+  count_launch(LC_SCALAR_SOLVE);
   hipLaunchKernelGGL((scalar_solve_kernel<IN_CM100, OUT_FALLBACK>), dim3(1), dim3(64), 0, st, M,
                      I, Q, park, out, ld, ok, take_scalar_signal());
   return launch_ok();
@@ -3299,6 +3310,7 @@ int launch_lookup(const DevMedium& M, const IceConsts& I, const airice_lookup_ta
   const QueryArgs Q{src, dist, depth, nullptr, ice_arg, (long long)n, flags};
   const unsigned grid = (unsigned)((n + kLkBlock - 1) / kLkBlock);
   ktimer_begin(KT_LOOKUP, st);
+  count_launch(LC_LOOKUP);
   hipLaunchKernelGGL(lookup_kernel, dim3(grid), dim3(kLkBlock), 0, st, T, M, I, Q, out, ld, ok,
                      flags, bisect_exact());
   ktimer_end(KT_LOOKUP, st);
@@ -3312,6 +3324,7 @@ int launch_trace(const DevMedium& M, const IceConsts& I, const double* depth, co
   const Park park{out10 + 5, out10 + 9, 10, bisect_exact(), nullptr};
   const dim3 grid(grid_for((long long)n)), block(kBlock);
   if (n == 1) {
+    count_launch(LC_SCALAR_SOLVE);
     hipLaunchKernelGGL((scalar_solve_kernel<IN_TRACE, OUT_TRACE>), dim3(1), dim3(64), 0, st, M, I, Q,
                        park, out10, 0, nullptr, take_scalar_signal());
     return launch_ok();
@@ -3320,6 +3333,7 @@ int launch_trace(const DevMedium& M, const IceConsts& I, const double* depth, co
   RootsScratch scr(st);
   if (int rc = launch_roots<IN_TRACE>(M, I, Q, park, n, st, sp, scr.ws)) return rc;
   ktimer_begin(KT_OUT, st);
+  count_launch(LC_OUT);
   hipLaunchKernelGGL(trace_out_kernel, grid, block, 0, st, M, I, Q, out10, sp);
   ktimer_end(KT_OUT, st);
   const int rc = launch_ok();

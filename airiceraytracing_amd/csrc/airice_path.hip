@@ -281,9 +281,11 @@ int launch_single_ray(const DevMedium& M, const airice_medium* m, double depth, 
     return AIRICE_EINVAL;
   }
   PathConsts* c = reinterpret_cast<PathConsts*>(d_work);  // summary[] first
+  count_launch(LC_SINGLE_RAY);
   hipLaunchKernelGGL(single_ray_kernel, dim3(1), dim3(64), 0, st, M, P, c);
   if (d_x != nullptr && d_z != nullptr && n > 0) {
     const unsigned grid = (unsigned)((n + kPathBlock - 1) / kPathBlock);
+    count_launch(LC_PATH);
     hipLaunchKernelGGL(path_kernel, dim3(grid), dim3(kPathBlock), 0, st, M, P, c, d_x, d_z);
   }
   return hipGetLastError() == hipSuccess ? AIRICE_OK : AIRICE_EHIP;

@@ -774,6 +774,7 @@ int launch_rtf(const DevMedium& M, int op, const double* args, size_t n_args, do
   c.op = op;
   c.n_out = rtf_outputs(op, M.ml);
   for (int i = 0; i < 8; i++) c.a[i] = (size_t)i < n_args ? args[i] : 0.0;
+  count_launch(LC_RTF);
   hipLaunchKernelGGL(rtf_kernel, dim3(1), dim3(64), 0, st, M, c, d_out, take_scalar_signal());
   return hipGetLastError() == hipSuccess ? AIRICE_OK : AIRICE_EHIP;
 }

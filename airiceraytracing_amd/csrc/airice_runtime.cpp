@@ -162,6 +162,10 @@ thread_local FoldCache t_fold;
 }  // namespace
 
 int folded_medium(const airice_medium* m, int variant, const DevMedium** out) {
+  if (m == nullptr) {  // as build_dev_medium: the C-ABI's error contract, not a crash
+    set_error("null medium");
+    return AIRICE_EINVAL;
+  }
   FoldCache& c = t_fold;
   if (c.variant != variant || std::memcmp(&c.key, m, sizeof(*m)) != 0) {
     c.variant = -1;
@@ -223,6 +227,27 @@ static std::vector<KtPair> g_kt_done[KT_COUNT];   // closed pairs
 static KtPair g_kt_open[KT_COUNT];                // pair whose end is pending
 static const char* const kKtNames[KT_COUNT] = {"table_kernel", "roots_kernel", "group_passes",
                                                "out_kernel", "lookup_kernel"};
+
+std::atomic<long long> g_launches[LC_COUNT];
+static const char* const kLcNames[LC_COUNT] = {
+    "table_kernel",        "rays_kernel",  "scalar_ray_kernel", "roots_kernel",
+    "scalar_solve_kernel", "out_kernel",   "lookup_kernel",     "rtf_kernel",
+    "single_ray_kernel",   "path_kernel"};
+
+// AIRICE_LAUNCH_REPORT=1: the counts go to stderr when the library unloads (the CLI tests read
+// them from a child process).
+namespace {
+struct LaunchReport {
+  ~LaunchReport() {
+    const char* e = getenv("AIRICE_LAUNCH_REPORT");
+    if (e == nullptr || *e == '\0' || *e == '0') return;
+    fprintf(stderr, "airice launches:");
+    for (int i = 0; i < LC_COUNT; ++i)
+      fprintf(stderr, " %s=%lld", kLcNames[i], g_launches[i].load(std::memory_order_relaxed));
+    fprintf(stderr, "\n");
+  }
+} g_launch_report;
+}  // namespace
 
 void ktimer_record(int id, bool begin, hipStream_t st) {
   std::lock_guard<std::mutex> lock(g_kt_mu);
@@ -426,6 +451,17 @@ extern "C" int airice_table_cache_stats(int out[6]) {
 extern "C" int airice_kernel_timing(int on) {
   g_ktimer_on.store(on != 0, std::memory_order_relaxed);
   return AIRICE_OK;
+}
+
+extern "C" int airice_launch_count(const char* name, int64_t* count, int reset) {
+  for (int i = 0; i < LC_COUNT; ++i)
+    if (name != nullptr && std::strcmp(name, kLcNames[i]) == 0) {
+      const long long v = reset ? g_launches[i].exchange(0) : g_launches[i].load();
+      if (count) *count = (int64_t)v;
+      return AIRICE_OK;
+    }
+  set_error("unknown counted kernel '%s'", name ? name : "(null)");
+  return AIRICE_EINVAL;
 }
 
 extern "C" int airice_kernel_time(const char* name, double* total_ms, int64_t* launches,
@@ -652,6 +688,10 @@ int airice_solve_host(const airice_medium* m, int variant, double ice_h_m, const
   if (n == 0) return AIRICE_OK;
   if (ld < n) {
     set_error("ld < n");
+    return AIRICE_EINVAL;
+  }
+  if (m == nullptr || txh == nullptr || dist == nullptr || depth == nullptr || out == nullptr) {
+    set_error("null argument");
     return AIRICE_EINVAL;
   }
   const int fields = variant == AIRICE_VARIANT_PYWRAPPER ? AIRICE_PYSOLVE_FIELDS : AIRICE_SOLVE_FIELDS;
@@ -917,6 +957,11 @@ int airice_trace_ice_to_air_launch(const airice_medium* m, const double* d_depth
 int airice_trace_ice_to_air_host(const airice_medium* m, const double* depth, const double* ice,
                                  const double* txh, const double* dist, size_t n, double* out10) {
   if (n == 0) return AIRICE_OK;
+  if (m == nullptr || depth == nullptr || ice == nullptr || txh == nullptr || dist == nullptr ||
+      out10 == nullptr) {
+    set_error("null argument");
+    return AIRICE_EINVAL;
+  }
   if (n == 1 && airice::scalar_on_host()) {  // one query: on the host (airice_scalar_mode)
     const double in[4] = {depth[0], ice[0], txh[0], dist[0]};
     return airice::trace_query_host(m, in, out10);

@@ -243,11 +243,60 @@ def ocml_priced(grid, rays: int, kernel_ms: float) -> dict:
             "note": "library-priced work model, not executed instructions"}
 
 
+def _free_port() -> int:
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def self_launch(n: int, argv, script: str | None = None, timeout: float | None = None) -> int:
+    """``bench.py --gpus N`` (N > 1) started without torch.distributed.run's environment: start
+    ``python -m torch.distributed.run --nproc-per-node N <script> <argv>`` as a CHILD process
+    (one rank per GPU; this process never touches the GPU and never execs), relay rank 0's JSON
+    line to stdout and return the child's exit status.  ``script``: the per-rank entry (bench.py
+    itself; the CPU tests pass a rehearsal entry that runs the same main() on gloo ranks)."""
+    import subprocess
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={n}", "--master-addr", "127.0.0.1",
+           "--master-port", str(_free_port()), script or os.path.abspath(__file__), *argv]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # dmabuf IPC for RCCL on this pool
+    print(f"bench.py: --gpus {n} without RANK in the environment: launching {n} ranks: "
+          + " ".join(cmd), file=sys.stderr, flush=True)
+    p = subprocess.run(cmd, stdout=subprocess.PIPE, env=env, timeout=timeout)
+    lines = [ln for ln in p.stdout.decode(errors="replace").splitlines() if ln.startswith("{")]
+    for ln in lines[-1:]:  # exactly one JSON line, rank 0's
+        sys.stdout.write(ln + "\n")
+    sys.stdout.flush()
+    if p.returncode == 0 and len(lines) != 1:
+        print(f"bench.py: the ranks printed {len(lines)} JSON lines (want 1)", file=sys.stderr)
+        return 1
+    return p.returncode
+
+
+def check_world(args) -> None:
+    """Under torch.distributed.run (RANK set), the world must be the --gpus the caller asked for:
+    a mismatch would report a line whose n_gpus differs from the request, so it is an error."""
+    if "RANK" in os.environ:
+        world = int(os.environ.get("WORLD_SIZE", "1"))
+        if world != args.gpus:
+            print(f"bench.py: WORLD_SIZE={world} but --gpus {args.gpus}: refusing to report an "
+                  f"{world}-GPU run as {args.gpus}", file=sys.stderr, flush=True)
+            raise SystemExit(2)
+
+
 def main(argv=None, make_backend=None, json_path=None):
     """The bench.  argv: command-line arguments (default sys.argv); make_backend(local_rank):
     where the table path runs (default HipBackend); json_path: write rank 0's JSON line there
     instead of to stdout."""
     args = parse(argv)
+    if args.gpus < 1:
+        raise SystemExit("bench.py: --gpus must be >= 1")
+    if args.gpus > 1 and "RANK" not in os.environ:
+        # before torch is imported: the launching process makes no GPU call
+        raise SystemExit(self_launch(args.gpus, sys.argv[1:] if argv is None else list(argv)))
+    check_world(args)
     CFG2["height_step"] = args.height_step
     CFG4["height_step"] = args.cfg4_height_step
     os.environ.setdefault("NCCL_DEBUG", "WARN")
@@ -767,6 +816,12 @@ def main(argv=None, make_backend=None, json_path=None):
             "cpu_baseline": cpu,
             "parity_vs_cpu": parity_rep,
             "sharded": shard_rep,
+            # BASELINE cfg4 (the north_star's 8-GPU fine table), strong scaling, beside the
+            # weak-scaling headline; the full record is table_cfg4
+            "sharded_cfg4": ({k: extra["table_cfg4"].get(k) for k in (
+                "value", "unit", "scaling", "n_gpus", "ms_per_build", "value_incl_assembly",
+                "assemble", "assemble_ms", "kernel_ms_per_rank")}
+                if world > 1 and isinstance(extra.get("table_cfg4"), dict) else None),
             "minimizer": solve,
             **extra,
         }
@@ -890,7 +945,9 @@ def table_cfg4(args, be, world, rank, distributed, coll_dev, pmc) -> dict:
     rep = {"metric": "cfg4 fine table rays/s (BASELINE cfg4: MakeRayTracingTable TxH 100000->3000 "
                      "m @1 m x 90.1->180 deg @0.01 deg, antenna 200 m below 3000 m ice)",
            "rays": n, "rows": g.table_rows, "angles": asteps, "table_bytes": 44 * n,
-           "n_gpus": world, "unit": "rays/s"}
+           "n_gpus": world, "unit": "rays/s",
+           # the same 872,135,991-ray table at every N: strong scaling across the GPUs
+           "scaling": "strong"}
     host_tab = None
     if distributed:
         mode = "host" if want_host else "rccl"

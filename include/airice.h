@@ -413,6 +413,16 @@ int airice_table_load(const char *path, const airice_medium *expect, float *h_ta
 int airice_kernel_timing(int on);
 int airice_kernel_time(const char *name, double *total_ms, int64_t *launches, int reset);
 
+/* Launch counters (no reference counterpart; always on, one atomic increment per launch): how
+ * many times a kernel was launched in this process since the last reset, so a test can prove the
+ * device path it checks really ran.  Names: "table_kernel", "rays_kernel", "scalar_ray_kernel",
+ * "roots_kernel" (roots_kernel / roots_sorted_kernel), "scalar_solve_kernel" (the one-query
+ * minimizer entry points in AIRICE_SCALAR_DEVICE mode), "out_kernel", "lookup_kernel",
+ * "rtf_kernel" (ray layer and the GSL-Brent search), "single_ray_kernel", "path_kernel".
+ * AIRICE_LAUNCH_REPORT=1 in the environment prints every count to stderr when the library
+ * unloads. */
+int airice_launch_count(const char *name, int64_t *count, int reset);
+
 /* The table launch's per-grid caches on the current device (no reference counterpart; tests and
  * diagnostics).  out[0..2]: row-constant keys seen, of them filled (device buffer resident),
  * pinned (used by a launch captured into a graph); out[3..5]: the same for the start-angle

@@ -65,38 +65,81 @@ def test_cli_solve_matches_pinned_multiray_answer(oracle_medium):
 
 
 @pytest.mark.gpu
-def test_device_air2ice_matches_oracle(oracle_medium):
-    from airiceraytracing_amd import AirIceSolver
+@pytest.mark.parametrize("where", ["host", "device"])
+def test_air2ice_matches_oracle(oracle_medium, where):
+    """AIRICE_RTF_AIR2ICE (the Brent search of Air2IceRayTracing.C:137 over
+    RayTracingFunctions::FindFunctionRoot, .cc:256-290) on the calling thread (AIRICE_SCALAR_HOST)
+    and on the GPU (AIRICE_SCALAR_DEVICE: rtf_kernel, whose launches are counted so the device
+    case cannot silently run on the host) against the oracle: <= 1e-9 relative, status bits
+    and probe steps equal."""
+    from airiceraytracing_amd import AirIceSolver, _lib
+    from airiceraytracing_amd.solver import scalar_mode
     s = AirIceSolver()
     rng = np.random.default_rng(31)
     worst = 0.0
     n_cmp = 0
-    for _ in range(150):
-        args = (rng.uniform(3100, 99000), rng.uniform(0, 40000), 3000.0, rng.uniform(1, 300))
-        g = s.rtf_eval(oracle.RTF_AIR2ICE, args)
-        r = oracle.rtf_eval(oracle_medium, oracle.RTF_AIR2ICE, args)
-        assert g[12] == r[12] and g[14] == r[14] and g[15] == r[15], (args, g[12:], r[12:])
-        if int(r[12]) & (oracle.SOLVE_NONFINITE_END | oracle.SOLVE_BAD_BRACKET):
-            continue  # reference UB (uninitialised GSL state): status only
-        n_cmp += 1
-        for i in range(12):
-            if np.isnan(r[i]):
-                assert np.isnan(g[i])
+    n_calls = 0
+    mode = scalar_mode(_lib.SCALAR_HOST if where == "host" else _lib.SCALAR_DEVICE)
+    with mode, _lib.launched("rtf_kernel") as k:
+        for _ in range(150):
+            args = (rng.uniform(3100, 99000), rng.uniform(0, 40000), 3000.0, rng.uniform(1, 300))
+            g = s.rtf_eval(oracle.RTF_AIR2ICE, args)
+            n_calls += 1
+            r = oracle.rtf_eval(oracle_medium, oracle.RTF_AIR2ICE, args)
+            _check_air2ice(g, r, args)
+            if int(r[12]) & (oracle.SOLVE_NONFINITE_END | oracle.SOLVE_BAD_BRACKET):
                 continue
-            rel = abs(g[i] - r[i]) / max(abs(r[i]), 1e-6)
-            worst = max(worst, rel)
-            assert rel <= 1e-9, (args, i, g[i], r[i])
+            n_cmp += 1
+            fin = np.isfinite(r[:12]) & (np.abs(r[:12]) > 1e-6)
+            if fin.any():
+                worst = max(worst, float(np.max(np.abs(g[:12][fin] - r[:12][fin]) /
+                                                np.abs(r[:12][fin]))))
+    assert k.count == (n_calls if where == "device" else 0), (where, k.count, n_calls)
     assert n_cmp > 100
-    print(f"[air2ice] {n_cmp} solves, max rel {worst:.2e}")
+    print(f"[air2ice {where}] {n_cmp} solves, max rel {worst:.2e}")
+
+
+def _check_air2ice(g, r, args):
+    """One solve: status bits, probe steps and filled layers equal, then <= 1e-9 relative
+    unless the row is reference UB."""
+    assert g[12] == r[12] and g[14] == r[14] and g[15] == r[15], (args, g[12:], r[12:])
+    if int(r[12]) & (oracle.SOLVE_NONFINITE_END | oracle.SOLVE_BAD_BRACKET):
+        return  # reference UB (uninitialised GSL state): status only
+    for i in range(12):
+        if np.isnan(r[i]):
+            assert np.isnan(g[i])
+            continue
+        rel = abs(g[i] - r[i]) / max(abs(r[i]), 1e-6)
+        assert rel <= 1e-9, (args, i, g[i], r[i])
+
+
+def _cli_env(where):
+    return dict(os.environ, AIRICE_SCALAR=where, AIRICE_LAUNCH_REPORT="1")
+
+
+def _rtf_launches(stderr):
+    """rtf_kernel launches the child process reported at exit (AIRICE_LAUNCH_REPORT)."""
+    for line in stderr.splitlines():
+        if line.startswith("airice launches:"):
+            for tok in line.split()[2:]:
+                k, v = tok.split("=")
+                if k == "rtf_kernel":
+                    return int(v)
+    raise AssertionError(f"no launch report in stderr: {stderr!r}")
 
 
 @pytest.mark.gpu
-def test_cli_stdout(tmp_path, atmosphere_text, oracle_medium):
+@pytest.mark.parametrize("where", ["host", "device"])
+def test_cli_stdout(tmp_path, atmosphere_text, oracle_medium, where):
+    """The Air2IceRayTracing CLI with its solve on the host (AIRICE_SCALAR=host, the default) and
+    on the GPU (AIRICE_SCALAR=device: two rtf_kernel launches, the Brent search and the ice leg,
+    read from the child's launch report)."""
     assert os.path.exists(CLI), "build with __graft_entry__.build()"
     (tmp_path / "Atmosphere.dat").write_bytes(atmosphere_text)
     p = subprocess.run([CLI, "5000", "1000", "3000", "200"], cwd=tmp_path, capture_output=True,
-                       text=True, timeout=120)
+                       text=True, timeout=120, env=_cli_env(where))
     assert p.returncode == 0, p.stderr
+    assert _rtf_launches(p.stderr) == (2 if where == "device" else 0), p.stderr
     vals = {}
     for line in p.stdout.splitlines():
         parts = line.split()
@@ -123,17 +166,19 @@ def test_cli_stdout(tmp_path, atmosphere_text, oracle_medium):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("where", ["host", "device"])
 @pytest.mark.parametrize("tx,rx,dist", [(5000.0, 3100.0, 1000.0), (3100.0, 5000.0, 1000.0),
                                         (60000.0, 3000.0, 45000.0)])
-def test_air_ray_cli_stdout(tmp_path, atmosphere_text, oracle_medium, tx, rx, dist):
+def test_air_ray_cli_stdout(tmp_path, atmosphere_text, oracle_medium, tx, rx, dist, where):
     """AirRayTracing (AirRayTracing.C): the same search with the Rx in the air (no ice leg); a Tx
     below the Rx is swapped and its angles reported as 180 - angle."""
     exe = os.path.join(ROOT, "airiceraytracing_amd", "bin", "AirRayTracing")
     assert os.path.exists(exe), "build with __graft_entry__.build()"
     (tmp_path / "Atmosphere.dat").write_bytes(atmosphere_text)
     p = subprocess.run([exe, repr(tx), repr(rx), repr(dist)], cwd=tmp_path, capture_output=True,
-                       text=True, timeout=120)
+                       text=True, timeout=120, env=_cli_env(where))
     assert p.returncode == 0, p.stderr
+    assert (_rtf_launches(p.stderr) > 0) == (where == "device"), p.stderr
     got = {}
     for line in p.stdout.splitlines():
         parts = line.split()

@@ -132,6 +132,55 @@ def test_error_codes():
                                  0, None, None) == -1
 
 
+def test_one_query_host_calls_reject_null_arguments():
+    """The n == 1 host routes (AIRICE_SCALAR_HOST) keep the C-ABI's error contract: a null medium
+    or a null input / output pointer is AIRICE_EINVAL, never a dereference."""
+    from airiceraytracing_amd import _lib
+    from airiceraytracing_amd.solver import scalar_mode
+    L = _lib.lib()
+    good = _lib.load_medium()
+    one = np.array([5000.0])
+    out = np.zeros(_lib.SOLVE_FIELDS)
+    st = np.zeros(1, dtype=np.uint8)
+    p = _lib.ptr
+    with scalar_mode(_lib.SCALAR_HOST):
+        assert L.airice_solve_host(None, 0, 3000.0, p(one), p(one), p(one), None, 1, p(out), 1,
+                                   p(st)) == -1
+        assert b"null" in L.airice_last_error()
+        for args in ((None, p(one), p(one)), (p(one), None, p(one)), (p(one), p(one), None)):
+            assert L.airice_solve_host(ctypes.byref(good), 0, 3000.0, *args, None, 1, p(out), 1,
+                                       p(st)) == -1
+        assert L.airice_solve_host(ctypes.byref(good), 0, 3000.0, p(one), p(one), p(one), None, 1,
+                                   None, 1, p(st)) == -1
+        out10 = np.zeros(10)
+        assert L.airice_trace_ice_to_air_host(None, p(one), p(one), p(one), p(one), 1,
+                                              p(out10)) == -1
+        assert L.airice_trace_ice_to_air_host(ctypes.byref(good), p(one), None, p(one), p(one), 1,
+                                              p(out10)) == -1
+        assert L.airice_trace_ice_to_air_host(ctypes.byref(good), p(one), p(one), p(one), p(one),
+                                              1, None) == -1
+        assert L.airice_rtf_eval(None, 3, p(np.array([170.0, 20000.0, 3000.0])), 3, p(out),
+                                 out.size) == -1
+
+
+def test_launch_counters():
+    """airice_launch_count: every documented name answers (0 here: no kernel ran on this CPU
+    box), an unknown one is AIRICE_EINVAL."""
+    from airiceraytracing_amd import _lib
+    for name in ("table_kernel", "rays_kernel", "scalar_ray_kernel", "roots_kernel",
+                 "scalar_solve_kernel", "out_kernel", "lookup_kernel", "rtf_kernel",
+                 "single_ray_kernel", "path_kernel"):
+        assert _lib.launch_count(name) == 0, name
+    cnt = ctypes.c_int64(7)
+    assert _lib.lib().airice_launch_count(b"no_such_kernel", ctypes.byref(cnt), 0) == -1
+    # the one-query host route launches nothing
+    from airiceraytracing_amd.solver import AirIceSolver, scalar_mode
+    s = AirIceSolver()
+    with scalar_mode(_lib.SCALAR_HOST), _lib.launched("scalar_solve_kernel") as k:
+        out, st = s.solve_host(np.array([5000.0]), np.array([1000.0]), np.array([-200.0]), 3000.0)
+    assert k.count == 0 and abs(out[10, 0] - 154.70167146999108) < 1e-9 * 155
+
+
 def test_no_cpu_fallback_when_library_missing(monkeypatch, tmp_path):
     from airiceraytracing_amd import _lib
     monkeypatch.setattr(_lib, "_lib", None)

@@ -262,3 +262,62 @@ def test_gloo_world8_bench_flow(tmp_path, cfg4_host):
         assert c4["assemble"] == "rccl" and "IsADirectoryError" in c4["host_assembly_error"]
     else:
         assert c4["assemble"] == "host" and "host_assembly_error" not in c4
+
+
+BENCH2 = ["--gpus", "2", "--steps", "2", "--warmup", "1", "--height-step", "400",
+          "--no-cfg4", "--no-cpu", "--no-solve", "--no-trace", "--no-lookup", "--no-multi",
+          "--no-scalar", "--no-default-grid", "--no-cold", "--no-pcie"]
+
+
+def test_bench_world_size_mismatch_exits_nonzero(monkeypatch):
+    """Under torch.distributed.run, WORLD_SIZE != --gpus is refused before any rendezvous or
+    device work: exit status 2, no JSON line."""
+    import bench
+    monkeypatch.setenv("RANK", "0")
+    monkeypatch.setenv("WORLD_SIZE", "2")
+    monkeypatch.setenv("LOCAL_RANK", "0")
+    for gpus in ("3", "1"):
+        argv = ["--gpus", gpus] + BENCH2[2:]
+        with pytest.raises(SystemExit) as e:
+            bench.main(argv, make_backend=lambda r: pytest.fail("backend built"))
+        assert e.value.code == 2
+
+
+def test_bench_self_launch_two_ranks(monkeypatch, capsys):
+    """``bench.py --gpus 2`` with no RANK in the environment starts torch.distributed.run with two
+    ranks as a child process (gloo here, the CPU rehearsal backend standing in for the kernels)
+    and relays rank 0's single JSON line: n_gpus 2, the sharded table bitwise equal to the whole
+    grid."""
+    import json
+    import bench
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK"):
+        monkeypatch.delenv(k, raising=False)
+    entry = os.path.join(os.path.dirname(os.path.abspath(__file__)), "bench_rehearsal_entry.py")
+    rc = bench.self_launch(2, BENCH2, script=entry, timeout=300)
+    out = capsys.readouterr().out
+    assert rc == 0, out
+    lines = [ln for ln in out.splitlines() if ln.strip()]
+    assert len(lines) == 1, lines
+    line = json.loads(lines[0])
+    assert line["n_gpus"] == 2 and line["rccl_world_size"] == 2 and line["dist_backend"] == "gloo"
+    assert line["scaling"] == "weak" and line["value"] > 0
+    assert line["sharded"]["assembled_bitwise_equal_single_gpu"] is True
+    assert len(line["kernel_ms_per_rank"]) == 2
+
+
+def test_bench_main_self_launches_without_rank(monkeypatch):
+    """bench.main(--gpus 2) outside torch.distributed.run goes to self_launch before importing
+    torch (no backend is built in the launching process) and exits with its status."""
+    import bench
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK"):
+        monkeypatch.delenv(k, raising=False)
+    seen = {}
+
+    def fake(n, argv, script=None, timeout=None):
+        seen.update(n=n, argv=list(argv))
+        return 0
+
+    monkeypatch.setattr(bench, "self_launch", fake)
+    with pytest.raises(SystemExit) as e:
+        bench.main(BENCH2, make_backend=lambda r: pytest.fail("backend built"))
+    assert e.value.code == 0 and seen == {"n": 2, "argv": BENCH2}

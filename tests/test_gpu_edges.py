@@ -74,13 +74,35 @@ def test_tables_skip_nonpositive_tx_rows(solver, oracle_medium, depth_cm, ice_cm
     assert parity.float_ulp_diff(table, ot) <= 1
 
 
-def test_single_query_batches(solver, oracle_medium):
-    """n = 1 through the batched minimizer (one lane in a 1024-query sort block)."""
+@pytest.mark.parametrize("where", ["host", "device"])
+def test_single_query_batches(solver, oracle_medium, where):
+    """n = 1 through airice_solve_host: on the calling thread in AIRICE_SCALAR_HOST mode (no
+    kernel), on the GPU's one-query kernel (scalar_solve_kernel) in AIRICE_SCALAR_DEVICE mode --
+    the launch counters prove which ran -- and, on the device, bit for bit the same query inside
+    a batch (n = 2: roots_kernel + solve_out_kernel)."""
+    from airiceraytracing_amd import _lib
+    from airiceraytracing_amd.solver import scalar_mode
+    mode = _lib.SCALAR_HOST if where == "host" else _lib.SCALAR_DEVICE
     for txh, dist, depth in ((5000.0, 1000.0, -200.0), (99999.0, 49999.0, -300.0),
                              (3001.0, 0.0, -0.5), (20000.0, 5000.0, 10.0)):
-        out, st = solver.solve_host(np.array([txh]), np.array([dist]), np.array([depth]), 3000.0)
+        with scalar_mode(mode), _lib.launched("scalar_solve_kernel") as k1, \
+                _lib.launched("roots_kernel") as kr:
+            out, st = solver.solve_host(np.array([txh]), np.array([dist]), np.array([depth]),
+                                        3000.0)
+        assert k1.count == (1 if where == "device" else 0) and kr.count == 0
         ref, rst = oracle.solve_batch(oracle_medium, np.array([txh]), np.array([dist]),
                                       np.array([depth]), 3000.0)
         mask = (rst & oracle.SOLVE_UNPINNED) == 0
         rep = parity.compare_columns(out, ref, parity.SOLVE_FLOORS, mask=mask)
         assert rep["ok"], (txh, dist, depth, rep)
+        assert st[0] == rst[0]
+        with _lib.launched("roots_kernel") as kr:
+            pair, pst = solver.solve_host(np.array([txh, txh]), np.array([dist, dist]),
+                                          np.array([depth, depth]), 3000.0)
+        assert kr.count == 1
+        if where == "device":
+            assert np.array_equal(out[:, 0].view(np.int64), pair[:, 0].view(np.int64))
+            assert np.array_equal(out[:, 0].view(np.int64), pair[:, 1].view(np.int64))
+            assert st[0] == pst[0] == pst[1]
+        else:  # the host's libm and correctly rounded quotients: within about an ulp
+            np.testing.assert_allclose(out[:, 0], pair[:, 0], rtol=1e-12, atol=1e-12)

@@ -128,15 +128,56 @@ def test_host_matches_device(oracle_medium):
     from airiceraytracing_amd.solver import scalar_mode
     s = AirIceSolver()
     worst = 0.0
-    for op, args in _rtf_cases(oracle_medium, 60, seed=8):
-        host = s.rtf_eval(op, args)
-        with scalar_mode(_lib.SCALAR_DEVICE):
-            dev = s.rtf_eval(op, args)
-        _close(host, dev, floor=1e-6, rtol=1e-12)
-        fin = np.isfinite(dev) & (np.abs(dev) > 1e-6)
-        if fin.any():
-            worst = max(worst, float(np.max(np.abs(host[fin] - dev[fin]) / np.abs(dev[fin]))))
+    cases = _rtf_cases(oracle_medium, 60, seed=8)
+    with _lib.launched("rtf_kernel") as k:
+        for op, args in cases:
+            with scalar_mode(_lib.SCALAR_HOST):
+                host = s.rtf_eval(op, args)
+            with scalar_mode(_lib.SCALAR_DEVICE):
+                dev = s.rtf_eval(op, args)
+            _close(host, dev, floor=1e-6, rtol=1e-12)
+            fin = np.isfinite(dev) & (np.abs(dev) > 1e-6)
+            if fin.any():
+                worst = max(worst, float(np.max(np.abs(host[fin] - dev[fin]) / np.abs(dev[fin]))))
+    assert k.count == len(cases)  # one rtf_kernel per device call, none for the host calls
     assert worst < 1e-12, worst
+
+
+@pytest.mark.gpu
+def test_air2ice_host_matches_device(oracle_medium):
+    """AIRICE_RTF_AIR2ICE (the Air2IceRayTracing CLI's GSL-Brent search, Air2IceRayTracing.C:137)
+    on the host and on the GPU: the same status bits, probe steps and filled layers; the roots
+    within the 1e-9 contract of each other (a last-ulp difference in f can move one Brent step),
+    and both within 1e-9 of the oracle.  Rx in the ice and in the air (AirRayTracing.C)."""
+    from airiceraytracing_amd import AirIceSolver, _lib
+    from airiceraytracing_amd.solver import scalar_mode
+    s = AirIceSolver()
+    rng = np.random.default_rng(44)
+    same_bits = 0
+    n = 0
+    with _lib.launched("rtf_kernel") as k:
+        for _ in range(80):
+            if rng.uniform() < 0.75:
+                args = [rng.uniform(3100, 99000), rng.uniform(0, 40000), rng.choice([3000.0, 0.0]),
+                        rng.uniform(1, 300)]
+            else:
+                args = [rng.uniform(3100, 60000), rng.uniform(0, 45000), rng.uniform(0, 3000), 0.0]
+            with scalar_mode(_lib.SCALAR_HOST):
+                host = s.rtf_eval(_lib.RTF_AIR2ICE, args)
+            with scalar_mode(_lib.SCALAR_DEVICE):
+                dev = s.rtf_eval(_lib.RTF_AIR2ICE, args)
+            n += 1
+            ref = oracle.rtf_eval(oracle_medium, _lib.RTF_AIR2ICE, args)
+            assert host[12] == dev[12] == ref[12], (args, host[12:], dev[12:], ref[12:])
+            assert host[14] == dev[14] and host[15] == dev[15], (args, host[12:], dev[12:])
+            same_bits += int(np.array_equal(host[:12].view(np.int64), dev[:12].view(np.int64)))
+            if int(ref[12]) & (oracle.SOLVE_NONFINITE_END | oracle.SOLVE_BAD_BRACKET):
+                continue  # reference UB: status only
+            _close(dev[:12], ref[:12], floor=1e-6)
+            _close(host[:12], ref[:12], floor=1e-6)
+            _close(host[:12], dev[:12], floor=1e-6)
+    assert k.count == n
+    print(f"[air2ice host/device] {n} solves, {same_bits} bit-identical")
 
 
 @pytest.mark.gpu

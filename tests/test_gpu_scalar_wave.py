@@ -114,3 +114,38 @@ def test_one_ray_matches_the_batch():
         bad = np.flatnonzero(~np.all(a.view(np.int64) == b.view(np.int64), axis=0))
         assert bad.size == 0, (ice_m, depth_m, bad[:10], a[:, bad[:2]], b[:, bad[:2]])
         assert np.isnan(a[2]).any() and np.isfinite(a[2]).any()
+
+
+def test_one_query_inside_a_1e6_batch():
+    """BASELINE cfg3 (1e6 queries, seed 12345): queries picked across the batch -- every status
+    class the batch produced among them -- solved one at a time through the C-ABI's one-query
+    route in AIRICE_SCALAR_DEVICE mode (scalar_solve_kernel, counted) equal the batch's
+    roots_kernel + solve_out_kernel outputs bit for bit."""
+    import torch
+    from airiceraytracing_amd import AirIceSolver, _lib
+    from airiceraytracing_amd.solver import scalar_mode
+    dev = torch.device("cuda:0")
+    s = AirIceSolver()
+    txh, dist, dep = parity.cfg3_queries(1_000_000)
+    t, d, p = [torch.from_numpy(a).to(dev) for a in (txh, dist, dep)]
+    n = t.numel()
+    out = torch.empty((17, n), dtype=torch.float64, device=dev)
+    st = torch.empty(n, dtype=torch.uint8, device=dev)
+    with _lib.launched("roots_kernel") as kr:
+        s.solve_device(t, d, p, 3000.0, out, st)
+        torch.cuda.synchronize()
+    assert kr.count == 1
+    a, sa = out.cpu().numpy(), st.cpu().numpy()
+    pick = list(np.linspace(0, n - 1, 40).astype(int))
+    for bit in (1, 2, 4, 8, 16, 32):  # a few queries of each status bit present
+        pick += list(np.flatnonzero(sa & bit)[:4])
+    pick = sorted(set(int(i) for i in pick))
+    with scalar_mode(_lib.SCALAR_DEVICE), _lib.launched("scalar_solve_kernel") as k1:
+        for i in pick:
+            o, so = s.solve_host(txh[i:i + 1], dist[i:i + 1], dep[i:i + 1], 3000.0)
+            assert np.array_equal(o[:, 0].view(np.int64), a[:, i].view(np.int64)), (i, o[:, 0],
+                                                                                     a[:, i])
+            assert so[0] == sa[i], (i, so[0], sa[i])
+    assert k1.count == len(pick)
+    print(f"[n=1 vs 1e6 batch] {len(pick)} queries bit-identical, status classes "
+          f"{sorted(set(int(sa[i]) for i in pick))}")
