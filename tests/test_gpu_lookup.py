@@ -174,3 +174,55 @@ def test_lookup_empty_batch(solver):
     solver.table_lookup_device(solver.lookup_table(table, g), e, e, e, ICE_CM,
                                torch.empty((9, 0), dtype=torch.float64, device="cuda:0"), u, u)
     torch.cuda.synchronize()
+
+
+def test_lookup_pack_angle_vector_fallback(solver, oracle_medium):
+    """Pack format 2's angle vector is used only when every row's column 4 equals row 0's bit for
+    bit; a table where one row differs (perturbed by one float ulp here) gets verification word 0,
+    and lookup_kernel then reads column 4 itself: outputs, ok and flags bit-identical to the
+    unpacked (entries = NULL) column path, and to the oracle on the same floats."""
+    import torch
+    from airiceraytracing_amd import _lib
+    g, table = _device_table(solver, -20000.0, 100.0, 92.0, 180.0, 0.5)
+    asteps = g.angle_steps
+    row = g.table_rows // 2
+    c4 = table[4, row * asteps:(row + 1) * asteps]
+    table[4, row * asteps:(row + 1) * asteps] = torch.nextafter(c4, torch.full_like(c4, 1e9))
+    torch.cuda.synchronize()
+    host = table.cpu().numpy()
+    assert not np.array_equal(host[4][row * asteps:(row + 1) * asteps], host[4][:asteps])
+    src, dist = parity.lookup_queries(host, 20000, seed=17)
+    n = src.size
+    dev = torch.device("cuda:0")
+    dep = np.full(n, -20000.0)
+    ts, td, tp = (torch.from_numpy(a).to(dev) for a in (src, dist, dep))
+    res = []
+    for packed in (False, True):
+        lt = solver.lookup_table(table, g)
+        if packed:
+            solver.lookup_pack(lt, stream=torch.cuda.current_stream())
+            torch.cuda.synchronize()
+            flat = lt._packed.cpu().numpy()
+            ne = host.shape[1]
+            a0 = _lib.lookup_rows_offset(ne) + (ne // asteps) * _lib.LOOKUP_ROW_FLOATS
+            assert flat[a0 + (asteps + 3) // 4 * 4:].view(np.int32)[0] == 0  # not verified
+        out = torch.empty((9, n), dtype=torch.float64, device=dev)
+        ok = torch.empty(n, dtype=torch.uint8, device=dev)
+        fl = torch.empty(n, dtype=torch.uint8, device=dev)
+        with _lib.launched("lookup_kernel") as k:
+            solver.table_lookup_device(lt, ts, td, tp, ICE_CM, out, ok, fl,
+                                       stream=torch.cuda.current_stream())
+            torch.cuda.synchronize()
+        assert k.count == 1
+        res.append((out.cpu().numpy(), ok.cpu().numpy(), fl.cpu().numpy()))
+    assert np.array_equal(res[0][0].view(np.int64), res[1][0].view(np.int64))
+    assert np.array_equal(res[0][1], res[1][1]) and np.array_equal(res[0][2], res[1][2])
+    og = oracle.grid_init(-20000.0, ICE_CM, 100.0, 92.0, 180.0, 0.5)
+    rout, rok, rfl = oracle.table_lookup_batch(oracle_medium, oracle.lookup_table(host, og),
+                                               src, dist, dep, ICE_CM, nthreads=NTHREADS)
+    out, ok, fl = res[1]
+    assert np.array_equal(fl, rfl)
+    nf = (rfl & oracle.LOOKUP_FALLBACK) == 0
+    a, b = out[:, nf], rout[:, nf]
+    assert ((a == b) | (np.isnan(a) & np.isnan(b))).all()
+    assert np.array_equal(ok[nf], rok[nf])
