@@ -12,12 +12,14 @@
  * and degrees throughout, Air2IceRayTracing's own 15-slot output layout (.cc:1070-1084).
  *
  * Where each function runs:
- *   - GPU: Air2IceRayTracing (.cc:929), GetRayTracingSolution (.cc:884), TraceIceToAir
- *     (TraceIceToAir.C:5) and the ray layer (fDnfR, ftimeD, fpathD, GetRay{Horizontal,Geometric}Path,
- *     GetRayPropagationTime, GetLayerHitPointPar, Get{Air,Ice}PropagationPar,
- *     MinimizeforLaunchAngle), one query per call through the pinned scalar slot (one launch, the
- *     kernel signals completion); batches belong on airice_solve_launch(AIRICE_VARIANT_PYWRAPPER)
- *     and airice_trace_ice_to_air_launch.
+ *   - One query per call, on the calling CPU thread by default: Air2IceRayTracing (.cc:929),
+ *     GetRayTracingSolution (.cc:884), TraceIceToAir (TraceIceToAir.C:5) and the ray layer (fDnfR,
+ *     ftimeD, fpathD, GetRay{Horizontal,Geometric}Path, GetRayPropagationTime,
+ *     GetLayerHitPointPar, Get{Air,Ice}PropagationPar, MinimizeforLaunchAngle), from the same
+ *     __host__ __device__ source as the GPU kernels (host sqrt and quotients: within about an ulp
+ *     of a GPU batch's result).  AIRICE_SCALAR=device (airice_scalar_mode) runs each on a one-wave
+ *     GPU kernel through the pinned scalar slot instead, bit-identical to the batch.  Batches run
+ *     on the GPU: airice_solve_launch(AIRICE_VARIANT_PYWRAPPER), airice_trace_ice_to_air_launch.
  *   - Host: the atmosphere readers, n(z) and the layer scans, Fresnel coefficients, and
  *     FindFunctionRoot (GSL bisection / Brent on the caller's host function, airice_gsl_roots.h).
  *

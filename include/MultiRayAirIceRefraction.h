@@ -7,18 +7,25 @@
  * `#include "MultiRayAirIceRefraction.cc"` line.
  *
  * Where each function runs:
- *   - GPU batch kernels: MakeRayTracingTable (.cc:2019), GetRayTracingSolutions (.cc:1796),
- *     Air2IceRayTracing (.cc:1464), GetHorizontalDistanceToIntersectionPoint (.cc:945) and the
- *     ray layer (fDnfR, ftimeD, fpathD, GetRay{Horizontal,Geometric}Path, GetRayPropagationTime,
- *     GetLayerHitPointPar, Get{Air,Ice}PropagationPar, MinimizeforLaunchAngle), one query per
- *     call through a pinned, device-mapped staging slot (one launch chain + one synchronisation).
+ *   - GPU, always: MakeRayTracingTable (.cc:2019) and the extensions MakeRayTracingTables and
+ *     TableLookupBatch below -- the batch entry points (one launch chain per call).
+ *   - The calling CPU thread, by default (airice_scalar_mode, include/airice.h): every one-query
+ *     call -- GetRayTracingSolutions (.cc:1796), Air2IceRayTracing (.cc:1464),
+ *     GetHorizontalDistanceToIntersectionPoint (.cc:945) and the ray layer (fDnfR, ftimeD,
+ *     fpathD, GetRay{Horizontal,Geometric}Path, GetRayPropagationTime, GetLayerHitPointPar,
+ *     Get{Air,Ice}PropagationPar, MinimizeforLaunchAngle).  They are compiled from the same
+ *     __host__ __device__ source as the GPU kernels, with the host's correctly rounded sqrt and
+ *     quotients, so a result can differ from the same query inside a GPU batch by about an ulp
+ *     (within the 1e-9 contract; the launch angle is the same GSL bisection's).
+ *     AIRICE_SCALAR=device in the environment, or airice_scalar_mode(AIRICE_SCALAR_DEVICE), sends
+ *     them to one-wave GPU kernels instead (bit-identical to the batch, ~10-20 us per call).
  *   - Host, from the same source the batch lookup kernel is compiled from (airice_lookup.hpp):
  *     GetHorizontalDistanceToIntersectionPoint_Table (.cc:1305), GetParValues (.cc:1172),
  *     FindClosestAirTxHeight (.cc:1033), FindClosestTHD (.cc:1128) -- table walks over the
  *     caller's host AllTableAllAntData, bit-identical to the device lookup; a query that reaches
- *     the reference's minimizer fallback (.cc:1418) runs that solve on the GPU.  Extrapolate /
- *     FindExtrapolationLimit (.cc:997-1031) and the atmosphere file readers are host code as in
- *     the reference.
+ *     the reference's minimizer fallback (.cc:1418) runs that solve where the mode above says.
+ *     Extrapolate / FindExtrapolationLimit (.cc:997-1031) and the atmosphere file readers are host
+ *     code as in the reference.
  *
  * FindFunctionRoot (.cc:340-374) keeps its GSL-typed signature (airice_gsl_roots.h) and runs GSL's
  * bisection / Brent on the caller's host function.  Not provided: the gsl_interp_accel /
@@ -111,7 +118,7 @@ double Trans_S(double thetai, double IceLayerHeight);
 double Refl_P(double thetai, double IceLayerHeight);
 double Trans_P(double thetai, double IceLayerHeight);
 
-/* CoREAS entry (cm in, cm/rad out), solved on the GPU. */
+/* CoREAS entry (cm in, cm/rad out): one query, on the calling thread (see above). */
 bool GetHorizontalDistanceToIntersectionPoint(
     double SrcHeightASL, double HorizontalDistanceToRx, double RxDepthBelowIceBoundary,
     double IceLayerHeight, double& opticalPathLengthInIce, double& opticalPathLengthInAir,
@@ -125,7 +132,7 @@ double oneDLinearInterpolation(double x, double xa, double ya, double xb, double
 double FindFunctionRoot(gsl_function F, double x_lo, double x_hi, const gsl_root_fsolver_type* T,
                         double tolerance);
 
-/* The ray layer (.cc:377-917), evaluated on the GPU.  *Par functions return new[]'d arrays the
+/* The ray layer (.cc:377-917), one query per call (see above).  *Par functions return new[]'d arrays the
  * caller delete[]s, as with the reference: GetLayerHitPointPar / GetIcePropagationPar 5 doubles
  * {THD, receive angle deg, L, time s, geometric path}; GetAirPropagationPar 5 x MaxLayers + 2,
  * per layer the same five, the filled-layer count at [5 * MaxLayers + 1]. */

@@ -7,9 +7,12 @@
  *     L, time (s)}; GetAirPropagationPar returns new double[4*MaxLayers+1] with the filled-layer
  *     count at [4*MaxLayers].  The caller delete[]s them, as with the reference.
  *   - Every ray quantity (fDnfR, ftimeD, GetRayOpticalPath, GetRayPropagationTime, the three
- *     *Par functions, MinimizeforLaunchAngle) is evaluated on the GPU with the reference's
- *     expressions, one call per launch (airice_rtf_eval, include/airice.h).  Batches belong on
- *     the batched C-ABI (airice_single_ray_*, airice_solve_*, airice_table_*).
+ *     *Par functions, MinimizeforLaunchAngle) is one query per call with the reference's
+ *     expressions (airice_rtf_eval, include/airice.h), on the calling CPU thread by default; with
+ *     AIRICE_SCALAR=device (or airice_scalar_mode(AIRICE_SCALAR_DEVICE)) on a one-wave GPU
+ *     kernel per call.  The host form is the same __host__ __device__ source with the host's
+ *     correctly rounded sqrt and quotients: within about an ulp of the GPU's.  Batches run on the
+ *     GPU through the batched C-ABI (airice_single_ray_*, airice_solve_*, airice_table_*).
  *   - MakeAtmosphere() reads "Atmosphere.dat" from the working directory (fallback
  *     $AIRICE_ATMOSPHERE) and fills ATMLAY, abc, B_air, C_air, MaxLayers, h_data, nh_data,
  *     lognh_data.  The reference defines these as header statics; here they are one shared copy.

@@ -153,13 +153,18 @@ int airice_rays_host(const airice_medium *m, const double *launch_deg, const dou
                      double ice_h_m, double depth_m, int32_t in_ice, size_t n, double *out,
                      size_t ld);
 
-/* Where the one-query calls of the C++ drop-ins run -- GetRayTracingSolutions and the ray layer
- * (airice_rtf_eval / _variant: RayTracingFunctions::, MultiRayAirIceRefraction:: and
- * AirIceRayTracing:: fDnfR ... MinimizeforLaunchAngle): AIRICE_SCALAR_HOST (default) or
- * AIRICE_SCALAR_DEVICE (a one-wave kernel per call).  The environment variable
- * AIRICE_SCALAR=device selects the device at start.  Returns the previous mode; any other value
- * only queries it.  One-query solves (Air2IceRayTracing, the CoREAS entry, Py_TraceIceToAir) and
- * every batch entry point run on the device either way. */
+/* Where one-query calls run: AIRICE_SCALAR_HOST (default: the calling CPU thread, from the same
+ * __host__ __device__ source as the kernels, with the host's correctly rounded sqrt and quotients,
+ * so within about an ulp of the same query inside a GPU batch) or AIRICE_SCALAR_DEVICE (a
+ * one-wave GPU kernel per call, bit-identical to the batch).  The mode covers every one-query
+ * call: GetRayTracingSolutions and the ray layer of the C++ drop-ins (airice_rtf_eval / _variant:
+ * RayTracingFunctions::, MultiRayAirIceRefraction:: and AirIceRayTracing:: fDnfR ...
+ * MinimizeforLaunchAngle), the one-query solves (Air2IceRayTracing, the CoREAS entry,
+ * Py_TraceIceToAir, the _Table lookup's minimizer fallback) and airice_solve_host /
+ * airice_trace_ice_to_air_host calls with n == 1.  The environment variable AIRICE_SCALAR=device
+ * selects the device at start.  Returns the previous mode; any other value only queries it.
+ * Batch entry points (n > 1 and every *_launch) always run on the GPU; airice_rays_host always
+ * runs on the host. */
 #define AIRICE_SCALAR_HOST 0
 #define AIRICE_SCALAR_DEVICE 1
 int airice_scalar_mode(int mode);
@@ -294,7 +299,8 @@ int airice_trace_ice_to_air_host(const airice_medium *m, const double *depth, co
 /* Drop-in for the reference ctypes symbol (TraceIceToAir.C:75-79): the C++ TraceIceToAir of
  * include/AirIceRayTracing.h, which reads "Atmosphere.dat" from the working directory like the
  * reference (parsed once while the file is unchanged; falls back to $AIRICE_ATMOSPHERE), then
- * solves on the GPU. */
+ * solves the one query where airice_scalar_mode says: the calling thread by default, a one-wave
+ * GPU kernel with AIRICE_SCALAR=device.  Batches: airice_trace_ice_to_air_launch. */
 void Py_TraceIceToAir(double AntennaDepth, double IceLayerHeight, double AirTxHeight,
                       double HorizontalDistance, double ArrayParameters[10]);
 
