@@ -197,6 +197,38 @@ def cpu_info(nthr: int) -> dict:
             "compiler": "gcc -O2 -ffp-contract=off -fopenmp (oracle/Makefile)"}
 
 
+def physical_cores() -> int:
+    """Physical cores among this process's CPUs (unique (package, core) pairs in /proc/cpuinfo)."""
+    try:
+        aff = os.sched_getaffinity(0)
+    except AttributeError:
+        aff = set(range(os.cpu_count() or 1))
+    cores, cpu, pkg = set(), None, None
+    try:
+        with open("/proc/cpuinfo") as f:
+            for ln in f:
+                k, _, v = ln.partition(":")
+                k, v = k.strip(), v.strip()
+                if k == "processor":
+                    cpu = int(v)
+                elif k == "physical id":
+                    pkg = v
+                elif k == "core id" and cpu in aff:
+                    cores.add((pkg, v))
+    except (OSError, ValueError):
+        pass
+    return len(cores) or len(aff)
+
+
+# what the CPU baseline is (VERDICT r05 item 6): the oracle restatement is NOT the reference's speed
+PORT_VS_REFERENCE = ("the oracle's C restatement (faithful call structure and libm calls, but no "
+                     "per-segment new[], no std::cout and one medium fold per call) runs about 4-5x "
+                     "the reference's own per-thread speed: the survey's probe of the real reference "
+                     "(compiled against a GSL stand-in) measured 2.42e5 rays/s and 8.8e3 solves/s on "
+                     "one thread against this port's ~1e6 rays/s and ~4.4e4 solves/s; so this "
+                     "baseline is conservative (faster than the reference), not the reference")
+
+
 def counter_roofline(kernel_key: str, units: int, kernel_ms: float, pmc: dict,
                      algorithmic_bytes_per_unit: float) -> dict:
     """Roofline of one kernel from its executed FP64 VALU instructions (PMC, per unit) over the
@@ -225,6 +257,42 @@ def counter_roofline(kernel_key: str, units: int, kernel_ms: float, pmc: dict,
         "hbm_bytes_per_launch_algorithmic": algorithmic_bytes_per_unit * units,
         "hbm_GBps_algorithmic": algorithmic_bytes_per_unit * units / (kernel_ms * 1e-3) / 1e9
         if kernel_ms else None,
+    }
+
+
+HBM_PEAK_GBPS = 8000.0        # MI355X HBM3E, spec (MI355X_MICROARCH.md §HBM)
+HBM_ACHIEVABLE_GBPS = 6300.0  # achievable streaming rate, same section
+# the lookup's necessary bytes per query: inputs (3 doubles), outputs (9 doubles + ok + flags),
+# and the two 64-byte pair records its interpolation reads (one per Tx height)
+LOOKUP_QUERY_IO_BYTES = 24 + 72 + 2
+LOOKUP_RECORD_BYTES = 2 * 64
+
+
+def lookup_roofline(units: int, kernel_ms: float, pmc: dict) -> dict:
+    """The lookup is memory-bound (random records; 15 % VALU busy): its traffic per launch from the
+    PMC summary, with FETCH_SIZE corrected by the factor calibrated for its access pattern
+    (tools/fetch_calib.hip, profiles/r06_fetch_calib.json) instead of the streaming x2, over the
+    live kernel time, against the HBM peak and the achievable 6.3 TB/s."""
+    p = pmc.get("lookup_kernel", {})
+    per_unit = (p["hbm_bytes_per_launch"] / p["units_per_launch"]
+                if p.get("hbm_bytes_per_launch") and p.get("units_per_launch") else None)
+    traffic = per_unit * units if per_unit else None
+    ach = traffic / (kernel_ms * 1e-3) / 1e9 if traffic and kernel_ms else None
+    algo = (LOOKUP_QUERY_IO_BYTES + LOOKUP_RECORD_BYTES) * units
+    return {
+        "bound": "hbm", "kernel": "lookup_kernel", "unit": "GB/s",
+        "achieved": ach, "peak": HBM_PEAK_GBPS, "frac": ach / HBM_PEAK_GBPS if ach else None,
+        "frac_of_achievable": ach / HBM_ACHIEVABLE_GBPS if ach else None,
+        "achievable": HBM_ACHIEVABLE_GBPS,
+        "traffic": traffic,
+        "traffic_source": p.get("hbm_bytes_source"),
+        "fetch_factor": p.get("fetch_factor"), "fetch_factor_source": p.get("fetch_factor_source"),
+        "algorithmic_bytes": algo,
+        "algorithmic_note": "per query: 98 B of query I/O + two 64-byte pair records",
+        "algorithmic_GBps": algo / (kernel_ms * 1e-3) / 1e9 if kernel_ms else None,
+        "traffic_over_algorithmic": traffic / algo if traffic else None,
+        "kernel_ms": kernel_ms, "units_per_launch": units,
+        "random_64B_probe_GBps": p.get("random_64B_probe_GBps"),
     }
 
 
@@ -614,7 +682,8 @@ def main(argv=None, make_backend=None, json_path=None):
             "value": args.lookup_n / (lms * 1e-3), "unit": "lookups/s", "ms": lms,
             "lookup_kernel_ms": lk_ms / lk_n if lk_n else None,
             "ok_fraction": float(lok.cpu().numpy().mean()),
-            "pack_ms": pack_ms, "packed": True}
+            "pack_ms": pack_ms, "packed": True,
+            "roofline": lookup_roofline(args.lookup_n, lk_ms / lk_n if lk_n else None, pmc)}
         if sharded:
             del ltable
     if not args.no_multi:
@@ -746,12 +815,27 @@ def main(argv=None, make_backend=None, json_path=None):
             if c1dt >= args.cpu_seconds / 4:
                 break
         one = passes * len(rows1) * og.angle_steps / c1dt
+        # context: whole cfg2 grids on all physical cores of the box, for about a second (the
+        # process's CPU quota, not only its affinity mask, bounds what this can show)
+        nall = physical_cores()
+        ca = time.perf_counter()
+        ga = 0
+        while True:
+            oracle.table_rows(om, og, 0, og.height_steps, nthreads=nall)
+            ga += 1
+            cadt = time.perf_counter() - ca
+            if cadt >= 1.0 or ga >= 200:
+                break
+        all_cores = {"value": ga * og.height_steps * og.angle_steps / cadt,
+                     "threads_used": nall, "sample": f"{ga} full cfg2 grids in {cadt:.1f} s"}
         cpu = {"value": grids * og.height_steps * og.angle_steps / cdt, "unit": "rays/s",
                "cores": nthr, "kind": "port",
                "sample": f"{grids} x the full cfg2 grid ({og.height_steps * og.angle_steps} rays "
                          f"each) in {cdt:.1f} s, oracle C restatement (faithful call structure), "
                          f"OpenMP {nthr} threads",
                "one_thread_value": one, "seconds": cdt, **info,
+               "all_physical_cores": all_cores,
+               "not_the_reference": PORT_VS_REFERENCE,
                "survey_reference_probe": SURVEY_REFERENCE_PROBE["table_rays_per_s"],
                "survey_reference_probe_source": SURVEY_REFERENCE_PROBE["source"]}
         gt = table.cpu().numpy()
@@ -1098,10 +1182,17 @@ def minimizer_cpu_baseline(args, om, txh, dst, dep, nthr, info) -> dict:
     t1 = time.perf_counter()
     oracle.solve_batch(om, txh[:m1], dst[:m1], dep[:m1], 3000.0, nthreads=1)
     one = m1 / (time.perf_counter() - t1)
+    nall = physical_cores()
+    ma = int(min(n, max(20000, 2 * rate * nall / max(nthr, 1))))  # ~2 s on all cores
+    ta = time.perf_counter()
+    oracle.solve_batch(om, txh[:ma], dst[:ma], dep[:ma], 3000.0, nthreads=nall)
+    all_cores = {"value": ma / (time.perf_counter() - ta), "threads_used": nall,
+                 "sample": f"the first {ma} queries"}
     return {"value": done / dt, "unit": "solves/s", "cores": nthr, "kind": "port",
             "sample": f"{done} cfg3 queries (the head of the timed batch) in {dt:.1f} s, oracle "
                       f"GSL-bisection restatement, OpenMP {nthr} threads; 1-thread on {m1}",
-            "one_thread_value": one, **info,
+            "one_thread_value": one, **info, "all_physical_cores": all_cores,
+            "not_the_reference": PORT_VS_REFERENCE,
             "survey_reference_probe": SURVEY_REFERENCE_PROBE["minimizer_solves_per_s"]}
 
 

@@ -87,3 +87,24 @@ def test_device_matches_twin_bitwise(tmp_path, lean):
     y_gpu = np.fromfile(out, dtype=np.float64)
     same = (y_gpu.view(np.uint64) == y_cpu.view(np.uint64)) | (np.isnan(y_gpu) & np.isnan(y_cpu))
     assert same.all(), np.flatnonzero(~same)[:10]
+
+
+def test_lookup_fetch_calibration_model():
+    """tools/make_pmc_summary.py's calibrated lookup traffic: streamed
+    inputs x2, random accesses at their 64-byte requests; the committed summary carries it."""
+    import json
+    import os
+    from tests.conftest import ROOT
+    from tools.make_pmc_summary import apply_lookup_calibration
+    calib = {"probes": {"stream16": {"factor_bytes_per_fetch_byte": 2.0, "GBps": 5000.0},
+                        "rand64_big": {"factor_bytes_per_fetch_byte": 1.0, "GBps": 3000.0}}}
+    d = {"units_per_launch": 1000, "write_bytes_per_launch": 98000.0,
+         "fetch_bytes_per_launch_raw": 12000.0 + 200000.0}
+    out = apply_lookup_calibration(dict(d), calib)
+    assert out["fetch_bytes_per_launch_corrected"] == 24000.0 + 200000.0
+    assert out["hbm_bytes_per_launch"] == 98000.0 + 224000.0
+    with open(os.path.join(ROOT, "profiles", "pmc_summary.json")) as f:
+        lk = json.load(f)["lookup_kernel"]
+    assert lk["fetch_factor"]["streaming_inputs"] > 1.9
+    assert 0.9 < lk["fetch_factor"]["random_records"] < 1.1
+    assert lk["hbm_bytes_per_launch"] < lk["write_bytes_per_launch"] + 2 * lk["fetch_bytes_per_launch_raw"]

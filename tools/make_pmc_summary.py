@@ -1,8 +1,10 @@
 """Derive per-kernel metrics from the PMC passes (tools/gpu_pmc.sh) -> profiles/pmc_summary.json.
 
 HBM bytes follow MI355X_MICROARCH.md §HBM: WRITE_SIZE/FETCH_SIZE are KiB (x1024); FETCH_SIZE
-under-reports wide coalesced streaming reads by 2x on gfx950 -- the kernels here read only
+under-reports wide coalesced streaming reads by 2x on gfx950 -- the compute kernels here read only
 kernel arguments and <=24 B per query, so FETCH is reported both raw and doubled (upper bound).
+The table lookup reads random records, whose FETCH_SIZE was calibrated separately
+(apply_lookup_calibration below).
 
 Busy figures, both bounded by construction:
 * fp64_pipe_busy_pct = 100 x (executed FP64 VALU instructions x 4 cycles) / (1024 SIMDs x the
@@ -67,11 +69,54 @@ def derive(name, c, n_units, kernel_ns=None):
     return d
 
 
+# FETCH_SIZE per access pattern (tools/fetch_calib.hip, profiles/r06_fetch_calib.json): a wide
+# coalesced streaming read reports 1/2 of its bytes; a random 64-byte record (four 16-byte loads)
+# reports its 64 bytes; a random 32-byte piece reports 64 (one 64-byte fabric request).  So for the
+# table lookup -- streaming query inputs, then random records and record pieces -- FETCH_SIZE
+# counts every random access at the 64-byte request it costs, and only the streaming inputs need
+# the x2: traffic = WRITE + (FETCH - inputs / 2) + inputs.
+LOOKUP_STREAM_BYTES_PER_QUERY = 24  # src, dist, depth: three doubles, coalesced
+CALIB_FILE = "profiles/r06_fetch_calib.json"
+
+
+def apply_lookup_calibration(d, calib):
+    """Replace the streaming x2 of lookup_kernel's FETCH_SIZE with the calibrated model above."""
+    probes = calib["probes"]
+    f_stream = probes["stream16"]["factor_bytes_per_fetch_byte"]
+    f_rand = probes["rand64_big"]["factor_bytes_per_fetch_byte"]
+    stream = LOOKUP_STREAM_BYTES_PER_QUERY * d["units_per_launch"]
+    fetch = d["fetch_bytes_per_launch_raw"]
+    reads = (fetch - stream / f_stream) * f_rand + stream
+    d["hbm_bytes_per_launch"] = d["write_bytes_per_launch"] + reads
+    d["fetch_bytes_per_launch_corrected"] = reads
+    d["fetch_factor"] = {"streaming_inputs": f_stream, "random_records": f_rand}
+    d["fetch_factor_source"] = (f"{CALIB_FILE}: stream16 (x{f_stream:.3f}) for the "
+                                f"{LOOKUP_STREAM_BYTES_PER_QUERY} B/query of streamed inputs, "
+                                f"rand64_big (x{f_rand:.3f}) for the rest (random 64-byte records "
+                                "and 32-byte row-record pieces, each one 64-byte request)")
+    d["hbm_bytes_source"] = "WRITE_SIZE + FETCH_SIZE corrected per access pattern (fetch_factor)"
+    d["random_64B_probe_GBps"] = {k: probes[k]["GBps"] for k in ("rand64_big", "rand64_small")
+                                  if k in probes}
+    return d
+
+
 # the cfg4 fine table (`bench.py --cfg4-only`): 97,001 x 8,991 rays in one launch
 UNITS_CFG4 = [("table_kernel", "table_kernel_cfg4", 872135991)]
 
 
 if __name__ == "__main__":
+    if sys.argv[1] == "--apply-calibration":
+        # re-derive the lookup's traffic in an existing summary from the calibration probes
+        # (python tools/make_pmc_summary.py --apply-calibration CALIB.json SUMMARY.json)
+        with open(sys.argv[2]) as f:
+            calib = json.load(f)
+        with open(sys.argv[3]) as f:
+            summ = json.load(f)
+        summ["lookup_kernel"] = apply_lookup_calibration(summ["lookup_kernel"], calib)
+        with open(sys.argv[3], "w") as f:
+            json.dump(summ, f, indent=1)
+        print(json.dumps(summ["lookup_kernel"], indent=1))
+        sys.exit(0)
     src, dst = sys.argv[1], sys.argv[2]
     with open(src) as f:
         raw = json.load(f)
@@ -88,6 +133,10 @@ if __name__ == "__main__":
                 if k.startswith(prefix):
                     out[key] = {**derive(k, c, n), "kernel": k,
                                 "raw": {a: b for a, b in c.items() if not a.startswith("_")}}
+    import os
+    if "lookup_kernel" in out and os.path.exists(CALIB_FILE):
+        with open(CALIB_FILE) as f:
+            out["lookup_kernel"] = apply_lookup_calibration(out["lookup_kernel"], json.load(f))
     with open(dst, "w") as f:
         json.dump(out, f, indent=1)
     print(json.dumps(out, indent=1)[:3000])
