@@ -229,6 +229,11 @@ PORT_VS_REFERENCE = ("the oracle's C restatement (faithful call structure and li
                      "baseline is conservative (faster than the reference), not the reference")
 
 
+ALL_CORES_NOTE = ("context only: one thread per physical core of the host; on the shared GPU box "
+                  "the process's CPU quota (16 CPUs per GPU) can make this lower than the "
+                  "16-thread value")
+
+
 def counter_roofline(kernel_key: str, units: int, kernel_ms: float, pmc: dict,
                      algorithmic_bytes_per_unit: float) -> dict:
     """Roofline of one kernel from its executed FP64 VALU instructions (PMC, per unit) over the
@@ -827,7 +832,8 @@ def main(argv=None, make_backend=None, json_path=None):
             if cadt >= 1.0 or ga >= 200:
                 break
         all_cores = {"value": ga * og.height_steps * og.angle_steps / cadt,
-                     "threads_used": nall, "sample": f"{ga} full cfg2 grids in {cadt:.1f} s"}
+                     "threads_used": nall, "sample": f"{ga} full cfg2 grids in {cadt:.1f} s",
+                     "note": ALL_CORES_NOTE}
         cpu = {"value": grids * og.height_steps * og.angle_steps / cdt, "unit": "rays/s",
                "cores": nthr, "kind": "port",
                "sample": f"{grids} x the full cfg2 grid ({og.height_steps * og.angle_steps} rays "
@@ -1187,7 +1193,7 @@ def minimizer_cpu_baseline(args, om, txh, dst, dep, nthr, info) -> dict:
     ta = time.perf_counter()
     oracle.solve_batch(om, txh[:ma], dst[:ma], dep[:ma], 3000.0, nthreads=nall)
     all_cores = {"value": ma / (time.perf_counter() - ta), "threads_used": nall,
-                 "sample": f"the first {ma} queries"}
+                 "sample": f"the first {ma} queries", "note": ALL_CORES_NOTE}
     return {"value": done / dt, "unit": "solves/s", "cores": nthr, "kind": "port",
             "sample": f"{done} cfg3 queries (the head of the timed batch) in {dt:.1f} s, oracle "
                       f"GSL-bisection restatement, OpenMP {nthr} threads; 1-thread on {m1}",
