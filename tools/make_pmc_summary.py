@@ -76,7 +76,10 @@ def derive(name, c, n_units, kernel_ns=None):
 # counts every random access at the 64-byte request it costs, and only the streaming inputs need
 # the x2: traffic = WRITE + (FETCH - inputs / 2) + inputs.
 LOOKUP_STREAM_BYTES_PER_QUERY = 24  # src, dist, depth: three doubles, coalesced
-CALIB_FILE = "profiles/r06_fetch_calib.json"
+CALIB_FILE = "profiles/r06_fetch_calib.json"  # relative to the repository root
+CALIB_PATH = __import__("os").path.join(
+    __import__("os").path.dirname(__import__("os").path.dirname(__import__("os").path.abspath(__file__))),
+    CALIB_FILE)
 
 
 def apply_lookup_calibration(d, calib):
@@ -134,8 +137,8 @@ if __name__ == "__main__":
                     out[key] = {**derive(k, c, n), "kernel": k,
                                 "raw": {a: b for a, b in c.items() if not a.startswith("_")}}
     import os
-    if "lookup_kernel" in out and os.path.exists(CALIB_FILE):
-        with open(CALIB_FILE) as f:
+    if "lookup_kernel" in out and os.path.exists(CALIB_PATH):
+        with open(CALIB_PATH) as f:
             out["lookup_kernel"] = apply_lookup_calibration(out["lookup_kernel"], json.load(f))
     with open(dst, "w") as f:
         json.dump(out, f, indent=1)
