@@ -321,3 +321,14 @@ def test_bench_main_self_launches_without_rank(monkeypatch):
     with pytest.raises(SystemExit) as e:
         bench.main(BENCH2, make_backend=lambda r: pytest.fail("backend built"))
     assert e.value.code == 0 and seen == {"n": 2, "argv": BENCH2}
+
+
+def test_bench_self_launch_relays_failure(tmp_path, capsys):
+    """A rank that fails makes the self-launched run fail: torch.distributed.run's non-zero
+    status is bench.py's, and no JSON line is printed."""
+    import bench
+    script = tmp_path / "fail_rank.py"
+    script.write_text("import os, sys\nsys.exit(3 if os.environ.get('RANK') == '1' else 0)\n")
+    rc = bench.self_launch(2, [], script=str(script), timeout=120)
+    out = capsys.readouterr().out
+    assert rc != 0 and not out.strip()
