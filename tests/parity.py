@@ -167,3 +167,44 @@ def lookup_queries(table: np.ndarray, n: int, seed: int = 4242, max_dist: float 
     H = np.concatenate([body_h, on_entry_h, on_row_h, edge_h])
     D = np.concatenate([body_d, on_entry_d, on_row_d, edge_d])
     return H * 100.0, D * 100.0
+
+
+# Root-window outliers.  A launch angle is GSL's bisection root, known only to its interval test
+# (|hi - lo| < 1e-9 min(|lo|, |hi|), .cc:363); where f at a late midpoint is within its rounding
+# noise (~1e-12 of THD) the two sides' bisections can take different halves, and their roots then
+# differ by up to that window.  An output that amplifies the angle (grazing rays, long paths) can
+# then differ by a few 1e-9.  Such a row is accepted when both roots lie within one window of each
+# other, its status agrees, and its outputs agree to WINDOW_RTOL; the rows are counted and must stay
+# rare (<= WINDOW_MAX_FRACTION of the batch).  tools/find_parity_outliers.py prints them.
+WINDOW_RTOL = 1e-8
+WINDOW_MAX_FRACTION = 1e-6
+
+
+def compare_with_root_window(gpu, ref, floors, theta_gpu, theta_ref, mask=None,
+                             rtol: float = RTOL):
+    """compare_columns, except that rows whose roots lie within one GSL tolerance window
+    (|theta_gpu - theta_ref| <= 1e-9 |theta_ref|) may reach WINDOW_RTOL; rep['window_rows'] counts
+    them, and 'ok' also requires that count to stay under WINDOW_MAX_FRACTION of the rows."""
+    gpu = np.asarray(gpu, dtype=np.float64)
+    ref = np.asarray(ref, dtype=np.float64)
+    tg = np.asarray(theta_gpu, dtype=np.float64)
+    tr = np.asarray(theta_ref, dtype=np.float64)
+    if mask is not None:
+        gpu, ref, tg, tr = gpu[:, mask], ref[:, mask], tg[mask], tr[mask]
+    strict = compare_columns(gpu, ref, floors, rtol=rtol)
+    both = np.isfinite(gpu) & np.isfinite(ref)
+    scale = np.maximum(np.abs(ref), floors[:, None])
+    err = np.where(both, np.abs(gpu - ref) / scale, 0.0)
+    over = (err > rtol).any(axis=0)
+    in_window = np.abs(tg - tr) <= 1e-9 * np.abs(tr)
+    window_rows = over & in_window & (err <= WINDOW_RTOL).all(axis=0)
+    unexplained = over & ~window_rows
+    rep = dict(strict)
+    rep["window_rows"] = int(window_rows.sum())
+    rep["window_max_rel"] = float(err[:, window_rows].max()) if window_rows.any() else 0.0
+    rep["n_bad"] = int(unexplained.sum())
+    rep["strict_max_rel_outside_window"] = float(err[:, ~window_rows].max()) if err.size else 0.0
+    rep["ok"] = (strict["nan_mismatch"] == 0 and strict["inf_mismatch"] == 0 and
+                 rep["n_bad"] == 0 and
+                 rep["window_rows"] <= max(1, WINDOW_MAX_FRACTION * ref.shape[1]))
+    return rep

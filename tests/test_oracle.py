@@ -223,3 +223,28 @@ def test_mt19937_64_known_answer_and_libstdcxx_golden():
     d, ice, txh, dist = parity.cfg5_queries(len(g5))
     np.testing.assert_array_equal(np.stack([d, txh, dist], axis=1), g5)
     assert np.all(ice == 3000.0)
+
+
+def test_root_window_rule():
+    """tests/parity.compare_with_root_window: a row over 1e-9 passes only with both roots inside
+    one GSL tolerance window and outputs within 1e-8, and such rows must stay rare."""
+    import numpy as np
+    from tests import parity
+    n = 2_000_000
+    ref = np.ones((2, n))
+    gpu = ref.copy()
+    th = np.full(n, 150.0)
+    gpu[1, 7] = 1 + 3e-9                       # over 1e-9, roots equal: a window row
+    rep = parity.compare_with_root_window(gpu, ref, np.array([1e-9, 1e-9]), th, th)
+    assert rep["ok"] and rep["window_rows"] == 1 and rep["n_bad"] == 0
+    thg = th.copy()
+    thg[7] = 150.0 * (1 + 2e-9)                # roots two windows apart: unexplained
+    rep = parity.compare_with_root_window(gpu, ref, np.array([1e-9, 1e-9]), thg, th)
+    assert not rep["ok"] and rep["n_bad"] == 1
+    gpu[1, 7] = 1 + 2e-8                       # beyond 1e-8: unexplained
+    rep = parity.compare_with_root_window(gpu, ref, np.array([1e-9, 1e-9]), th, th)
+    assert not rep["ok"]
+    gpu[1, :5] = 1 + 3e-9                      # too many window rows for 2e6 queries
+    gpu[1, 7] = 1.0
+    rep = parity.compare_with_root_window(gpu, ref, np.array([1e-9, 1e-9]), th, th)
+    assert rep["window_rows"] == 5 and not rep["ok"]
