@@ -1210,9 +1210,11 @@ def minimizer_parity(args, om, txh, dst, dep, out_h, st_h, nthr) -> dict:
     idx = np.arange(0, len(txh), args.parity_stride)
     ref, rst = oracle.solve_batch(om, txh[idx], dst[idx], dep[idx], 3000.0, nthreads=nthr)
     pinned = (rst & oracle.SOLVE_UNPINNED) == 0
-    rep = parity.compare_columns(out_h[:, idx], ref, parity.SOLVE_FLOORS, mask=pinned)
+    rep = parity.compare_with_root_window(out_h[:, idx], ref, parity.SOLVE_FLOORS,
+                                          out_h[10, idx], ref[10], mask=pinned)
     return {"sample": f"every {args.parity_stride}th query of the timed batch ({idx.size})",
             "max_rel": rep["max_rel"], "max_abs": rep["max_abs"], "n_bad": rep["n_bad"],
+            "root_window_rows": rep["window_rows"],
             "nan_mask_equal": rep["nan_mismatch"] == 0 and rep["inf_mismatch"] == 0,
             "status_bits_equal": bool(np.array_equal(st_h[idx][pinned] & 0x1F,
                                                      rst[pinned] & 0x1F)),
@@ -1226,10 +1228,12 @@ def trace_parity(trace_h, nthr) -> dict:
     om = oracle.load_atmosphere(os.path.join(ROOT, "airiceraytracing_amd", "data",
                                              "Atmosphere.dat.gz"), pi=oracle.PI_EXACT)
     ref = oracle.py_trace_batch(om, depth[idx], ice[idx], txh[idx], dist_[idx], nthreads=nthr)
-    rep = parity.compare_columns(got.T, ref.T, parity.TRACE_FLOORS)
+    rep = parity.compare_with_root_window(got.T, ref.T, parity.TRACE_FLOORS, 180 - got[:, 5],
+                                          180 - ref[:, 5])
     return {"sample": f"every {idx[1] - idx[0] if idx.size > 1 else 1}th query of the timed "
                       f"1e7 batch ({idx.size})",
             "max_rel": rep["max_rel"], "max_abs": rep["max_abs"], "n_bad": rep["n_bad"],
+            "root_window_rows": rep["window_rows"],
             "nan_mask_equal": rep["nan_mismatch"] == 0 and rep["inf_mismatch"] == 0,
             "solved_mask_equal": bool(np.array_equal(got[:, 0] != -1000, ref[:, 0] != -1000)),
             "ok": rep["ok"]}
