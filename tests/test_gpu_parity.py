@@ -54,6 +54,21 @@ def test_table_full_grid(solver, oracle_medium, depth_cm, hstep, a0, a1, astep):
     assert ulps <= 1, ulps
 
 
+def test_table_reference_default_grid_whole(solver, oracle_medium):
+    """Reference defaults (10 m x 0.1 deg, 9,701 x 900 = 8,730,900 rays): the whole float table
+    (AllTableAllAntData's 11 columns) within 1 f32 ulp of the oracle's, NaN pattern identical."""
+    from airiceraytracing_amd import make_grid
+    g = make_grid(-20000.0, 300000.0)
+    og = oracle.grid_init(-20000.0, 300000.0)
+    table = solver.table_host(g)
+    ot = oracle.table_rows(oracle_medium, og, 0, og.height_steps, nthreads=NTHREADS)
+    assert table.shape == ot.shape == (11, 8730900)
+    assert np.array_equal(np.isnan(table), np.isnan(ot))
+    ulps = parity.float_ulp_diff(table, ot)
+    print(f"[default-grid-whole] 8,730,900 rays, max {ulps} f32 ulp")
+    assert ulps <= 1, ulps
+
+
 def test_table_reference_default_grid_rows(solver, oracle_medium):
     """Reference defaults (10 m x 0.1 deg, 9,701 x 900): strided rows through the row API."""
     from airiceraytracing_amd import make_grid
