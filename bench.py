@@ -284,6 +284,18 @@ def lookup_roofline(units: int, kernel_ms: float, pmc: dict) -> dict:
     traffic = per_unit * units if per_unit else None
     ach = traffic / (kernel_ms * 1e-3) / 1e9 if traffic and kernel_ms else None
     algo = (LOOKUP_QUERY_IO_BYTES + LOOKUP_RECORD_BYTES) * units
+    # the access-pattern bound: each part of the traffic at the rate tools/fetch_calib.hip
+    # measured for its pattern (random 64-byte records from an L3-resident table, streamed reads,
+    # streamed writes), one after the other
+    pb = None
+    probes = p.get("probe_GBps") or {}
+    if traffic and all(k in probes for k in ("rand64_small", "stream16", "wstream16")):
+        scale = units / p["units_per_launch"]
+        stream_in = p["stream_input_bytes_per_launch"] * scale
+        random_rd = p["fetch_bytes_per_launch_corrected"] * scale - stream_in
+        writes = p["write_bytes_per_launch"] * scale
+        pb = (random_rd / probes["rand64_small"] + stream_in / probes["stream16"] +
+              writes / probes["wstream16"]) / 1e9 * 1e3  # ms
     return {
         "bound": "hbm", "kernel": "lookup_kernel", "unit": "GB/s",
         "achieved": ach, "peak": HBM_PEAK_GBPS, "frac": ach / HBM_PEAK_GBPS if ach else None,
@@ -298,6 +310,10 @@ def lookup_roofline(units: int, kernel_ms: float, pmc: dict) -> dict:
         "traffic_over_algorithmic": traffic / algo if traffic else None,
         "kernel_ms": kernel_ms, "units_per_launch": units,
         "random_64B_probe_GBps": p.get("random_64B_probe_GBps"),
+        "pattern_bound_ms": pb,
+        "frac_of_pattern_bound": pb / kernel_ms if pb and kernel_ms else None,
+        "pattern_bound_note": "random reads at rand64_small's rate, streamed inputs at "
+                              "stream16's, results at wstream16's (profiles/r06_fetch_calib.json)",
     }
 
 

@@ -12,6 +12,7 @@
 //
 // Probes (each launched kReps times after one warm-up launch; a dispatch reads its bytes once):
 //   stream16     : 16 B per lane, coalesced, over a 2 GiB buffer (the guide's calibrated case)
+//   wstream16    : 16 B per lane stored, coalesced, 2 GiB (the streaming write rate; timing only)
 //   rand64_big   : one random 64-byte record per lane (4 x float4), 2^24 draws from 2^25 records
 //                  of a 2 GiB table -- larger than the 256 MiB Infinity Cache
 //   rand32_big   : one random 32-byte piece (2 x float4) of a random 256-byte record, 2 GiB table
@@ -64,6 +65,12 @@ __global__ __launch_bounds__(kBlock) void stream16(const float4* __restrict__ a,
     v = x.x + x.y + x.z + x.w;
   }
   wave_out(v, out);
+}
+
+// 16 B per lane stored, coalesced: the streaming write rate (the lookup's result columns)
+__global__ __launch_bounds__(kBlock) void wstream16(float4* __restrict__ a, long long n) {
+  const long long i = (long long)blockIdx.x * kBlock + threadIdx.x;
+  if (i < n) a[i] = float4{(float)i, 1.f, 2.f, 3.f};
 }
 
 // lane i reads record scatter(i) of 64 B: four 16-byte loads at p[0..3], as lk_pair does
@@ -152,6 +159,14 @@ int main(int argc, char** argv) {
     const unsigned g = (unsigned)((n + kBlock - 1) / kBlock);
     if (timed("stream16", 16.0 * n, n, [&] {
           hipLaunchKernelGGL(stream16, dim3(g), dim3(kBlock), 0, 0, buf, n, out);
+        }))
+      return 1;
+  }
+  {  // wstream16: 2^27 lanes x 16 B = 2 GiB written
+    const long long n = (long long)(big / 16);
+    const unsigned g = (unsigned)((n + kBlock - 1) / kBlock);
+    if (timed("wstream16", 16.0 * n, n, [&] {
+          hipLaunchKernelGGL(wstream16, dim3(g), dim3(kBlock), 0, 0, buf, n);
         }))
       return 1;
   }

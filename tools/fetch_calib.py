@@ -14,8 +14,8 @@ import statistics
 import sys
 from collections import defaultdict
 
-PROBE_KERNELS = {"stream16": "stream16", "rand64_big": "rand64", "rand32_big": "rand32",
-                 "rand64_small": "rand64_n"}
+PROBE_KERNELS = {"stream16": "stream16", "wstream16": "wstream16", "rand64_big": "rand64",
+                 "rand32_big": "rand32", "rand64_small": "rand64_n"}
 
 
 def per_dispatch(dirs):
@@ -42,9 +42,9 @@ def main():
     for probe, kern in PROBE_KERNELS.items():
         t = timings.get(probe)
         c = acc.get(kern, {})
-        if t is None or not c:
+        if t is None:
             continue
-        med = {name: statistics.median(v.values()) for name, v in c.items()}
+        med = {name: statistics.median(v.values()) for name, v in c.items()} if c else {}
         fetch = med.get("FETCH_SIZE")
         rec = {"bytes_per_launch": t["bytes_per_launch"], "ms": t["ms"], "GBps": t["GBps"],
                "dispatches": {name: len(v) for name, v in c.items()},

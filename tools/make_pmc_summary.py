@@ -100,6 +100,8 @@ def apply_lookup_calibration(d, calib):
     d["hbm_bytes_source"] = "WRITE_SIZE + FETCH_SIZE corrected per access pattern (fetch_factor)"
     d["random_64B_probe_GBps"] = {k: probes[k]["GBps"] for k in ("rand64_big", "rand64_small")
                                   if k in probes}
+    d["probe_GBps"] = {k: v["GBps"] for k, v in probes.items()}
+    d["stream_input_bytes_per_launch"] = stream
     return d
 
 
