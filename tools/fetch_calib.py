@@ -49,7 +49,7 @@ def main():
         rec = {"bytes_per_launch": t["bytes_per_launch"], "ms": t["ms"], "GBps": t["GBps"],
                "dispatches": {name: len(v) for name, v in c.items()},
                "counters_median": med}
-        if fetch:
+        if fetch and probe != "wstream16":  # a write probe: its FETCH_SIZE is not its bytes
             rec["fetch_bytes_raw"] = fetch * 1024
             rec["factor_bytes_per_fetch_byte"] = t["bytes_per_launch"] / (fetch * 1024)
         res["probes"][probe] = rec
