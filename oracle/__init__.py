@@ -116,6 +116,7 @@ def lib():
         L.or_solve_batch.argtypes = [M, P, P, P, D, ctypes.c_size_t, P, ctypes.c_size_t, P, I]
         L.or_hdtip.argtypes = [M, D, D, D, D, P]
         L.or_hdtip.restype = I
+        L.or_hdtip_batch.argtypes = [M, P, P, P, D, ctypes.c_size_t, P, ctypes.c_size_t, P, P, I]
         L.or_py_air2ice.argtypes = [M, D, D, D, D, D, P]
         L.or_py_air2ice.restype = I
         L.or_py_trace_ice_to_air.argtypes = [M, D, D, D, D, P]
@@ -253,6 +254,20 @@ def hdtip(m: Medium, src_cm, dist_cm, depth_cm, ice_cm):
     out = np.zeros(9)
     ok = lib().or_hdtip(ctypes.byref(m), src_cm, dist_cm, depth_cm, ice_cm, _ptr(out))
     return bool(ok), out
+
+
+def hdtip_batch(m: Medium, src_cm, dist_cm, depth_cm, ice_cm, nthreads: int = 0):
+    """or_hdtip over arrays (cm): (out (9, n), ok bool (n,), status of the solve (n,))."""
+    src = np.ascontiguousarray(src_cm, dtype=np.float64)
+    dst = np.ascontiguousarray(dist_cm, dtype=np.float64)
+    dep = np.ascontiguousarray(np.broadcast_to(depth_cm, src.shape), dtype=np.float64)
+    n = src.size
+    out = np.zeros((9, n))
+    ok = np.zeros(n, dtype=np.uint8)
+    st = np.zeros(n, dtype=np.uint8)
+    lib().or_hdtip_batch(ctypes.byref(m), _ptr(src), _ptr(dst), _ptr(dep), ice_cm, n, _ptr(out),
+                         n, _ptr(ok), _ptr(st), nthreads)
+    return out, ok.astype(bool), st
 
 
 def py_air2ice(m: Medium, txh, dist, ice_h, depth, straight_angle):

@@ -959,6 +959,27 @@ int or_hdtip(const or_medium *m, double Src, double Dist, double Depth, double I
   return ok;
 }
 
+/* or_hdtip over a batch (cm), OpenMP: out 9 columns (stride ld), ok[i] the returned bool,
+ * status[i] the Air2IceRayTracing status bits of the solve behind it (masks the reference-UB rows) */
+void or_hdtip_batch(const or_medium *m, const double *src_cm, const double *dist_cm,
+                    const double *depth_cm, double ice_cm, size_t n, double *out, size_t ld,
+                    uint8_t *ok, uint8_t *status, int nthreads) {
+#ifdef _OPENMP
+  if (nthreads > 0) omp_set_num_threads(nthreads);
+#pragma omp parallel for schedule(dynamic, 16) if (nthreads > 0)
+#endif
+  for (long i = 0; i < (long)n; i++) {
+    double o[9];
+    ok[i] = (uint8_t)or_hdtip(m, src_cm[i], dist_cm[i], depth_cm[i], ice_cm, o);
+    for (int c = 0; c < 9; c++) out[c * ld + i] = o[c];
+    if (status) {
+      const double H = src_cm[i] / 100, D = dist_cm[i] / 100, I = ice_cm / 100, d = depth_cm[i] / 100;
+      double dm[17];
+      status[i] = (uint8_t)or_air2ice(m, H, D, I, d, or_straight_angle(m, H, D, I, d), dm);
+    }
+  }
+}
+
 /* ------------------------------------------------------------------------- */
 /* pythonwrapper variant (pythonwrapper/AirIceRayTracing.cc, TraceIceToAir.C) */
 /* ------------------------------------------------------------------------- */

@@ -120,6 +120,10 @@ void or_solve_batch(const or_medium *m, const double *txh, const double *dist,
 /* GetHorizontalDistanceToIntersectionPoint (.cc:945-989), cm in, outs[9], returns bool. */
 int or_hdtip(const or_medium *m, double src_cm, double dist_cm, double depth_cm,
              double ice_cm, double outs[9]);
+/* The same over a batch (OpenMP): out 9 columns (stride ld), ok[], status[] (solve status bits). */
+void or_hdtip_batch(const or_medium *m, const double *src_cm, const double *dist_cm,
+                    const double *depth_cm, double ice_cm, size_t n, double *out, size_t ld,
+                    uint8_t *ok, uint8_t *status, int nthreads);
 
 /* pythonwrapper variant: AirIceRayTracing::Air2IceRayTracing (AirIceRayTracing.cc:929-1086),
  * dummy[15]; TraceIceToAir (TraceIceToAir.C:5-73) -> ArrayParameters[10]. */

@@ -95,3 +95,17 @@ def test_batch_matches_scalar(oracle_medium, coarse):
         ok1, o1, fl1 = oracle.table_lookup(oracle_medium, lt, H[i], D[i], DEPTH_CM, ICE_CM)
         assert ok1 == bool(ok[i]) and fl1 == fl[i]
         np.testing.assert_array_equal(o1, out[:, i])
+
+
+def test_hdtip_batch_matches_scalar(oracle_medium):
+    """or_hdtip_batch (the RunMultiRayCode_loop harness's checker) is or_hdtip per row."""
+    rng = np.random.default_rng(21)
+    n = 64
+    H = rng.uniform(3100, 99000, n) * 100
+    D = rng.uniform(10, 40000, n) * 100
+    out, ok, st = oracle.hdtip_batch(oracle_medium, H, D, np.full(n, DEPTH_CM), ICE_CM, nthreads=4)
+    assert out.shape == (9, n) and ok.dtype == bool
+    for i in range(n):
+        ok1, o1 = oracle.hdtip(oracle_medium, H[i], D[i], DEPTH_CM, ICE_CM)
+        assert bool(ok1) == ok[i]
+        np.testing.assert_array_equal(out[:, i], o1)
