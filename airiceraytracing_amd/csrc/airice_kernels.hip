@@ -35,6 +35,14 @@ namespace airice {
 
 constexpr double kSpeedC = 299792458.0;  // .h:30
 constexpr int kBlock = 256;
+#ifndef AIRICE_OUT_WAVES
+#define AIRICE_OUT_WAVES 1
+#endif
+constexpr int kOutWaves = AIRICE_OUT_WAVES;  // stage-2 kernels: minimum waves per SIMD (1: no cap)
+#ifndef AIRICE_TRACE_OUT_WAVES
+#define AIRICE_TRACE_OUT_WAVES AIRICE_OUT_WAVES
+#endif
+constexpr int kTraceOutWaves = AIRICE_TRACE_OUT_WAVES;
 // Table launch shape: 256-thread blocks at 8 waves/SIMD (64 VGPRs), measured best of 64 / 128 /
 // 256 / 512 threads, 7 / 8 waves and 1 / 2 rays per lane.
 #ifndef AIRICE_TABLE_BLOCK
@@ -2291,7 +2299,7 @@ __host__ __device__ __forceinline__ void solve_out_body(const DevMedium& M, cons
 // occupancy of the stage-2 kernel: the compiler's choice (80 VGPRs = 6 waves/SIMD; 7 and 8
 // measured slower)
 template <int VARIANT>
-__global__ __launch_bounds__(kBlock) void solve_out_kernel(DevMedium M, IceConsts I, QueryArgs Q,
+__global__ __launch_bounds__(kBlock, kOutWaves) void solve_out_kernel(DevMedium M, IceConsts I, QueryArgs Q,
                                                            double* __restrict__ out, size_t ld,
                                                            uint8_t* __restrict__ status,
                                                            SortedPark sp) {
@@ -2336,7 +2344,7 @@ __host__ __device__ __forceinline__ void hdtip_out_body(const DevMedium& M, cons
   ok[k] = check_solution(thd, g.D) ? 1 : 0;
 }
 
-__global__ __launch_bounds__(kBlock) void hdtip_out_kernel(DevMedium M, IceConsts I, QueryArgs Q,
+__global__ __launch_bounds__(kBlock, kOutWaves) void hdtip_out_kernel(DevMedium M, IceConsts I, QueryArgs Q,
                                                            double* __restrict__ out, size_t ld,
                                                            uint8_t* __restrict__ ok, SortedPark sp) {
   const long long k = (long long)blockIdx.x * kBlock + threadIdx.x;
@@ -2437,7 +2445,7 @@ __host__ __device__ __forceinline__ void trace_out_body(const DevMedium& M, cons
   }
 }
 
-__global__ __launch_bounds__(kBlock) void trace_out_kernel(DevMedium M, IceConsts I, QueryArgs Q,
+__global__ __launch_bounds__(kBlock, kTraceOutWaves) void trace_out_kernel(DevMedium M, IceConsts I, QueryArgs Q,
                                                            double* __restrict__ out10,
                                                            SortedPark sp) {
   const long long k = (long long)blockIdx.x * kBlock + threadIdx.x;
