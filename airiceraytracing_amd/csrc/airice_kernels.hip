@@ -39,8 +39,11 @@ constexpr int kBlock = 256;
 #define AIRICE_OUT_WAVES 1
 #endif
 constexpr int kOutWaves = AIRICE_OUT_WAVES;  // stage-2 kernels: minimum waves per SIMD (1: no cap)
+// trace_out_kernel held to 8 waves/SIMD: 64 VGPRs without scratch (94 uncapped, 5 waves), cfg5
+// 1e7 trace calls 2.059-2.064 against 2.074-2.100 ms, same outputs (profiles/r06_ab/stage2_waves_ab.log);
+// solve_out / hdtip_out capped at 5-8 waves measured within noise or slower (8: spills), uncapped
 #ifndef AIRICE_TRACE_OUT_WAVES
-#define AIRICE_TRACE_OUT_WAVES AIRICE_OUT_WAVES
+#define AIRICE_TRACE_OUT_WAVES 8
 #endif
 constexpr int kTraceOutWaves = AIRICE_TRACE_OUT_WAVES;
 // Table launch shape: 256-thread blocks at 8 waves/SIMD (64 VGPRs), measured best of 64 / 128 /
