@@ -2299,8 +2299,8 @@ __host__ __device__ __forceinline__ void solve_out_body(const DevMedium& M, cons
   if (status != nullptr) status[k] = (uint8_t)S.status;
 }
 
-// occupancy of the stage-2 kernel: the compiler's choice (80 VGPRs = 6 waves/SIMD; 7 and 8
-// measured slower)
+// occupancy of the stage-2 kernel: the compiler's choice (104 VGPRs, 4 waves/SIMD; held to 5-6
+// waves it takes 80 VGPRs and runs within noise, at 8 it spills and runs slower: round 6)
 template <int VARIANT>
 __global__ __launch_bounds__(kBlock, kOutWaves) void solve_out_kernel(DevMedium M, IceConsts I, QueryArgs Q,
                                                            double* __restrict__ out, size_t ld,
