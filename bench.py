@@ -638,6 +638,7 @@ def main(argv=None, make_backend=None, json_path=None):
         idx5 = np.arange(0, args.trace_n, args.parity_stride)
         trace_h = (q5, idx5, tout[torch.from_numpy(idx5).to(dev)].cpu().numpy())
         del q, tout
+    lookup_h = None
     if not args.no_lookup:
         # batched GetHorizontalDistanceToIntersectionPoint_Table on this step's table (HBM
         # resident), cfg3-distributed queries (cm) for the table's own antenna
@@ -705,6 +706,10 @@ def main(argv=None, make_backend=None, json_path=None):
             "ok_fraction": float(lok.cpu().numpy().mean()),
             "pack_ms": pack_ms, "packed": True,
             "roofline": lookup_roofline(args.lookup_n, lk_ms / lk_n if lk_n else None, pmc)}
+        if rank == 0 and world == 1:
+            # the last timed batch's results, checked against the oracle in the CPU legs
+            lookup_h = (lk_txh * 100, lk_dst * 100, depth_cm, ltable.cpu().numpy(),
+                        lout.cpu().numpy(), lok.cpu().numpy(), lfl.cpu().numpy())
         if sharded:
             del ltable
     if not args.no_multi:
@@ -873,6 +878,8 @@ def main(argv=None, make_backend=None, json_path=None):
             solve["parity_vs_cpu"] = minimizer_parity(args, om, txh, dst, dep, out_h, st_h, nthr)
         if trace_h is not None:
             extra["pywrapper_trace"]["parity_vs_cpu"] = trace_parity(trace_h, nthr)
+        if lookup_h is not None:
+            extra["table_lookup"]["parity_vs_cpu"] = lookup_parity(om, og, lookup_h, nthr)
         if isinstance(extra.get("scalar_latency_us"), dict):
             extra["scalar_latency_us"]["cpu_oracle_per_call_us"] = scalar_cpu_per_call(om, og, ot)
 
@@ -1253,6 +1260,38 @@ def trace_parity(trace_h, nthr) -> dict:
             "nan_mask_equal": rep["nan_mismatch"] == 0 and rep["inf_mismatch"] == 0,
             "solved_mask_equal": bool(np.array_equal(got[:, 0] != -1000, ref[:, 0] != -1000)),
             "ok": rep["ok"]}
+
+
+def lookup_parity(om, og, lookup_h, nthr) -> dict:
+    """Every query of the timed lookup batch against the oracle's lookup on the same table (the
+    GPU's floats copied to the host): lanes without the minimizer fallback bit for bit (NaN
+    positions included), fallback lanes (.cc:1418-1420) within the minimizer tolerance, rows whose
+    bracket set-up reads uninitialised GSL state masked as in tests/test_gpu_lookup.py."""
+    import oracle
+    from tests import parity
+    src, dcm, depth_cm, tab, out, ok, fl = lookup_h
+    dep = np.full(src.size, depth_cm)
+    rout, rok, rfl = oracle.table_lookup_batch(om, oracle.lookup_table(tab, og), src, dcm, dep,
+                                               CFG2["ice_cm"], nthreads=nthr)
+    fb = (rfl & oracle.LOOKUP_FALLBACK) != 0
+    a, b = out[:, ~fb], rout[:, ~fb]
+    same = (a == b) | (np.isnan(a) & np.isnan(b))
+    idx = np.flatnonzero(fb)
+    mask = np.ones(idx.size, dtype=bool)
+    for j, i in enumerate(idx):
+        _, st = oracle.air2ice(om, src[i], dcm[i], CFG2["ice_cm"] / 100, dep[i])
+        mask[j] = (st & oracle.SOLVE_UNPINNED) == 0
+    rep = parity.compare_columns(out[:, idx], rout[:, idx], parity.HDTIP_FLOORS, mask=mask) \
+        if idx.size else {"ok": True, "max_rel": 0.0}
+    return {"sample": f"every query of the timed batch ({src.size})",
+            "flags_equal": bool(np.array_equal(fl, rfl)),
+            "non_fallback_lanes": int((~fb).sum()),
+            "non_fallback_bitwise_equal": bool(same.all()),
+            "non_fallback_ok_equal": bool(np.array_equal(ok[~fb], rok[~fb])),
+            "fallback_lanes": int(idx.size), "fallback_masked": int((~mask).sum()),
+            "fallback_max_rel": rep["max_rel"],
+            "ok": bool(np.array_equal(fl, rfl) and same.all() and
+                       np.array_equal(ok[~fb], rok[~fb]) and rep["ok"])}
 
 
 def scalar_cpu_per_call(om, og, ot) -> dict:
