@@ -187,7 +187,81 @@ def straddle_trips(m, H, D, d, f, lo, hi, tau, b):
     return 1.3 + steps
 
 
+def paired_first_trips(f, lo, hi, tau, pair_h=None):
+    """Trips (a paired evaluation counted 1.3) of the kept search from the paired bracket ends to
+    |f| < tau, with the first search point evaluated alone (pair_h None, the kernel) or together
+    with a second point pair_h degrees above it (both in one paired evaluation), the search then
+    stepping by IQI through the last three points; None when the ends do not bracket a root."""
+    fL, fR = f(lo), f(hi)
+    if not (math.isfinite(fL) and math.isfinite(fR)) or (fL < 0) == (fR < 0) or \
+            abs(fL) < tau or abs(fR) < tau:
+        return None
+    trips = 1.3
+    ul, uh = f32(math.tan(f32((180 - lo) * D2R))), f32(math.tan(f32((180 - hi) * D2R)))
+    un = f32(uh - f32(fR) * f32(f32(uh - ul) / f32(fR - fL)))
+    x2 = 180 - math.atan(un) * R2D
+    pts = [(lo, fL), (hi, fR)]
+    if pair_h is None:
+        fa = f(x2)
+        trips += 1
+        pts.append((x2, fa))
+        if abs(fa) < tau:
+            return trips
+    else:
+        fa, fb = f(x2), f(x2 + pair_h)
+        trips += 1.3
+        pts += [(x2, fa), (x2 + pair_h, fb)]
+        if abs(fa) < tau or abs(fb) < tau:
+            return trips
+    for _ in range(12):
+        (xA, fA), (xB, fB), (xC, fC) = pts[-3:]
+        x = xC - fC * (xC - xB) / (fC - fB)
+        d1 = (xC - xB) / (fC - fB)
+        d0 = (xB - xA) / (fB - fA)
+        x += fB * fC * ((d1 - d0) / (fC - fA))
+        v = f(x)
+        trips += 1
+        pts.append((x, v))
+        if not math.isfinite(v) or abs(v) < tau:
+            break
+    return trips
+
+
+def main_pair(n):
+    m = oracle.load_atmosphere(os.path.join(ROOT, "airiceraytracing_amd", "data",
+                                            "Atmosphere.dat.gz"))
+    txh, dst, dep = cfg3_queries(4 * n, seed=2024)
+    hs = (None, 1e-5, 1e-4, 1e-3, 1e-2)
+    res = {h: [] for h in hs}
+    k = 0
+    for i in range(len(txh)):
+        H, D, d = txh[i], dst[i], dep[i]
+        thR = oracle.straight_angle_of(m, H, D, 3000.0, d)
+        lo, hi = thR - 16, thR
+        if lo < 90.001:
+            continue
+
+        def f(t):
+            return D - oracle.ray_solution(m, t, H, 3000.0, d)[2]
+
+        tau = 1e-6 + 1e-10 * abs(D)
+        out = {h: paired_first_trips(f, lo, hi, tau, h) for h in hs}
+        if any(v is None for v in out.values()):
+            continue
+        for h, v in out.items():
+            res[h].append(v)
+        k += 1
+        if k >= n:
+            break
+    for h, v in res.items():
+        print(f"first point {'alone' if h is None else f'paired, +{h} deg'}: {np.mean(v):.3f} "
+              f"trips per solve (p90 {np.percentile(v, 90):.2f}, max {max(v):.1f})")
+
+
 def main():
+    if len(sys.argv) > 1 and sys.argv[1] == "--pair":
+        main_pair(int(sys.argv[2]) if len(sys.argv) > 2 else 300)
+        return
     n = int(sys.argv[1]) if len(sys.argv) > 1 else 300
     m = oracle.load_atmosphere(os.path.join(ROOT, "airiceraytracing_amd", "data",
                                             "Atmosphere.dat.gz"))
